@@ -1,0 +1,114 @@
+"""ctypes binding of the amx C ABI (include/amx_hip.h).
+
+The product path goes through these bindings only: there is no CPU or eager-PyTorch
+fallback for any hot-path op.  If the library is missing or cannot be loaded, every op
+raises `AmxNativeError` — loudly, on purpose.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+from . import _build
+
+_HEADER = os.path.join(_build.INCLUDE, "amx_hip.h")
+
+c_int, c_ll, c_dbl, c_flt, c_u64, c_u32, vp = C.c_int, C.c_longlong, C.c_double, C.c_float, C.c_uint64, C.c_uint32, C.c_void_p
+ip = C.POINTER(C.c_int)
+
+# name -> (restype, argtypes); must match include/amx_hip.h exactly.
+SIGNATURES = {
+    "amx_create": (vp, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    "amx_destroy": (c_int, [vp]),
+    "amx_last_error": (C.c_char_p, []),
+    "amx_abi_version": (c_int, []),
+    "amx_layout": (c_int, [vp, ip, ip, ip, ip]),
+    "amx_set_normalizers": (c_int, [vp, vp, vp, vp, vp, vp, vp]),
+    "amx_set_termination": (c_int, [vp, c_int, vp, vp, vp, vp, c_int, c_int, c_int, c_int, c_int,
+                                    c_int, c_int, c_dbl, c_int, c_dbl]),
+    "amx_assemble_input": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp]),
+    "amx_gemm_bias_act": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
+                                  vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp]),
+    "amx_gemm_out_unnorm": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
+                                    vp, c_ll, vp, c_int, c_ll, vp]),
+    "amx_step": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_int, vp]),
+    "amx_disagreement": (c_int, [vp, vp, c_int, c_ll, vp, c_int, vp]),
+    "amx_reset_lanes": (c_int, [vp, vp, vp, c_int, vp, c_u64, vp, vp, vp, vp, vp, vp, c_int, vp]),
+    "amx_policy_act": (c_int, [vp, vp, c_int, vp, vp, c_int, vp, vp, c_int, vp, vp, vp, vp, c_u64, c_u64,
+                               c_int, vp, vp, vp]),
+    "amx_rff_features": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_flt, vp, c_int,
+                                 vp, vp, vp]),
+    "amx_sum_partials": (c_int, [vp, vp, c_int, c_int, vp, vp]),
+    "amx_mmd_fit": (c_int, [vp, vp, c_dbl, vp, c_int, vp, vp, vp]),
+    "amx_mmd_reward": (c_int, [vp, vp, c_int, vp, c_int, vp, c_flt, c_dbl, c_flt, c_flt, vp, vp, vp, c_int, vp]),
+    "amx_expert_cost": (c_int, [vp, vp, c_int, vp, c_int, c_int, c_flt, c_flt, vp, vp]),
+    "amx_amp_reward": (c_int, [vp, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
+    "amx_philox": (c_int, [vp, c_u64, c_u32, c_u32, c_u32, vp, c_int, vp]),
+}
+
+AMX_ROW_TILE = 128
+AMX_K_TILE = 32
+AMX_SHAPE_SPHERE, AMX_SHAPE_CAPSULE, AMX_SHAPE_BOX = 0, 1, 2
+AMX_ACT_NONE, AMX_ACT_RELU = 0, 1
+AMX_IN_F64, AMX_IN_F32 = 0, 1
+
+
+class AmxNativeError(RuntimeError):
+    pass
+
+
+def header_symbols(path: str = _HEADER) -> list[str]:
+    """Every function the public header declares (used by the export test)."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(amx_[a-z0-9_]+)\s*\(", txt)))
+
+
+_LIB = None
+
+
+def load(path: str | None = None, build_if_missing: bool = False):
+    """Load libamx_hip.so and bind signatures.  Never falls back to anything else."""
+    global _LIB
+    if _LIB is not None and path is None:
+        return _LIB
+    path = path or _build.LIB_PATH
+    if not os.path.exists(path):
+        if build_if_missing:
+            _build.build()
+        else:
+            raise AmxNativeError(
+                f"{path} is missing: build it with `python -m amp_extensions_amd._build` "
+                "(there is no CPU fallback for the rollout hot path)")
+    try:
+        lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    except OSError as e:
+        raise AmxNativeError(f"cannot load {path}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.amx_abi_version() != 1:
+        raise AmxNativeError("libamx_hip ABI version mismatch")
+    if path == _build.LIB_PATH:
+        _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = _LIB.amx_last_error().decode() if _LIB is not None else "?"
+        raise AmxNativeError(f"{what or 'amx call'} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,207 @@
+// Reward kernels of the relabel block (mjrl/mjrl/algos/batch_reinforce.py:103-169):
+// ordered fp64 reduction of the RFF feature-sum partials, the closed-form MMD witness
+// (RBFLinearCost.fit_cost), the per-sample pessimistic MMD reward (get_costs +
+// get_bonus_costs), the expert cost, and the AMP least-squares discriminator reward.
+//
+// All are HBM-bound streaming passes over per-sample rows (phi rows are 2 KB); one wave
+// per row, float4 loads, fp64 wave reductions.  Built with -ffp-contract=off so the
+// scalar reward algebra rounds exactly like the reference's separate torch fp32 ops.
+#include "amx_common.h"
+
+namespace {
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// out[f] = sum_p partials[p][f] in ascending p (deterministic).
+__global__ __launch_bounds__(256) void k_sum_partials(const double* __restrict__ partials, int n_parts, int F,
+                                                      double* __restrict__ out) {
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  double s = 0.0;
+  for (int p = 0; p < n_parts; ++p) s += partials[(long long)p * F + f];
+  out[f] = s;
+}
+
+// w = (float)(sum/count) - phi_e ; mmd = dot(w, w).  One block; F <= 4096.
+__global__ __launch_bounds__(256) void k_mmd_fit(const double* __restrict__ phi_sum, double count,
+                                                 const float* __restrict__ phi_e, int F, float* __restrict__ w,
+                                                 float* __restrict__ mmd) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (int f = threadIdx.x; f < F; f += blockDim.x) {
+    const float mean = (float)(phi_sum[f] / count);
+    const float wf = mean - phi_e[f];
+    w[f] = wf;
+    acc += (double)wf * (double)wf;
+  }
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *mmd = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+// dot(phi[row], w) over F (F % 256 == 0 handled by float4 x 64 lanes per 256 floats)
+__device__ inline double row_dot(const float* __restrict__ row, const float* __restrict__ w, int F, int lane) {
+  double s = 0.0;
+  for (int f = lane * 4; f < F; f += 256) {
+    const float4 p = *reinterpret_cast<const float4*>(row + f);
+    const float4 q = *reinterpret_cast<const float4*>(w + f);
+    s += (double)p.x * q.x + (double)p.y * q.y + (double)p.z * q.z + (double)p.w * q.w;
+  }
+  return wave_sum(s);
+}
+
+__device__ inline float clampf_ref(float v, float lo, float hi) {
+  // torch.clamp(min, max): min first, then max; NaN propagates
+  if (v != v) return v;
+  v = v < lo ? lo : v;
+  return v > hi ? hi : v;
+}
+
+__global__ __launch_bounds__(256) void k_mmd_reward(const float* __restrict__ phi, int ldphi,
+                                                    const float* __restrict__ w, int F,
+                                                    const float* __restrict__ disc, float thr, float one_m_lambda,
+                                                    float lambda_b, float c_min, float c_max,
+                                                    float* __restrict__ reward, float* __restrict__ ipm_out,
+                                                    float* __restrict__ wb_out, int n) {
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  const double dot = row_dot(phi + (long long)r * ldphi, w, F, lane);
+  if (lane != 0) return;
+  const float v = clampf_ref((float)dot, c_min, c_max);       // linear_cost.py:102
+  float dh = disc[r] / thr;                                    // :132
+  if (dh > 1.0f) dh = 1.0f;                                    // :134
+  const float bonus = dh * c_min;                              // :136
+  const float ipm = one_m_lambda * v;                          // :141  (1-lambda)*rff_cost
+  const float wb = lambda_b * bonus;                           // :144
+  const float cost = ipm - wb;                                 // :147
+  reward[r] = -1.0f * cost;                                    // batch_reinforce.py:144
+  if (ipm_out) ipm_out[r] = ipm;
+  if (wb_out) wb_out[r] = wb;
+}
+
+// Block partial of sum clamp(phi_E[r].w): 4 rows per block-iteration (one per wave),
+// grid-stride; partials[block] in fp64, then an ordered sum.
+__global__ __launch_bounds__(256) void k_expert_cost(const float* __restrict__ phi, int ldphi,
+                                                     const float* __restrict__ w, int F, int n, float c_min,
+                                                     float c_max, double* __restrict__ partials) {
+  __shared__ double red[4];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double acc = 0.0;
+  for (int r = blockIdx.x * 4 + wave; r < n; r += gridDim.x * 4) {
+    const double dot = row_dot(phi + (long long)r * ldphi, w, F, lane);
+    acc += (double)clampf_ref((float)dot, c_min, c_max);
+  }
+  if (lane == 0) red[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void k_sum_small(const double* __restrict__ partials, int n, double* __restrict__ out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += partials[i];
+    out[0] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_amp_reward(const float* __restrict__ h, int ldh, int Hd,
+                                                    const float* __restrict__ w3, float b3,
+                                                    const float* __restrict__ disc, float one_m_lambda,
+                                                    float lambda_b, float* __restrict__ reward,
+                                                    float* __restrict__ logits, int n) {
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (r >= n) return;
+  double s = 0.0;
+  const float* row = h + (long long)r * ldh;
+  for (int k = lane; k < Hd; k += 64) s += (double)row[k] * (double)w3[k];
+  s = wave_sum(s);
+  if (lane != 0) return;
+  const float D = (float)s + b3;                     // Discriminator last nn.Linear
+  const float om = 1.0f - D;                         // gail_cost.py:234  1.0 - disc_outs
+  const float sq = om * om;                          //                   (.)**2
+  const float q = 0.25f * sq;                        //                   0.25 * (.)
+  float rew = 1.0f - q;                              //                   1.0 - (.)
+  if (rew < 0.0f) rew = 0.0f;                        // :235
+  if (logits) logits[r] = D;
+  if (disc == nullptr) {                             // get_costs path: reward = -cost = r
+    reward[r] = rew;
+    return;
+  }
+  const float input_cost = -rew;                     // :236
+  const float ipm = one_m_lambda * input_cost;       // :269
+  const float bonus = lambda_b * disc[r];            // :273 (raw disagreement)
+  const float cost = ipm - bonus;                    // :275
+  reward[r] = -1.0f * cost;                          // batch_reinforce.py:144
+}
+
+}  // namespace
+
+extern "C" int amx_sum_partials(amx_ctx* ctx, const double* partials, int n_parts, int F, double* out,
+                                void* stream) {
+  AMX_CHECK_ARG(ctx && partials && out && n_parts >= 0 && F > 0, "amx_sum_partials: bad argument");
+  hipLaunchKernelGGL(k_sum_partials, dim3((F + 255) / 256), dim3(256), 0, (hipStream_t)stream, partials, n_parts,
+                     F, out);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_mmd_fit(amx_ctx* ctx, const double* phi_sum, double count, const float* phi_e, int F,
+                           float* w, float* mmd, void* stream) {
+  AMX_CHECK_ARG(ctx && phi_sum && phi_e && w && mmd && F > 0, "amx_mmd_fit: bad argument");
+  AMX_CHECK_ARG(count > 0.0, "amx_mmd_fit: count must be positive (empty rollout)");
+  hipLaunchKernelGGL(k_mmd_fit, dim3(1), dim3(256), 0, (hipStream_t)stream, phi_sum, count, phi_e, F, w, mmd);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_mmd_reward(amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
+                              float thr, double lambda_b, float c_min, float c_max, float* reward, float* ipm,
+                              float* wbonus, int n, void* stream) {
+  AMX_CHECK_ARG(ctx && phi && w && disc && reward, "amx_mmd_reward: null pointer");
+  AMX_CHECK_ARG(F > 0 && F % 256 == 0 && ldphi >= F && ldphi % 4 == 0, "amx_mmd_reward: F=%d ldphi=%d", F, ldphi);
+  AMX_CHECK_ARG(amx::aligned16(phi) && amx::aligned16(w), "amx_mmd_reward: phi/w must be 16-byte aligned");
+  AMX_CHECK_ARG(n >= 0, "amx_mmd_reward: n=%d", n);
+  if (n == 0) return AMX_OK;
+  // lambda is a Python double in the reference: (1 - lambda) is formed in double, then
+  // torch rounds each scalar to float32 for the fp32 kernel (linear_cost.py:141,144).
+  const float one_m_lambda = (float)(1.0 - lambda_b);
+  hipLaunchKernelGGL(k_mmd_reward, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, phi, ldphi, w, F, disc,
+                     thr, one_m_lambda, (float)lambda_b, c_min, c_max, reward, ipm, wbonus, n);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
+                               float c_min, float c_max, double* out, void* stream) {
+  AMX_CHECK_ARG(ctx && phi_e_rows && w && out, "amx_expert_cost: null pointer");
+  AMX_CHECK_ARG(F > 0 && F % 256 == 0 && ldphi >= F && ldphi % 4 == 0, "amx_expert_cost: F=%d ldphi=%d", F, ldphi);
+  AMX_CHECK_ARG(n > 0, "amx_expert_cost: n=%d", n);
+  // partials live in out[1 .. nb]; out must hold 1 + 1024 doubles
+  const int nb = (n + 3) / 4 < 1024 ? (n + 3) / 4 : 1024;
+  hipLaunchKernelGGL(k_expert_cost, dim3(nb), dim3(256), 0, (hipStream_t)stream, phi_e_rows, ldphi, w, F, n, c_min,
+                     c_max, out + 1);
+  AMX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_sum_small, dim3(1), dim3(64), 0, (hipStream_t)stream, out + 1, nb, out);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_amp_reward(amx_ctx* ctx, const float* h, int ldh, int Hd, const float* w3, float b3,
+                              const float* disc, double lambda_b, float* reward, float* logits, int n,
+                              void* stream) {
+  AMX_CHECK_ARG(ctx && h && w3 && reward, "amx_amp_reward: null pointer");
+  AMX_CHECK_ARG(Hd > 0 && ldh >= Hd && n >= 0, "amx_amp_reward: Hd=%d ldh=%d n=%d", Hd, ldh, n);
+  if (n == 0) return AMX_OK;
+  const float one_m_lambda = (float)(1.0 - lambda_b);
+  hipLaunchKernelGGL(k_amp_reward, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, Hd, w3, b3, disc,
+                     one_m_lambda, (float)lambda_b, reward, logits, n);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}

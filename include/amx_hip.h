@@ -1,0 +1,223 @@
+/*
+ * amx_hip.h — C ABI of the MI355X-native learned-dynamics rollout engine.
+ *
+ * This is the drop-in boundary for ONE hot path of dhruvsreenivas/amp_extensions:
+ * the gym_simenv learned-dynamics step (4-model dense-MLP ensemble), the MILO
+ * random-Fourier-feature MMD cost + ensemble-disagreement bonus, the AMP/GAIL
+ * least-squares discriminator reward and the humanoid3d fall/horizon termination.
+ * Each entry point names the reference interface it replaces (paths relative to
+ * the reference repository root).
+ *
+ * Conventions
+ *   - Every buffer argument is a DEVICE pointer owned by the caller, except where a
+ *     comment says "host".  Nothing is retained after a call returns, except the
+ *     small configuration copied by amx_set_* into context-owned device memory.
+ *   - Every launching call takes a hipStream_t (passed as void* so this header
+ *     needs no HIP include) and is asynchronous on it.  No call allocates, frees
+ *     or synchronises on the launch path, so a caller may capture them in a graph.
+ *   - Return value: AMX_OK (0) or a negative AMX_E_* code.  No exception crosses
+ *     the ABI.  amx_last_error() returns a thread-local message for the last
+ *     failing call on the calling thread.
+ *   - Thread safety: one amx_ctx per device; calls on one context are not
+ *     re-entrant; distinct contexts/devices are independent.
+ *   - Row padding: GEMM operands/outputs have a row count that is a multiple of
+ *     AMX_ROW_TILE (128); K of every GEMM is a multiple of AMX_K_TILE (32); leading
+ *     dimensions are multiples of 4 floats; pointers are 16-byte aligned.
+ *     amx_layout() reports the padded widths the engine expects.
+ */
+#ifndef AMX_HIP_H
+#define AMX_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMX_ABI_VERSION 1
+#define AMX_ROW_TILE 128
+#define AMX_K_TILE 32
+#define AMX_MAX_MODELS 8
+#define AMX_MAX_BODIES 32
+
+enum {
+  AMX_OK = 0,
+  AMX_E_INVAL = -1,   /* bad argument (shape, alignment, null pointer) */
+  AMX_E_HIP = -2,     /* HIP runtime error (launch, memcpy) */
+  AMX_E_NOMEM = -3,   /* device allocation failed */
+  AMX_E_STATE = -4    /* context not configured for this call */
+};
+
+enum { AMX_SHAPE_SPHERE = 0, AMX_SHAPE_CAPSULE = 1, AMX_SHAPE_BOX = 2 };
+enum { AMX_ACT_NONE = 0, AMX_ACT_RELU = 1 };
+enum { AMX_IN_F64 = 0, AMX_IN_F32 = 1 };
+
+typedef struct amx_ctx amx_ctx;
+
+/* ---- context ------------------------------------------------------------------ */
+
+/* Replaces the sizes SimEnv/DynamicsEnsemble read at construction:
+ * gym-simenv/gym_simenv/envs/sim_env.py:66-67 (state/action size),
+ * milo/milo/dynamics.py:19-79 (num_models, hidden_sizes) and
+ * milo/milo/linear_cost.py:23-62 (feature_dim).  n_hidden hidden layers of width
+ * `hidden`, dense-connected (BasicMLP, milo/milo/dynamics.py:394-433). */
+amx_ctx* amx_create(int device, int S, int A, int n_models, int hidden, int n_hidden, int feat_dim);
+int amx_destroy(amx_ctx* ctx);
+const char* amx_last_error(void);
+int amx_abi_version(void);
+
+/* Padded layout the engine expects (host outputs):
+ *   k0_pad   = round_up(S + A, 32)   width of the [s~, a~] block of the activation row
+ *   ldk      = k0_pad + n_hidden*hidden  activation row length (dense-concat buffer)
+ *   n_out_pad= round_up(S, 128)      output rows of the padded last-layer weight
+ *   k_rff_pad= round_up(2*S, 32)     width of the float32 [s, s'] cost input row   */
+int amx_layout(const amx_ctx* ctx, int* k0_pad, int* ldk, int* n_out_pad, int* k_rff_pad);
+
+/* Normalizers (host pointers, copied).  Contract of AmpDataset.get_transformations,
+ * milo/milo/datasets.py:23-43: means and mean-absolute-deviation+1e-8 scales, in
+ * the order DynamicsModel.forward consumes them (milo/milo/dynamics.py:225-232). */
+int amx_set_normalizers(amx_ctx* ctx, const float* mu_s, const float* sd_s, const float* mu_a,
+                        const float* sd_a, const float* mu_d, const float* sd_d);
+
+/* Fall-termination configuration (host pointers, copied).  Replaces SimEnv.__init__'s
+ * fall-body tables and ctrl flags, gym-simenv/gym_simenv/envs/sim_env.py:83-115, and
+ * is_done/check_velocity's parameters, :164-173, :259-268.  body_id[i] is the
+ * character body index; p0/p1 are BodyDefs Param0/Param1 (radius = 0.5*p0, capsule
+ * height = p1).  pos_dim/rot_dim: per-body pose feature widths (3 and 6). */
+int amx_set_termination(amx_ctx* ctx, int n_bodies, const int32_t* body_id, const int32_t* shape,
+                        const double* p0, const double* p1, int record_all_world,
+                        int record_world_root_pos, int pos_dim, int rot_dim, int horizon,
+                        int vel_check, int vel_offset, double vel_thresh, int record_vel_as_pos,
+                        double sampling_rate);
+
+/* ---- ensemble forward --------------------------------------------------------- */
+
+/* State assembly for DynamicsModel.forward, milo/milo/dynamics.py:216-230:
+ * x0 = [(float(s)-mu_s)/sd_s, (float(a)-mu_a)/sd_a, 0-pad] written at column 0 of
+ * every model's activation row (act_buf[m][b][0:k0_pad], m < n_models).
+ * in_dtype = AMX_IN_F64 (SimEnv's float64 ob, sim_env.py:155-156) or AMX_IN_F32. */
+int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
+                       long long stride_m, int ldk, int B, void* stream);
+
+/* Grouped fp32 GEMM on MFMA with fused bias (+ReLU) epilogue: for g < groups,
+ * C_g[r][col_off + n] = act(sum_k A_g[r][k] * W_g[n][k] + bias_g[n]).
+ * One dense-connect hidden layer of all ensemble members at once
+ * (BasicMLP.forward, milo/milo/dynamics.py:427-430: relu(fc(x)); x = cat[x, h]);
+ * also the Discriminator hidden layers, milo/milo/gail_cost.py:18-42.
+ * rows % 128 == 0, N % 128 == 0, K % 32 == 0. */
+int amx_gemm_bias_act(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
+                      long long strideA, const float* W, int ldw, long long strideW,
+                      const float* bias, long long strideBias, float* C, int ldc, long long strideC,
+                      int col_off, int act, void* stream);
+
+/* Last dense layer + output un-normalisation (BasicMLP.forward :432 then
+ * DynamicsModel.forward :231-232): preds_g[r][n] = (sum_k A W + b[n]) * sd_d[n] + mu_d[n]
+ * for n < n_valid (=S); W_g is padded to round_up(n_valid,128) rows. */
+int amx_gemm_out_unnorm(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
+                        int lda, long long strideA, const float* W, int ldw, long long strideW,
+                        const float* bias, long long strideBias, float* preds, int ldp,
+                        long long strideP, void* stream);
+
+/* ---- step + termination ------------------------------------------------------- */
+
+/* One batched SimEnv.step after the forward (gym-simenv/gym_simenv/envs/sim_env.py:140-173):
+ * num_steps[b] += 1; ob_next[b] = ob[b] + (double)preds[model_idx[b]][b] (fp64 state,
+ * fp32 model, :158); done[b] = horizon | check_collision | check_velocity (:164-268),
+ * bit-exact fp64 comparisons.  Fused extras (nullable):
+ *   disc[b]   = max over model pairs of ||preds_i - preds_j||_2 (compute_discrepancy,
+ *               milo/milo/dynamics.py:134-143) — reuses the step's own forward;
+ *   cost_in   = float32 [ob, ob_next] rows, ld = ldc (the 'ss' cost input,
+ *               mjrl/mjrl/algos/batch_reinforce.py:107-113);
+ *   nonfinite[b] = 1 if ob_next holds a NaN/Inf (diagnostic only; done unchanged). */
+int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
+             const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+             float* cost_in, int ldc, uint8_t* nonfinite, int B, void* stream);
+
+/* Disagreement only (DynamicsEnsemble.get_action_discrepancy / compute_threshold,
+ * milo/milo/dynamics.py:145-165). */
+int amx_disagreement(amx_ctx* ctx, const float* preds, int ldp, long long strideP, float* disc,
+                     int B, void* stream);
+
+/* SimEnv.reset for masked lanes (gym-simenv/gym_simenv/envs/sim_env.py:270-285), with
+ * the DeepMimicCore pose replaced by a row of a device reset-state table (documented
+ * deviation).  For every lane b with mask[b] != 0 (mask NULL = all lanes):
+ *   reset_count[b] += 1; model_idx[b] = reset_count[b] % n_models; num_steps[b] = 0;
+ *   row = rows ? rows[b] : philox(seed, b, reset_count[b]) mod R; ob_out[b] = table[row].
+ * Lanes with mask 0 copy ob_src[b] into ob_out[b] (carry; ob_src may equal ob_out).
+ * row_out (nullable) receives the chosen row (-1 for carried lanes). */
+int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* table, int R,
+                    const int32_t* rows, uint64_t seed, const double* ob_src, double* ob_out,
+                    int32_t* num_steps, int32_t* model_idx, int32_t* reset_count, int32_t* row_out,
+                    int B, void* stream);
+
+/* ---- device policy ------------------------------------------------------------ */
+
+/* mjrl Gaussian MLP policy action (mjrl/mjrl/policies/gaussian_mlp.py:95-104 over
+ * FCNetwork tanh, mjrl/mjrl/utils/fc_network.py:42-55), two hidden layers:
+ *   mean = W3 tanh(W2 tanh(W1 float(ob) + b1) + b2) + b3   (float32)
+ *   act  = (double)mean + noise_scale * n,  n ~ N(0,1) fp64 (philox(seed, b, counter)
+ *          Box-Muller) or injected noise[b][A] (nullable).  eval_mode: act = mean.
+ * noise_scale = exp(log_std) in fp64 (host pointer not allowed: device, [A]). */
+int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* W1, const float* b1, int H1,
+                   const float* W2, const float* b2, int H2, const float* W3, const float* b3,
+                   const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
+                   int eval_mode, double* act, float* mean, void* stream);
+
+/* ---- MILO RFF MMD cost -------------------------------------------------------- */
+
+/* RBFLinearCost.get_rep (milo/milo/linear_cost.py:64-71) on MFMA:
+ * phi[r][f] = cos(sum_k x[r][k] W[f][k] + b[f]) * scale, scale = (float)sqrt(2/F),
+ * plus fp64 column sums of the tile's valid rows (r < n_valid and (row_mask==NULL or
+ * row_mask[r])) into col_partials[r/128][f] — the per-rank share of the global
+ * feature mean of fit_cost (:84-94).  rows % 128 == 0, F % 128 == 0. */
+int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
+                     const float* W, int ldw, const float* b, float scale, float* phi, int ldphi,
+                     double* col_partials, const uint8_t* row_mask, void* stream);
+
+/* Deterministic ordered sum of n_parts rows of fp64 partials -> out[F] (fp64). */
+int amx_sum_partials(amx_ctx* ctx, const double* partials, int n_parts, int F, double* out,
+                     void* stream);
+
+/* fit_cost closed form (milo/milo/linear_cost.py:84-94) after the cross-rank sum:
+ * phi_pi = (float)(phi_sum / count); w = phi_pi - phi_e; mmd[0] = dot(w, w) (fp32). */
+int amx_mmd_fit(amx_ctx* ctx, const double* phi_sum, double count, const float* phi_e, int F,
+                float* w, float* mmd, void* stream);
+
+/* Per-sample MILO reward with pessimism (RBFLinearCost.get_costs + get_bonus_costs,
+ * milo/milo/linear_cost.py:96-103, 111-152; reward = -cost, batch_reinforce.py:144):
+ *   v = clamp(phi[n].w, c_min, c_max); dh = min(disc[n]/thr, 1); bonus = dh*c_min;
+ *   ipm = (1-lambda)*v; wb = lambda*bonus; reward = -(ipm - wb).
+ * ipm/wbonus outputs are nullable (info['ipm'], info['bonus']). */
+int amx_mmd_reward(amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
+                   float thr, double lambda_b, float c_min, float c_max, float* reward, float* ipm,
+                   float* wbonus, int n, void* stream);
+
+/* get_expert_cost (milo/milo/linear_cost.py:105-109): partial fp64 sums over row
+ * blocks of clamp(phi_E[r].w, c_min, c_max); out[0] = sum (fp64), caller scales by
+ * (1-lambda)/N_e.  Uses the resident expert features. */
+int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
+                    float c_min, float c_max, double* out, void* stream);
+
+/* ---- AMP / GAIL least-squares discriminator reward ---------------------------- */
+
+/* Last Discriminator layer (512->1, milo/milo/gail_cost.py:18-42) fused with
+ * get_ls_costs (:231-236) and get_bonus_costs (:254-279):
+ *   D = h[n].w3 + b3; r = max(0, 1 - 0.25*(1-D)^2); ipm = (1-lambda)*(-r);
+ *   bonus = lambda*disc[n] (raw disagreement); reward = -(ipm - bonus).
+ * disc NULL -> plain get_costs path: reward = r. logits (nullable) receives D. */
+int amx_amp_reward(amx_ctx* ctx, const float* h, int ldh, int Hd, const float* w3, float b3,
+                   const float* disc, double lambda_b, float* reward, float* logits, int n,
+                   void* stream);
+
+/* ---- RNG ----------------------------------------------------------------------- */
+
+/* Philox4x32-10 block for (key = seed, counter = {ctr0, ctr1, ctr2, ctr3}), written
+ * to out[4*i .. 4*i+3] for i < n with ctr0 += i.  Exposed for parity tests of the
+ * device RNG the reset/policy kernels use. */
+int amx_philox(amx_ctx* ctx, uint64_t seed, uint32_t ctr1, uint32_t ctr2, uint32_t ctr3,
+               uint32_t* out, int n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AMX_HIP_H */
