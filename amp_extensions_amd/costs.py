@@ -1,0 +1,253 @@
+"""Device-backed drop-ins for the reference cost objects.
+
+* `RBFLinearCost` — milo/milo/linear_cost.py:6-152 (MILO RFF MMD cost + pessimism bonus)
+* `GAILCost`      — milo/milo/gail_cost.py:44-279, inference surface (AMP least-squares
+                    discriminator reward + bonus); discriminator training is out of scope.
+
+Initialisation reproduces the reference's torch-CPU RNG stream exactly (seed, bandwidth
+draw, nn.Linear construction order), so the same seed yields the same W, b, bandwidth and
+discriminator weights; every per-sample computation then runs in the HIP kernels with the
+expert features resident in HBM.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from .engine import AmxContext, RffMap, round_up
+
+
+class RBFLinearCost:
+    """MMD cost with random-Fourier-feature representations (linear_cost.py:6-152).
+
+    Same constructor arguments and methods as the reference; tensors returned by the
+    cost methods live on the engine's device.
+    """
+
+    def __init__(self, expert_data: torch.Tensor, feature_dim=1024, input_type="ss", cost_range=(-1.0, 0.0),
+                 bw_quantile=0.1, bw_samples=100000, lambda_b=1.0, lr=0.0, seed=100, ctx: AmxContext | None = None,
+                 device="cuda"):
+        torch.manual_seed(seed)          # linear_cost.py:34-35
+        np.random.seed(seed)
+        expert_cpu = expert_data.detach().float().cpu()
+        input_dim = expert_cpu.size(1)
+        self.input_type = input_type
+        self.feature_dim = feature_dim
+        self.cost_range = cost_range
+        if cost_range is not None:
+            self.c_min, self.c_max = float(cost_range[0]), float(cost_range[1])
+        else:
+            raise NotImplementedError("cost_range=None (unclamped cost) is not on the MILO path")
+        self.lambda_b = float(lambda_b)
+        self.lr = lr
+        self.quantile = bw_quantile
+        self.bw_samples = bw_samples
+        self.bw = self.fit_bandwidth(expert_cpu)                  # :50 (torch-CPU RNG order)
+        rff = nn.Linear(input_dim, feature_dim)                   # :53
+        rff.bias.data = (torch.rand_like(rff.bias.data) - 0.5) * 2.0 * np.pi          # :54
+        rff.weight.data = torch.rand_like(rff.weight.data) / (self.bw + 1e-8)          # :55
+        self.rff_weight, self.rff_bias = rff.weight.data, rff.bias.data
+        if ctx is None:
+            S = input_dim // 2 if input_type == "ss" else input_dim
+            ctx = AmxContext(S, 1, n_models=1, hidden=128, n_hidden=0, feat_dim=feature_dim, device=device)
+        self.ctx = ctx
+        self.map = RffMap(ctx, self.rff_weight, self.rff_bias)
+        self.w = None
+        # expert features resident in HBM (:61-62); phi_e from fp64 column sums
+        phi, tot = self.map.embed(expert_cpu)
+        self.expert_rep = phi
+        self.n_expert = expert_cpu.shape[0]
+        self.phi_e = (tot / self.n_expert).float()
+        self._expert_out = torch.empty(1 + 1024, dtype=torch.float64, device=ctx.device)
+
+    # linear_cost.py:73-82
+    def fit_bandwidth(self, data: torch.Tensor) -> float:
+        n = data.shape[0]
+        i0 = torch.randint(low=0, high=n, size=(self.bw_samples,))
+        i1 = torch.randint(low=0, high=n, size=(self.bw_samples,))
+        norm = torch.norm(data[i0, :] - data[i1, :], dim=1)
+        return torch.quantile(norm, q=self.quantile).item()
+
+    def get_rep(self, x: torch.Tensor) -> torch.Tensor:
+        """linear_cost.py:64-71."""
+        return self.map.embed(x)[0]
+
+    def fit_w(self, phi_sum: torch.Tensor, count: float) -> float:
+        """Closed-form witness from an (already all-reduced) fp64 feature sum."""
+        c = self.ctx
+        self.w = torch.empty(self.feature_dim, dtype=torch.float32, device=c.device)
+        mmd = torch.empty(1, dtype=torch.float32, device=c.device)
+        N.check(c.lib.amx_mmd_fit(c.h, phi_sum.data_ptr(), float(count), self.phi_e.data_ptr(), self.feature_dim,
+                                  self.w.data_ptr(), mmd.data_ptr(), c.stream), "amx_mmd_fit")
+        return float(mmd.item())
+
+    def fit_cost(self, data_pi: torch.Tensor) -> float:
+        """linear_cost.py:84-94: w = mean phi(data_pi) - phi_e; returns w.w."""
+        _, tot = self.map.embed(data_pi)
+        return self.fit_w(tot, data_pi.shape[0])
+
+    def _values(self, phi: torch.Tensor, disc: torch.Tensor, thr: float):
+        c = self.ctx
+        n = phi.shape[0]
+        reward = torch.empty(n, dtype=torch.float32, device=c.device)
+        ipm = torch.empty(n, dtype=torch.float32, device=c.device)
+        wb = torch.empty(n, dtype=torch.float32, device=c.device)
+        N.check(c.lib.amx_mmd_reward(c.h, phi.data_ptr(), phi.stride(0), self.w.data_ptr(), self.feature_dim,
+                                     disc.data_ptr(), float(thr), self.lambda_b, self.c_min, self.c_max,
+                                     reward.data_ptr(), ipm.data_ptr(), wb.data_ptr(), n, c.stream), "amx_mmd_reward")
+        return reward, ipm, wb
+
+    def get_costs(self, x: torch.Tensor) -> torch.Tensor:
+        """linear_cost.py:96-103: clamp(phi(x).w, c_min, c_max) [n, 1]."""
+        phi = self.get_rep(x)
+        n = phi.shape[0]
+        zeros = torch.zeros(n, dtype=torch.float32, device=self.ctx.device)
+        # with lambda = 0 the kernel's ipm output is exactly the clamped cost
+        lam, self.lambda_b = self.lambda_b, 0.0
+        try:
+            _, ipm, _ = self._values(phi, zeros, 1.0)
+        finally:
+            self.lambda_b = lam
+        return ipm.view(-1, 1)
+
+    def get_expert_cost(self) -> torch.Tensor:
+        """linear_cost.py:105-109 over the resident expert features."""
+        c = self.ctx
+        N.check(c.lib.amx_expert_cost(c.h, self.expert_rep.data_ptr(), self.expert_rep.stride(0), self.w.data_ptr(),
+                                      self.feature_dim, self.n_expert, self.c_min, self.c_max,
+                                      self._expert_out.data_ptr(), c.stream), "amx_expert_cost")
+        mean = (self._expert_out[0] / self.n_expert).float()
+        return np.float32(1 - self.lambda_b) * mean
+
+    def get_bonus_costs(self, states, actions, ensemble, next_states=None):
+        """linear_cost.py:111-152 (input_type 'ss'): cost [T, 1] and the info dict."""
+        if self.input_type != "ss":
+            raise NotImplementedError("only the 'ss' cost input of the MILO humanoid path is implemented")
+        assert next_states is not None
+        x = torch.cat([states.float(), next_states.float()], dim=1)
+        phi = self.get_rep(x)
+        disc = ensemble.get_action_discrepancy(states, actions)
+        reward, ipm, wb = self._values(phi, disc, ensemble.threshold)
+        cost = -reward
+        rff_cost = self.get_costs(x)
+        return cost.view(-1, 1), {"bonus": wb.view(-1, 1), "ipm": ipm.view(-1, 1), "v_targ": rff_cost,
+                                  "cost": cost.view(-1, 1)}
+
+
+class GAILCost:
+    """AMP/GAIL least-squares discriminator cost, inference surface (gail_cost.py:44-279)."""
+
+    def __init__(self, expert_data: torch.Tensor, agent_rb=None, feature_dim: int = 1, hidden_dims=(1024, 512),
+                 input_type: str = "ss", scaling_coef: float = 0.5, reg_coef: float = 0.05, lambda_b: float = 0.5,
+                 seed=100, grad_lambda=10.0, disc_loss_type="least_squares", disc_opt="sgd", disc_opt_args=None,
+                 ctx: AmxContext | None = None, device="cuda"):
+        if disc_loss_type != "least_squares":
+            raise NotImplementedError("only the least-squares (AMP) discriminator reward is on the hot path")
+        if feature_dim != 1:
+            raise ValueError("Discriminator output must be 1-D")
+        torch.manual_seed(seed)          # gail_cost.py:62-63
+        np.random.seed(seed)
+        self.expert_data = expert_data
+        self.input_dim = expert_data.size(1)
+        self.input_type = input_type
+        self.lambda_b = float(lambda_b)
+        self.disc_loss_type = disc_loss_type
+        sizes = [self.input_dim] + list(hidden_dims) + [1]
+        layers = [nn.Linear(sizes[i], sizes[i + 1]) for i in range(len(sizes) - 1)]   # Discriminator :28-37
+        for lin in layers:                                                             # disc_weight_init :11-16
+            if lin.out_features == 1:
+                nn.init.uniform_(lin.weight.data, a=-1.0, b=1.0)
+            else:
+                nn.init.xavier_uniform_(lin.weight.data)
+        self.weights = [(l.weight.data.clone(), l.bias.data.clone()) for l in layers]
+        if ctx is None:
+            S = self.input_dim // 2
+            ctx = AmxContext(S, 1, n_models=1, hidden=128, n_hidden=0, feat_dim=128, device=device)
+        self.ctx = ctx
+        self.load_weights(self.weights)
+
+    def load_weights(self, weights) -> None:
+        """Upload discriminator weights (e.g. after an out-of-scope training step)."""
+        dev = self.ctx.device
+        self.Kin = round_up(self.input_dim, 32)
+        self.dev_layers = []
+        k_in, k_pad = self.input_dim, self.Kin
+        for (W, b) in weights[:-1]:
+            out = W.shape[0]
+            out_p = round_up(out, 128)
+            Wp = torch.zeros(out_p, k_pad, dtype=torch.float32)
+            Wp[:out, :k_in] = W.float().cpu()
+            bp = torch.zeros(out_p, dtype=torch.float32)
+            bp[:out] = b.float().cpu()
+            self.dev_layers.append((Wp.to(dev).contiguous(), bp.to(dev).contiguous(), out_p, k_pad))
+            k_in, k_pad = out, out_p
+        W3, b3 = weights[-1]
+        w3 = torch.zeros(k_pad, dtype=torch.float32)
+        w3[:k_in] = W3.float().cpu().view(-1)
+        self.w3 = w3.to(dev).contiguous()
+        self.b3 = float(b3.float().cpu().view(-1)[0])
+        self.h_last = k_pad
+        self._ws = {}
+
+    def _hidden(self, x_pad: torch.Tensor, rows: int) -> torch.Tensor:
+        c = self.ctx
+        ws = self._ws.get(rows)
+        if ws is None:
+            ws = [torch.empty(rows, out_p, dtype=torch.float32, device=c.device) for (_, _, out_p, _) in self.dev_layers]
+            self._ws[rows] = ws
+        h = x_pad
+        for (Wp, bp, out_p, k_pad), o in zip(self.dev_layers, ws):
+            N.check(c.lib.amx_gemm_bias_act(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0, Wp.data_ptr(),
+                                            k_pad, 0, bp.data_ptr(), 0, o.data_ptr(), out_p, 0, 0, N.AMX_ACT_RELU,
+                                            c.stream), "amx_gemm_bias_act(disc)")
+            h = o
+        return h
+
+    def rewards_from_input(self, x_pad: torch.Tensor, rows: int, n: int, disc: torch.Tensor | None,
+                           out: torch.Tensor | None = None, logits: torch.Tensor | None = None) -> torch.Tensor:
+        """Fused discriminator + reward on already padded input rows [rows, Kin]."""
+        c = self.ctx
+        h = self._hidden(x_pad, rows)
+        out = torch.empty(n, dtype=torch.float32, device=c.device) if out is None else out
+        N.check(c.lib.amx_amp_reward(c.h, h.data_ptr(), h.stride(0), self.h_last, self.w3.data_ptr(), self.b3,
+                                     None if disc is None else disc.data_ptr(), self.lambda_b, out.data_ptr(),
+                                     None if logits is None else logits.data_ptr(), n, c.stream), "amx_amp_reward")
+        return out
+
+    def _pad(self, x: torch.Tensor):
+        n = x.shape[0]
+        rows = round_up(max(n, 1), 128)
+        xp = torch.zeros(rows, self.Kin, dtype=torch.float32, device=self.ctx.device)
+        xp[:n, :self.input_dim] = x.to(self.ctx.device, torch.float32)
+        return xp, rows, n
+
+    def disc_logits(self, ss: torch.Tensor) -> torch.Tensor:
+        xp, rows, n = self._pad(ss)
+        logits = torch.empty(n, dtype=torch.float32, device=self.ctx.device)
+        self.rewards_from_input(xp, rows, n, None, logits=logits)
+        return logits.view(-1, 1)
+
+    def get_ls_costs(self, ss: torch.Tensor) -> torch.Tensor:
+        """gail_cost.py:231-236: -max(0, 1 - 0.25 (1 - D)^2)  [n, 1]."""
+        xp, rows, n = self._pad(ss)
+        return (-self.rewards_from_input(xp, rows, n, None)).view(-1, 1)
+
+    def get_costs(self, ss: torch.Tensor) -> torch.Tensor:
+        return self.get_ls_costs(ss)
+
+    def get_bonus_costs(self, states, actions, ensemble, next_states=None):
+        """gail_cost.py:254-279 ('ss'): cost = (1-lambda) * ls_cost - lambda * disagreement."""
+        if self.input_type != "ss":
+            raise NotImplementedError("only the 'ss' input of the humanoid path is implemented")
+        x = torch.cat([states.float(), next_states.float()], dim=1)
+        xp, rows, n = self._pad(x)
+        disc = ensemble.get_action_discrepancy(states, actions)
+        reward = self.rewards_from_input(xp, rows, n, disc)
+        input_cost = self.get_ls_costs(x)
+        lam = np.float32(self.lambda_b)
+        ipm = np.float32(1 - self.lambda_b) * input_cost
+        bonus = lam * disc.view(-1, 1)
+        cost = (-reward).view(-1, 1)
+        return cost, {"bonus": bonus, "ipm": ipm, "v_targ": input_cost, "cost": cost}

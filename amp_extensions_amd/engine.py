@@ -1,0 +1,269 @@
+"""Device-resident building blocks over the amx C ABI: context, the dense-MLP ensemble,
+RFF features and the reward kernels.
+
+Layout in HBM (all fp32 unless noted; B_pad = round_up(B, 128)):
+  act   [M][B_pad][ldk]     dense-concat activation rows: [s~, a~, 0-pad | h0 | h1 | h2 | h3]
+                            (ldk = k0_pad + L*Hp; k0_pad = round_up(S+A, 32))
+  W_i   [M][Hp][k0_pad+i*Hp] hidden-layer weights re-indexed into that column layout
+  W_out [M][n_out_pad][ldk]  last layer, rows >= S zero
+  preds [M][B_pad][S]        un-normalised state deltas of every member
+Hidden widths that are not multiples of 128 are zero-padded (ReLU(0) = 0 keeps the pad
+inert), so any BasicMLP config runs on the same 128x128 MFMA tiles.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .humanoid import TerminationConfig
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class AmxContext:
+    """One amx_ctx per device (include/amx_hip.h)."""
+
+    def __init__(self, S: int, A: int, n_models: int = 4, hidden: int = 512, n_hidden: int = 4,
+                 feat_dim: int = 512, device: torch.device | str | int = "cuda"):
+        self.lib = N.load()
+        self.device = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+        if self.device.type != "cuda":
+            raise N.AmxNativeError("the amx engine runs on a ROCm GPU only (no CPU path)")
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", idx)
+        self.S, self.A, self.M = S, A, n_models
+        self.Hp = round_up(hidden, 128)
+        self.L = n_hidden
+        self.F = round_up(feat_dim, 128)
+        with torch.cuda.device(idx):
+            h = self.lib.amx_create(idx, S, A, n_models, self.Hp, n_hidden, self.F)
+        if not h:
+            raise N.AmxNativeError("amx_create failed: " + self.lib.amx_last_error().decode())
+        self.h = h
+        k0, ldk, nout, kr = (N.C.c_int(), N.C.c_int(), N.C.c_int(), N.C.c_int())
+        N.check(self.lib.amx_layout(h, N.C.byref(k0), N.C.byref(ldk), N.C.byref(nout), N.C.byref(kr)), "amx_layout")
+        self.k0_pad, self.ldk, self.n_out_pad, self.k_rff_pad = k0.value, ldk.value, nout.value, kr.value
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                self.lib.amx_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def set_normalizers(self, norms) -> None:
+        arrs = [np.ascontiguousarray(torch.as_tensor(x).detach().cpu().float().numpy()) for x in norms]
+        assert arrs[0].shape == (self.S,) and arrs[2].shape == (self.A,) and arrs[4].shape == (self.S,)
+        self._norm_host = arrs  # keep alive during the (synchronous) copy
+        N.check(self.lib.amx_set_normalizers(self.h, *[a.ctypes.data for a in arrs]), "amx_set_normalizers")
+
+    def set_termination(self, cfg: TerminationConfig) -> None:
+        ids, shapes, p0, p1 = cfg.tables()
+        ids_a = np.ascontiguousarray(ids, dtype=np.int32)
+        sh_a = np.ascontiguousarray(shapes, dtype=np.int32)
+        p0_a = np.ascontiguousarray(p0, dtype=np.float64)
+        p1_a = np.ascontiguousarray(p1, dtype=np.float64)
+        N.check(self.lib.amx_set_termination(
+            self.h, len(ids), ids_a.ctypes.data, sh_a.ctypes.data, p0_a.ctypes.data, p1_a.ctypes.data,
+            int(cfg.record_all_world), int(cfg.record_world_root_pos), cfg.pos_dim, cfg.rot_dim, int(cfg.horizon),
+            int(cfg.enable_velocity_check), int(cfg.vel_offset), float(cfg.vel_threshold),
+            int(cfg.record_vel_as_pos), float(cfg.sampling_rate)), "amx_set_termination")
+
+    # ---- thin checked launchers -------------------------------------------------------
+    def gemm_bias_act(self, groups, rows, Nn, K, A, lda, sA, W, ldw, sW, bias, sB, C, ldc, sC, col_off, act):
+        N.check(self.lib.amx_gemm_bias_act(self.h, groups, rows, Nn, K, A.data_ptr(), lda, sA, W.data_ptr(), ldw, sW,
+                                           bias.data_ptr(), sB, C.data_ptr(), ldc, sC, col_off, act, self.stream),
+                "amx_gemm_bias_act")
+
+
+def _check_dev(t: torch.Tensor, dtype, name: str, device) -> None:
+    if not isinstance(t, torch.Tensor) or t.device != device or t.dtype != dtype or not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous {dtype} tensor on {device}, got "
+                         f"{getattr(t, 'dtype', type(t))} on {getattr(t, 'device', '?')}")
+
+
+class DeviceEnsemble:
+    """The dense-connect BasicMLP ensemble resident in HBM (milo/milo/dynamics.py:19-233).
+
+    `weights[m]` = [(W0, b0), ..., (WL, bL)] in nn.Linear layout (W [out, in]); `norms` =
+    the 6 transformation vectors of AmpDataset.get_transformations (datasets.py:23-43).
+    All members share the normalizers (DynamicsEnsemble.load_ensemble, dynamics.py:128-131).
+    """
+
+    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0):
+        self.ctx = ctx
+        S, A, M, Hp, L = ctx.S, ctx.A, ctx.M, ctx.Hp, ctx.L
+        if len(weights) != M:
+            raise ValueError(f"expected {M} ensemble members, got {len(weights)}")
+        hidden = weights[0][0][0].shape[0]
+        self.hidden = hidden
+        if round_up(hidden, 128) != Hp or len(weights[0]) != L + 1:
+            raise ValueError("weights do not match the context's (hidden, n_hidden)")
+        dev, k0 = ctx.device, ctx.k0_pad
+        # original input column -> padded activation column
+        colmap = np.concatenate([np.arange(S + A)] + [k0 + i * Hp + np.arange(hidden) for i in range(L)])
+        self.W, self.b = [], []
+        for i in range(L + 1):
+            last = i == L
+            n_rows = ctx.n_out_pad if last else Hp
+            Kp = ctx.ldk if last else k0 + i * Hp
+            Wp = torch.zeros(M, n_rows, Kp, dtype=torch.float32)
+            bp = torch.zeros(M, n_rows, dtype=torch.float32)
+            for m in range(M):
+                W_m, b_m = weights[m][i]
+                W_m = torch.as_tensor(W_m).float().cpu()
+                out_dim, in_dim = W_m.shape
+                exp_in = S + A + i * hidden
+                if in_dim != exp_in or out_dim != (S if last else hidden):
+                    raise ValueError(f"layer {i} of member {m}: shape {tuple(W_m.shape)}, expected "
+                                     f"({S if last else hidden}, {exp_in})")
+                Wp[m, :out_dim][:, torch.from_numpy(colmap[:in_dim])] = W_m
+                bp[m, :out_dim] = torch.as_tensor(b_m).float().cpu()
+            self.W.append(Wp.to(dev).contiguous())
+            self.b.append(bp.to(dev).contiguous())
+        ctx.set_normalizers(norms)
+        self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
+        self.threshold = float(threshold)
+        self._ws = {}
+
+    @property
+    def num_models(self) -> int:
+        return self.ctx.M
+
+    def workspace(self, B: int):
+        """Activation + prediction buffers for B lanes (cached per B_pad)."""
+        Bp = round_up(max(B, 1), 128)
+        ws = self._ws.get(Bp)
+        if ws is None:
+            c = self.ctx
+            ws = dict(Bp=Bp, act=torch.zeros(c.M, Bp, c.ldk, dtype=torch.float32, device=c.device),
+                      preds=torch.zeros(c.M, Bp, c.S, dtype=torch.float32, device=c.device))
+            self._ws[Bp] = ws
+        return ws
+
+    def forward_preds(self, ob: torch.Tensor, act: torch.Tensor, B: int | None = None) -> torch.Tensor:
+        """All members' un-normalised deltas for rows [0, B): returns preds [M, Bp, S] (view
+        of the workspace; rows >= B are padding).  ob/act fp64 or fp32 on the device."""
+        c = self.ctx
+        B = ob.shape[0] if B is None else B
+        if ob.dtype != act.dtype or ob.dtype not in (torch.float64, torch.float32):
+            raise ValueError("ob and act must both be float64 or both float32")
+        _check_dev(ob, ob.dtype, "ob", c.device)
+        _check_dev(act, act.dtype, "act", c.device)
+        if ob.shape[-1] != c.S or act.shape[-1] != c.A or ob.shape[0] < B or act.shape[0] < B:
+            raise ValueError(f"ob {tuple(ob.shape)} / act {tuple(act.shape)} do not match S={c.S}, A={c.A}, B={B}")
+        ws = self.workspace(B)
+        Bp, buf, preds = ws["Bp"], ws["act"], ws["preds"]
+        dt = N.AMX_IN_F64 if ob.dtype == torch.float64 else N.AMX_IN_F32
+        s = c.stream
+        N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
+                                         c.ldk, B, s), "amx_assemble_input")
+        self._mlp(buf, preds, Bp, s)
+        return preds
+
+    def _mlp(self, buf, preds, Bp, s):
+        c = self.ctx
+        sA = Bp * c.ldk
+        for i in range(c.L):
+            K = c.k0_pad + i * c.Hp
+            N.check(c.lib.amx_gemm_bias_act(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W[i].data_ptr(), K,
+                                            c.Hp * K, self.b[i].data_ptr(), c.Hp, buf.data_ptr(), c.ldk, sA,
+                                            K, N.AMX_ACT_RELU, s), "amx_gemm_bias_act")
+        N.check(c.lib.amx_gemm_out_unnorm(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
+                                          self.W[c.L].data_ptr(), c.ldk, c.n_out_pad * c.ldk,
+                                          self.b[c.L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, s),
+                "amx_gemm_out_unnorm")
+
+    def mlp_flops_per_sample(self) -> int:
+        """Algorithmic FLOPs of one sample through all members (unpadded shapes)."""
+        c, h = self.ctx, self.hidden
+        macs = sum(h * (c.S + c.A + i * h) for i in range(c.L)) + c.S * (c.S + c.A + c.L * h)
+        return 2 * macs * c.M
+
+    def disagreement(self, preds: torch.Tensor, B: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        c = self.ctx
+        out = torch.empty(B, dtype=torch.float32, device=c.device) if out is None else out
+        N.check(c.lib.amx_disagreement(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, out.data_ptr(), B, c.stream),
+                "amx_disagreement")
+        return out
+
+    # ---- reference-compatible surface (milo/milo/dynamics.py) ------------------------------
+    def get_action_discrepancy(self, state: torch.Tensor, action: torch.Tensor) -> torch.Tensor:
+        """DynamicsEnsemble.get_action_discrepancy (dynamics.py:154-165): float32 inputs,
+        returns the per-row max pairwise L2 disagreement [B] (on the device)."""
+        state = state.to(self.ctx.device, torch.float32).contiguous()
+        action = action.to(self.ctx.device, torch.float32).contiguous()
+        if state.dim() == 1:
+            state, action = state.unsqueeze(0), action.unsqueeze(0)
+        B = state.shape[0]
+        preds = self.forward_preds(state, action, B)
+        return self.disagreement(preds, B)
+
+    def compute_threshold(self, states: torch.Tensor, actions: torch.Tensor, batch: int = 65536) -> float:
+        """compute_threshold (dynamics.py:145-152): max disagreement over the offline set."""
+        best = None
+        for i in range(0, states.shape[0], batch):
+            d = self.get_action_discrepancy(states[i:i + batch], actions[i:i + batch]).max()
+            best = d if best is None else torch.maximum(best, d)
+        self.threshold = float(best.item())
+        return self.threshold
+
+    def model_forward(self, k: int, state: torch.Tensor, action: torch.Tensor) -> torch.Tensor:
+        """models[k].forward(state, action, unnormalize_out=True) (dynamics.py:216-233)."""
+        state = state.to(self.ctx.device, torch.float32).contiguous()
+        action = action.to(self.ctx.device, torch.float32).contiguous()
+        B = state.shape[0]
+        return self.forward_preds(state, action, B)[k, :B].clone()
+
+
+class RffMap:
+    """phi(x) = cos(x W^T + b) * sqrt(2/F) on MFMA (linear_cost.py:64-71) with fp64 column sums."""
+
+    def __init__(self, ctx: AmxContext, W: torch.Tensor, b: torch.Tensor):
+        self.ctx = ctx
+        F, D = W.shape
+        self.F, self.D = F, D
+        self.Fp = round_up(F, 128)
+        if self.Fp != F:
+            raise ValueError("feature_dim must be a multiple of 128 for the MFMA RFF path")
+        self.Kp = round_up(D, 32)
+        Wp = torch.zeros(F, self.Kp, dtype=torch.float32)
+        Wp[:, :D] = W.float().cpu()
+        self.W = Wp.to(ctx.device).contiguous()
+        self.b = b.float().to(ctx.device).contiguous()
+        # np.sqrt(2/F) is a float64 scalar; torch multiplies the fp32 tensor by it rounded to fp32
+        self.scale = float(np.float32(np.sqrt(2 / F)))
+
+    def features(self, x: torch.Tensor, rows: int, n_valid: int, phi: torch.Tensor, partials: torch.Tensor,
+                 row_mask: torch.Tensor | None = None, ldx: int | None = None) -> None:
+        c = self.ctx
+        ldx = self.Kp if ldx is None else ldx
+        N.check(c.lib.amx_rff_features(c.h, rows, n_valid, self.F, self.Kp, x.data_ptr(), ldx, self.W.data_ptr(),
+                                       self.Kp, self.b.data_ptr(), self.scale, phi.data_ptr(), phi.shape[-1],
+                                       partials.data_ptr(), None if row_mask is None else row_mask.data_ptr(),
+                                       c.stream), "amx_rff_features")
+
+    def embed(self, x: torch.Tensor):
+        """(phi [n, F], column sums [F] fp64) of arbitrary rows x [n, D] (fp32, any device)."""
+        c = self.ctx
+        n = x.shape[0]
+        rows = round_up(max(n, 1), 128)
+        xp = torch.zeros(rows, self.Kp, dtype=torch.float32, device=c.device)
+        xp[:n, :self.D] = x.to(c.device, torch.float32)
+        phi = torch.empty(rows, self.F, dtype=torch.float32, device=c.device)
+        part = torch.empty(rows // 128, self.F, dtype=torch.float64, device=c.device)
+        self.features(xp, rows, n, phi, part)
+        tot = torch.empty(self.F, dtype=torch.float64, device=c.device)
+        N.check(c.lib.amx_sum_partials(c.h, part.data_ptr(), rows // 128, self.F, tot.data_ptr(), c.stream),
+                "amx_sum_partials")
+        return phi[:n], tot

@@ -1,0 +1,65 @@
+"""Device copy of the mjrl Gaussian MLP policy (mjrl/mjrl/policies/gaussian_mlp.py:7-104).
+
+Only the sampling surface the rollout needs (get_action on B lanes at once) runs on the
+GPU; the learner (NPG/TRPO) is out of scope and keeps the host-side policy object.  Call
+`sync_from(params)` after every policy update to refresh the device weights.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _native as N
+from .engine import AmxContext
+
+
+def init_mlp_policy_params(S: int, A: int, hidden=(32, 32), seed=100, init_log_std=-0.25):
+    """Parameters exactly as mjrl MLP.__init__ draws them (gaussian_mlp.py:28-40): seeded,
+    FCNetwork layers in order, last layer weight and bias scaled by 1e-2."""
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    sizes = (S,) + tuple(hidden) + (A,)
+    layers = [nn.Linear(sizes[i], sizes[i + 1]) for i in range(len(sizes) - 1)]
+    layers[-1].weight.data = 1e-2 * layers[-1].weight.data
+    layers[-1].bias.data = 1e-2 * layers[-1].bias.data
+    return [(l.weight.data.clone(), l.bias.data.clone()) for l in layers], torch.ones(A) * init_log_std
+
+
+class DevicePolicy:
+    """Tanh MLP(S -> H1 -> H2 -> A) + exp(log_std) Gaussian noise, on the device."""
+
+    def __init__(self, ctx: AmxContext, layers, log_std, seed: int = 0):
+        if len(layers) != 3:
+            raise NotImplementedError("the device policy kernel supports two hidden layers (mjrl default)")
+        self.ctx = ctx
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.sync_from(layers, log_std)
+
+    @classmethod
+    def from_mjrl(cls, ctx: AmxContext, policy, seed: int = 0):
+        """Build from an mjrl `MLP` object (model.fc_layers + log_std)."""
+        layers = [(l.weight.data, l.bias.data) for l in policy.model.fc_layers]
+        return cls(ctx, layers, policy.log_std.data, seed)
+
+    def sync_from(self, layers, log_std) -> None:
+        dev = self.ctx.device
+        self.W = [torch.as_tensor(W).float().to(dev).contiguous() for (W, _) in layers]
+        self.b = [torch.as_tensor(b).float().to(dev).contiguous() for (_, b) in layers]
+        self.H1, self.H2 = self.W[0].shape[0], self.W[1].shape[0]
+        assert self.W[0].shape[1] == self.ctx.S and self.W[2].shape[0] == self.ctx.A
+        # log_std_val = float64(log_std); noise scale = np.exp(log_std_val) (gaussian_mlp.py:53,102)
+        ls = np.float64(torch.as_tensor(log_std).detach().cpu().numpy().ravel())
+        self.log_std_val = ls
+        self.noise_scale = torch.from_numpy(np.exp(ls)).to(dev)
+
+    def act(self, ob: torch.Tensor, B: int, out: torch.Tensor, counter: int, noise: torch.Tensor | None = None,
+            eval_mode: bool = False, mean_out: torch.Tensor | None = None) -> torch.Tensor:
+        c = self.ctx
+        N.check(c.lib.amx_policy_act(
+            c.h, ob.data_ptr(), B, self.W[0].data_ptr(), self.b[0].data_ptr(), self.H1, self.W[1].data_ptr(),
+            self.b[1].data_ptr(), self.H2, self.W[2].data_ptr(), self.b[2].data_ptr(), self.noise_scale.data_ptr(),
+            None if noise is None else noise.data_ptr(), self.seed, int(counter) & 0xFFFFFFFFFFFFFFFF,
+            int(eval_mode), out.data_ptr(), None if mean_out is None else mean_out.data_ptr(), c.stream),
+            "amx_policy_act")
+        return out

@@ -1,0 +1,184 @@
+"""Batched learned-dynamics rollout engine: B SimEnv lanes stepped in lock-step on one GPU.
+
+One synchronous step (all lanes) is, in launch order on one HIP stream:
+  1. policy      amx_policy_act        a_t = mean(s_t) + exp(log_std) * n      (gaussian_mlp.py:95-104)
+  2. assemble    amx_assemble_input    x0 = [(s-mu)/sd, (a-mu)/sd]               (dynamics.py:225-230)
+  3. ensemble    L x amx_gemm_bias_act + amx_gemm_out_unnorm (all M members)     (dynamics.py:422-433)
+  4. step        amx_step              s' = s + Δ_k (fp64), done, disagreement, [s, s'] f32 (sim_env.py:140-268)
+  5. reward      amx_rff_features      phi(s, s') + fp64 column sums             (linear_cost.py:64-94)
+             or  disc GEMMs + amx_amp_reward (AMP/GAIL path, fused reward)        (gail_cost.py:231-279)
+  6. auto-reset  amx_reset_lanes       done lanes <- reset-table row, model k+1  (sim_env.py:270-285)
+A rollout of K steps is followed by the relabel (batch_reinforce.py:103-169): ordered
+fp64 sum of the feature partials -> (all-reduce across ranks) -> w -> amx_mmd_reward over
+all K*B transitions -> expert cost.
+
+Lane semantics: every lane is a persistent SimEnv; a trajectory that ends (fall/horizon)
+auto-resets in the same step, exactly as `o = env.reset()` after `done` in get_samples
+(sampler.py:48-65), and continues in the next rollout.  The model index follows SimEnv's
+reset counter: model k = (#resets of the lane) mod M, so a lane's first trajectory uses
+member 1 (sim_env.py:118, 282-283).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .costs import GAILCost, RBFLinearCost
+from .engine import DeviceEnsemble, round_up
+from .humanoid import TerminationConfig
+from .policy import DevicePolicy
+
+
+class RolloutEngine:
+    def __init__(self, ensemble: DeviceEnsemble, reset_table, lanes: int, term: TerminationConfig | None = None,
+                 policy: DevicePolicy | None = None, cost=None, seed: int = 0, max_steps: int = 16,
+                 eval_mode: bool = False):
+        self.ens = ensemble
+        self.ctx = c = ensemble.ctx
+        self.term = term or TerminationConfig()
+        c.set_termination(self.term)
+        self.B = int(lanes)
+        self.Bp = round_up(self.B, 128)
+        self.K = int(max_steps)
+        self.policy = policy
+        self.cost = cost
+        self.eval_mode = eval_mode
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        dev = c.device
+        table = torch.as_tensor(reset_table, dtype=torch.float64)
+        if table.dim() != 2 or table.shape[1] != c.S:
+            raise ValueError(f"reset table must be [R, {c.S}] float64")
+        self.table = table.to(dev).contiguous()
+        S, A, B, Bp, K = c.S, c.A, self.B, self.Bp, self.K
+        z = lambda *shape, dt=torch.float32: torch.zeros(*shape, dtype=dt, device=dev)
+        # trajectory buffers of one rollout (obs[K] carries the lane state into the next rollout)
+        self.obs = z(K + 1, B, S, dt=torch.float64)
+        self.next_obs = z(K, B, S, dt=torch.float64)
+        self.acts = z(K, B, A, dt=torch.float64)
+        self.done = z(K, B, dt=torch.uint8)
+        self.disc = z(K, Bp)
+        self.rewards = z(K, Bp)
+        self.ipm = z(K, Bp)
+        self.wbonus = z(K, Bp)
+        self.nonfinite = z(K, B, dt=torch.uint8)
+        self.num_steps = z(B, dt=torch.int32)
+        self.model_idx = z(B, dt=torch.int32)
+        self.reset_count = z(B, dt=torch.int32)
+        self.reset_rows = z(K, B, dt=torch.int32)
+        self.cost_in = z(Bp, c.k_rff_pad)
+        if isinstance(cost, RBFLinearCost):
+            self.phi = z(K, Bp, cost.feature_dim)
+            self.partials = z(K, Bp // 128, cost.feature_dim, dt=torch.float64)
+            self.phi_sum = z(cost.feature_dim, dt=torch.float64)
+            if cost.map.Kp != c.k_rff_pad:
+                raise ValueError("cost input width does not match the state size")
+        elif isinstance(cost, GAILCost):
+            if cost.Kin != c.k_rff_pad:
+                raise ValueError("discriminator input width does not match the state size")
+        self.t = 0              # steps taken in the current rollout
+        self.step_counter = 0   # global step counter (policy RNG stream)
+        self.mb_mmd = None
+
+    # ------------------------------------------------------------------------------------
+    def reset_all(self, rows: torch.Tensor | None = None) -> None:
+        """SimEnv.reset on every lane (sim_env.py:270-285)."""
+        c = self.ctx
+        dst = self.obs[0]
+        N.check(c.lib.amx_reset_lanes(c.h, None, self.table.data_ptr(), self.table.shape[0],
+                                      None if rows is None else rows.data_ptr(), self.seed, None, dst.data_ptr(),
+                                      self.num_steps.data_ptr(), self.model_idx.data_ptr(),
+                                      self.reset_count.data_ptr(), None, self.B, c.stream), "amx_reset_lanes")
+        self.t = 0
+
+    def begin_rollout(self) -> None:
+        """Carry the lane states of the previous rollout into slot 0."""
+        if self.t != 0:
+            self.obs[0].copy_(self.obs[self.t])
+        self.t = 0
+
+    def step(self, actions: torch.Tensor | None = None, reset_rows: torch.Tensor | None = None,
+             noise: torch.Tensor | None = None) -> int:
+        """One synchronous step of all lanes; returns the slot index t it was recorded in.
+        `actions` [B, A] f64 on device replaces the policy; `noise` [B, A] f64 replaces the
+        policy's Philox noise; `reset_rows` [B] i32 forces the rows of lanes that reset."""
+        c, t, B = self.ctx, self.t, self.B
+        if t >= self.K:
+            raise RuntimeError(f"rollout buffer full ({self.K} steps): call begin_rollout()")
+        s = c.stream
+        ob, ob_next, act = self.obs[t], self.next_obs[t], self.acts[t]
+        if actions is not None:
+            act.copy_(actions)
+        else:
+            if self.policy is None:
+                raise RuntimeError("no policy and no actions given")
+            self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode)
+        preds = self.ens.forward_preds(ob, act, B)
+        N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+                               ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
+                               self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                               self.cost_in.data_ptr(), c.k_rff_pad, self.nonfinite[t].data_ptr(), B, s), "amx_step")
+        if isinstance(self.cost, RBFLinearCost):
+            self.cost.map.features(self.cost_in, self.Bp, B, self.phi[t], self.partials[t])
+        elif isinstance(self.cost, GAILCost):
+            self.cost.rewards_from_input(self.cost_in, self.Bp, B, self.disc[t] if c.M >= 2 else None,
+                                         out=self.rewards[t])
+        N.check(c.lib.amx_reset_lanes(c.h, self.done[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
+                                      None if reset_rows is None else reset_rows.data_ptr(), self.seed,
+                                      ob_next.data_ptr(), self.obs[t + 1].data_ptr(), self.num_steps.data_ptr(),
+                                      self.model_idx.data_ptr(), self.reset_count.data_ptr(),
+                                      self.reset_rows[t].data_ptr(), B, s), "amx_reset_lanes")
+        self.t += 1
+        self.step_counter += 1
+        return t
+
+    def rollout(self, K: int | None = None) -> int:
+        """K synchronous steps (default: the buffer depth).  Returns K*B transitions."""
+        K = self.K if K is None else K
+        self.begin_rollout()
+        for _ in range(K):
+            self.step()
+        return K * self.B
+
+    # ------------------------------------------------------------------------------------
+    def feature_sum(self) -> torch.Tensor:
+        """Ordered fp64 sum of this rank's RFF column partials over the recorded steps."""
+        c, cost = self.ctx, self.cost
+        n_parts = self.t * (self.Bp // 128)
+        N.check(c.lib.amx_sum_partials(c.h, self.partials.data_ptr(), n_parts, cost.feature_dim,
+                                       self.phi_sum.data_ptr(), c.stream), "amx_sum_partials")
+        return self.phi_sum
+
+    def relabel(self, allreduce=None) -> dict:
+        """Relabel the recorded transitions (batch_reinforce.py:103-169, MMD + ensemble).
+        `allreduce(tensor)` sums a device tensor across ranks in place (None: one rank)."""
+        c, cost, T, B = self.ctx, self.cost, self.t, self.B
+        if isinstance(cost, GAILCost):
+            return {}  # rewards were produced per step
+        if not isinstance(cost, RBFLinearCost):
+            raise RuntimeError("relabel needs an RBFLinearCost or GAILCost")
+        phi_sum = self.feature_sum()
+        if allreduce is not None:
+            # one collective per rollout: the fp64 feature sum and the sample count
+            cnt = torch.tensor([float(T * B)], dtype=torch.float64, device=c.device)
+            allreduce(phi_sum)
+            allreduce(cnt)
+            # amx_mmd_fit rounds (sum / count) to fp32; dividing on device first and passing
+            # count 1.0 gives the same value without a host round trip for the count
+            self.mb_mmd = cost.fit_w((phi_sum / cnt).contiguous(), 1.0)
+        else:
+            self.mb_mmd = cost.fit_w(phi_sum, float(T * B))
+        n = T * self.Bp
+        N.check(c.lib.amx_mmd_reward(c.h, self.phi.data_ptr(), cost.feature_dim, cost.w.data_ptr(),
+                                     cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),
+                                     cost.lambda_b, cost.c_min, cost.c_max, self.rewards.data_ptr(),
+                                     self.ipm.data_ptr(), self.wbonus.data_ptr(), n, c.stream), "amx_mmd_reward")
+        return {"mb_mmd": self.mb_mmd}
+
+    def bonus_mmd(self) -> float:
+        """infos['bonus_mmd'] = mean(-rewards) - expert cost (batch_reinforce.py:169)."""
+        T, B = self.t, self.B
+        mean_cost = (-self.rewards[:T, :B]).double().mean()
+        return float(mean_cost.item()) - float(self.cost.get_expert_cost().item())
