@@ -16,14 +16,27 @@ __device__ inline double wave_sum(double v) {
   return v;
 }
 
-// out[f] = sum_p partials[p][f] in ascending p (deterministic).
-__global__ __launch_bounds__(256) void k_sum_partials(const double* __restrict__ partials, int n_parts, int F,
-                                                      double* __restrict__ out) {
-  const int f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= F) return;
+// out[f] = sum_p partials[p][f].  Block = 64 columns x 16 waves; wave w sums its contiguous
+// chunk of parts in ascending order, then the 16 chunk sums are added in wave order:
+// the result is deterministic (fixed association) and the dependent-add chain is n/16 long.
+__global__ __launch_bounds__(1024) void k_sum_partials(const double* __restrict__ partials, int n_parts, int F,
+                                                       double* __restrict__ out) {
+  __shared__ double red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;
+  const int per = (n_parts + 15) / 16;
+  const int p0 = w * per, p1 = min(n_parts, p0 + per);
   double s = 0.0;
-  for (int p = 0; p < n_parts; ++p) s += partials[(long long)p * F + f];
-  out[f] = s;
+  if (f < F)
+    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && f < F) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    out[f] = t;
+  }
 }
 
 // w = (float)(sum/count) - phi_e ; mmd = dot(w, w).  One block; F <= 4096.
@@ -102,12 +115,19 @@ __global__ __launch_bounds__(256) void k_expert_cost(const float* __restrict__ p
   if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void k_sum_small(const double* __restrict__ partials, int n, double* __restrict__ out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    double s = 0.0;
-    for (int i = 0; i < n; ++i) s += partials[i];
-    out[0] = s;
+// Deterministic sum of n partials: thread t sums t, t+256, ... then a fixed-shape tree.
+__global__ __launch_bounds__(256) void k_sum_small(const double* __restrict__ partials, int n,
+                                                   double* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += partials[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) out[0] = red[0];
 }
 
 __global__ __launch_bounds__(256) void k_amp_reward(const float* __restrict__ h, int ldh, int Hd,
@@ -146,7 +166,7 @@ __global__ __launch_bounds__(256) void k_amp_reward(const float* __restrict__ h,
 extern "C" int amx_sum_partials(amx_ctx* ctx, const double* partials, int n_parts, int F, double* out,
                                 void* stream) {
   AMX_CHECK_ARG(ctx && partials && out && n_parts >= 0 && F > 0, "amx_sum_partials: bad argument");
-  hipLaunchKernelGGL(k_sum_partials, dim3((F + 255) / 256), dim3(256), 0, (hipStream_t)stream, partials, n_parts,
+  hipLaunchKernelGGL(k_sum_partials, dim3((F + 63) / 64), dim3(1024), 0, (hipStream_t)stream, partials, n_parts,
                      F, out);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
@@ -188,7 +208,7 @@ extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi,
   hipLaunchKernelGGL(k_expert_cost, dim3(nb), dim3(256), 0, (hipStream_t)stream, phi_e_rows, ldphi, w, F, n, c_min,
                      c_max, out + 1);
   AMX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_sum_small, dim3(1), dim3(64), 0, (hipStream_t)stream, out + 1, nb, out);
+  hipLaunchKernelGGL(k_sum_small, dim3(1), dim3(256), 0, (hipStream_t)stream, out + 1, nb, out);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

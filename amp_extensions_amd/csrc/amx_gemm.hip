@@ -80,28 +80,41 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
 
-  // staging map: float4 index q = t + 256*j (j < 4) -> row q>>3, column 4*(q&7)
+  // staging map: float4 index q = t + 256*j (j < 4) -> row q>>3, column 4*(q&7).
+  // The stage registers are named scalars (not an array captured by a lambda: that put
+  // them in scratch and made every iteration wait for its own prefetch).
   const int st_r = t >> 3, st_c = (t & 7) * 4;
+  const float* a_src = Ag + (long long)st_r * a.lda + st_c;
+  const float* w_src = Wg + (long long)st_r * a.ldw + st_c;
+  const long long a_step = 32LL * a.lda, w_step = 32LL * a.ldw;
+  float* const a_dst0 = smem + st_r * LDS_LD + st_c;
+  float* const w_dst0 = smem + BM * LDS_LD + st_r * LDS_LD + st_c;
 
-  float4 ra[4], rw[4];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = st_r + 32 * j;
-      ra[j] = *reinterpret_cast<const float4*>(Ag + (long long)r * a.lda + k0 + st_c);
-      rw[j] = *reinterpret_cast<const float4*>(Wg + (long long)r * a.ldw + k0 + st_c);
-    }
-  };
-  auto lstore = [&](int buf) {
-    float* As = smem + buf * TILE_FLOATS;
-    float* Ws = As + BM * LDS_LD;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int r = st_r + 32 * j;
-      *reinterpret_cast<float4*>(As + r * LDS_LD + st_c) = ra[j];
-      *reinterpret_cast<float4*>(Ws + r * LDS_LD + st_c) = rw[j];
-    }
-  };
+  float4 ra0, ra1, ra2, ra3, rw0, rw1, rw2, rw3;
+#define AMX_GLOAD(k0)                                                             \
+  do {                                                                            \
+    ra0 = *reinterpret_cast<const float4*>(a_src + (k0));                         \
+    ra1 = *reinterpret_cast<const float4*>(a_src + a_step + (k0));                \
+    ra2 = *reinterpret_cast<const float4*>(a_src + 2 * a_step + (k0));            \
+    ra3 = *reinterpret_cast<const float4*>(a_src + 3 * a_step + (k0));            \
+    rw0 = *reinterpret_cast<const float4*>(w_src + (k0));                         \
+    rw1 = *reinterpret_cast<const float4*>(w_src + w_step + (k0));                \
+    rw2 = *reinterpret_cast<const float4*>(w_src + 2 * w_step + (k0));            \
+    rw3 = *reinterpret_cast<const float4*>(w_src + 3 * w_step + (k0));            \
+  } while (0)
+#define AMX_LSTORE(buf)                                                           \
+  do {                                                                            \
+    float* ad = a_dst0 + (buf) * TILE_FLOATS;                                     \
+    float* wd = w_dst0 + (buf) * TILE_FLOATS;                                     \
+    *reinterpret_cast<float4*>(ad) = ra0;                                         \
+    *reinterpret_cast<float4*>(ad + 32 * LDS_LD) = ra1;                           \
+    *reinterpret_cast<float4*>(ad + 64 * LDS_LD) = ra2;                           \
+    *reinterpret_cast<float4*>(ad + 96 * LDS_LD) = ra3;                           \
+    *reinterpret_cast<float4*>(wd) = rw0;                                         \
+    *reinterpret_cast<float4*>(wd + 32 * LDS_LD) = rw1;                           \
+    *reinterpret_cast<float4*>(wd + 64 * LDS_LD) = rw2;                           \
+    *reinterpret_cast<float4*>(wd + 96 * LDS_LD) = rw3;                           \
+  } while (0)
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -112,43 +125,44 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = a.K / BK;
-  gload(0);
-  lstore(0);
+  AMX_GLOAD(0);
+  AMX_LSTORE(0);
   __syncthreads();
 
+  const int a_off = (wm * 64 + li) * LDS_LD + lh * 16;
+  const int w_off = BM * LDS_LD + (wn * 64 + li) * LDS_LD + lh * 16;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * BK);
+    // prefetch the next K-tile (the last iteration re-reads its own tile: branch-free loop)
+    const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
+    AMX_GLOAD(kn);
+    // keep the prefetch ahead of the MFMA block (hipcc otherwise sinks the loads to their
+    // consumer, the LDS store after the MFMAs, and the latency is exposed every K-tile)
+    __builtin_amdgcn_sched_barrier(0);
 
-    const float* As = smem + cur * TILE_FLOATS;
-    const float* Ws = As + BM * LDS_LD;
-    float4 fa[2][4], fb[2][4];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-        fa[m][v] = *reinterpret_cast<const float4*>(As + (wm * 64 + m * 32 + li) * LDS_LD + lh * 16 + v * 4);
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int v = 0; v < 4; ++v)
-        fb[n][v] = *reinterpret_cast<const float4*>(Ws + (wn * 64 + n * 32 + li) * LDS_LD + lh * 16 + v * 4);
-
+    const float* As = smem + cur * TILE_FLOATS + a_off;
+    const float* Ws = smem + cur * TILE_FLOATS + w_off;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
+      const float4 fa0 = *reinterpret_cast<const float4*>(As + v * 4);
+      const float4 fa1 = *reinterpret_cast<const float4*>(As + 32 * LDS_LD + v * 4);
+      const float4 fb0 = *reinterpret_cast<const float4*>(Ws + v * 4);
+      const float4 fb1 = *reinterpret_cast<const float4*>(Ws + 32 * LDS_LD + v * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float a0 = fa[0][v][e], a1 = fa[1][v][e];
-        const float b0 = fb[0][v][e], b1 = fb[1][v][e];
+        const float a0 = fa0[e], a1 = fa1[e];
+        const float b0 = fb0[e], b1 = fb1[e];
         acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
         acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
         acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
       }
     }
-    if (kt + 1 < nk) lstore(cur ^ 1);
+    AMX_LSTORE(cur ^ 1);
     __syncthreads();
   }
+#undef AMX_GLOAD
+#undef AMX_LSTORE
 
   // ---- epilogue ---------------------------------------------------------------------
   // C/D map of 32x32 f32 MFMA: column = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
@@ -195,34 +209,41 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
       }
     }
   } else {  // EPI_RFF
-    // column sums of this wave's 64 rows -> LDS -> ordered sum of the two M-waves
-    double* red = reinterpret_cast<double*>(smem);  // [2 (wm)][128 cols], reuses stage LDS
-    float* Cg = a.C;
+    // Stage the raw 128x128 tile through LDS, then one column per thread: coalesced phi
+    // rows, one (non-unrolled) cos call site instead of 64 inlined copies, and the fp64
+    // column sum of the valid rows in fixed row order (deterministic).
+    constexpr int CLD = BN + 4;
+    float* Cs = smem;  // [BM][CLD] = 67,584 B, reuses the stage buffers (last barrier passed)
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int col = col0 + n * 32 + li;
-      const float bv = a.bias[col];
-      double csum = 0.0;
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
+      for (int m = 0; m < 2; ++m)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-          const float z = acc[m][n][e] + bv;
-          const float phi = cosf(z) * a.rff_scale;
-          Cg[(long long)row * a.ldc + col] = phi;
-          const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
-          csum += valid ? (double)phi : 0.0;
+          const int r = wm * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          Cs[r * CLD + wn * 64 + n * 32 + li] = acc[m][n][e];
         }
-      }
-      csum += __shfl_xor(csum, 32);
-      if (lh == 0) red[wm * BN + wn * 64 + n * 32 + li] = csum;
+    __syncthreads();
+    const int c = t & (BN - 1), half = t >> 7;
+    const int col = tn * BN + c;
+    const float bv = a.bias[col];
+    double csum = 0.0;
+    float* Cg = a.C;
+#pragma unroll 2
+    for (int i = 0; i < BM / 2; ++i) {
+      const int r = half * (BM / 2) + i;
+      const int row = tm * BM + r;
+      const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
+      const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
+      Cg[(long long)row * a.ldc + col] = phi;
+      const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
+      csum += valid ? (double)phi : 0.0;
     }
     __syncthreads();
-    if (t < BN) {
-      const double s = red[t] + red[BN + t];
-      a.col_partials[(long long)tm * a.N + tn * BN + t] = s;
-    }
+    double* red = reinterpret_cast<double*>(smem);
+    if (half == 1) red[c] = csum;
+    __syncthreads();
+    if (half == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[c];
   }
 }
 

@@ -135,6 +135,9 @@ class DeviceEnsemble:
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
         self._ws = {}
+        # optional timing hook: when a list, every forward appends a (start, end) pair of
+        # torch.cuda.Events recorded on the launch stream around the L+1 GEMM launches
+        self.gemm_events = None
 
     @property
     def num_models(self) -> int:
@@ -174,6 +177,10 @@ class DeviceEnsemble:
     def _mlp(self, buf, preds, Bp, s):
         c = self.ctx
         sA = Bp * c.ldk
+        ev = self.gemm_events
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         for i in range(c.L):
             K = c.k0_pad + i * c.Hp
             N.check(c.lib.amx_gemm_bias_act(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W[i].data_ptr(), K,
@@ -183,6 +190,9 @@ class DeviceEnsemble:
                                           self.W[c.L].data_ptr(), c.ldk, c.n_out_pad * c.ldk,
                                           self.b[c.L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, s),
                 "amx_gemm_out_unnorm")
+        if ev is not None:
+            e1.record()
+            ev.append((e0, e1, Bp))
 
     def mlp_flops_per_sample(self) -> int:
         """Algorithmic FLOPs of one sample through all members (unpadded shapes)."""

@@ -1,0 +1,220 @@
+#!/usr/bin/env python
+"""Headline benchmark: learned-dynamics env-steps/s of the full MILO rollout on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): one bench step = one complete
+40 000-sample MILO rollout on every rank — B persistent humanoid3d lanes x ceil(40000/B)
+synchronous steps of {device Gaussian-MLP policy -> 4-model dense [512]x4 ensemble ->
+fp64 state update + fall/horizon termination + disagreement -> RFF (s,s') features ->
+auto-reset}, then the relabel {ordered fp64 feature sum -> RCCL all-reduce (N>1) -> MMD
+witness -> per-sample pessimistic reward -> expert cost over the resident 50k-row expert
+buffer}.  Synthetic data of the BASELINE shape (obs 197, act 36; --faithful for the
+226/28 layout the reference scene actually builds) and random-init weights of the
+reference architecture.  Inputs are resident in HBM before timing starts.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run
+(one rank per GPU, RCCL).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), v_mfma_f32_32x32x2_f32
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20, help="timed rollouts")
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--lanes", type=int, default=4096, help="persistent env lanes per GPU")
+    p.add_argument("--samples", type=int, default=40000, help="samples per rollout per GPU (weak scaling)")
+    p.add_argument("--faithful", action="store_true", help="use the 226/28 state/action layout")
+    p.add_argument("--cost", choices=["mmd", "gail"], default="mmd")
+    p.add_argument("--expert-rows", type=int, default=50000)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-workers", type=int, default=0)
+    p.add_argument("--cpu-samples", type=int, default=0)
+    return p.parse_args()
+
+
+def cpu_baseline_leg(S, A, args):
+    """The oracle's restated reference sampler + host relabel, timed on this host's cores.
+    Runs before anything touches the GPU (its worker pool forks)."""
+    from oracle import cpu_baseline as cb
+    workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+    samples = args.cpu_samples or 8000 * workers
+    r = cb.run(S, A, workers=workers, samples=samples, expert_rows=args.expert_rows)
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": round(r["end_to_end_steps_per_s"], 1), "unit": "env-steps/s", "cores": r["workers"],
+        "kind": "port",
+        "sample": (f"{r['samples']} env-steps ({r['paths']} complete trajectories) by {r['workers']} forked "
+                   f"sampler workers (torch threads 1) + host relabel (fit_cost + per-path bonus costs, "
+                   f"{args.expert_rows}-row expert buffer); sampler alone {r['sampler_steps_per_s']:.0f} "
+                   f"env-steps/s; sampler {r['sampler_s']:.2f}s + relabel {r['relabel_s']:.2f}s; cpu '{cpu}', "
+                   f"os.cpu_count()={os.cpu_count()}"),
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    S, A = (226, 28) if args.faithful else (197, 36)
+
+    cpu_base = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        cpu_base = cpu_baseline_leg(S, A, args)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import amp_extensions_amd as amx
+    from amp_extensions_amd import synthetic as syn
+    from amp_extensions_amd.policy import init_mlp_policy_params
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    allreduce = (lambda t: dist.all_reduce(t)) if world > 1 else None
+
+    # ---- model + data setup (untimed) -------------------------------------------------------
+    hidden = [512] * 4
+    M = 4
+    s, a, s2 = syn.offline(100000, S, A, 0)
+    st, at, s2t = (torch.from_numpy(x).float() for x in (s, a, s2))
+    from amp_extensions_amd.datasets import get_transformations
+    norms = get_transformations(st, at, s2t)
+    from amp_extensions_amd.ensemble import init_ensemble_weights
+    ens_w = init_ensemble_weights(S, A, hidden, M, base_seed=100)
+    ctx = amx.AmxContext(S, A, n_models=M, hidden=512, n_hidden=4, feat_dim=512, device=dev)
+    ens = amx.DeviceEnsemble(ctx, ens_w, norms)
+    thr = ens.compute_threshold(st.to(dev), at.to(dev))
+    expert = torch.from_numpy(syn.expert(args.expert_rows, S, 3))
+    if args.cost == "mmd":
+        cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, bw_samples=100000, lambda_b=0.0025,
+                                 seed=100, ctx=ctx)
+    else:
+        cost = amx.GAILCost(expert, hidden_dims=(1024, 512), lambda_b=0.0025, seed=100, ctx=ctx)
+    pw, log_std = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    pol = amx.DevicePolicy(ctx, pw, log_std, seed=1000 + rank)
+    B = args.lanes
+    T = math.ceil(args.samples / B)
+    eng = amx.RolloutEngine(ens, syn.reset_table(65536, S, 1), lanes=B, policy=pol, cost=cost,
+                            seed=(7 << 32) + rank, max_steps=T)
+    eng.reset_all()
+
+    def one_rollout():
+        eng.rollout(T)
+        if args.cost == "mmd":
+            eng.relabel(allreduce)
+            cost.get_expert_cost()
+        return T * B
+
+    for _ in range(args.warmup):
+        one_rollout()
+    torch.cuda.synchronize()
+
+    # ---- timed region -----------------------------------------------------------------------
+    ens.gemm_events = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    samples = 0
+    done_count = 0
+    for _ in range(args.steps):
+        samples += one_rollout()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    term_rate = float(eng.done[:T].float().mean().item())
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    total_samples = samples * world
+
+    # dominant kernel: the ensemble GEMM launches (HIP events on the launch stream)
+    gemm_ms = sum(e0.elapsed_time(e1) for (e0, e1, _) in ens.gemm_events)
+    n_fwd = len(ens.gemm_events)
+    launches = n_fwd * (ctx.L + 1)
+    flops_per_fwd = ens.mlp_flops_per_sample() * B
+    achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
+    ens.gemm_events = None
+
+    step_flops = ens.mlp_flops_per_sample() + 2 * (2 * S) * 512  # + RFF features
+    value = total_samples / elapsed
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "gemm_traffic.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                tj = json.load(f)
+            if tj.get("state_dim") == S and tj.get("lanes") == B:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "learned-dynamics env steps/sec (humanoid3d, 40k-sample rollout)",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (SURVEY §8d distributions; random-init reference architecture)",
+            "config": {
+                "workload": "full MILO rollout: policy + 4-model ensemble step + termination + "
+                            f"{'RFF-MMD relabel' if args.cost == 'mmd' else 'AMP/GAIL LS-disc reward'}",
+                "samples_per_rollout_per_gpu": T * B, "lanes_per_gpu": B, "sync_steps": T,
+                "state_dim": S, "action_dim": A, "ensemble": "4 x dense-connect [512]x4 ReLU",
+                "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
+                "parallelism": f"dp{world} (lane-sharded, 1 all-reduce/rollout)",
+                "termination_rate": round(term_rate, 5), "threshold": thr,
+            },
+            "roofline": {
+                "bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved_tflops / F32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": "k_gemm_nt (ensemble layers, f32 MFMA 32x32x2)",
+                "avg_launch_us": round(gemm_ms * 1e3 / max(launches, 1), 2),
+                "flops_per_launch": flops_per_fwd / (ctx.L + 1),
+            },
+            "step_flops_frac": round(value / world * step_flops / (F32_MFMA_PEAK_TFLOPS * 1e12), 4),
+            "cpu_baseline": cpu_base,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

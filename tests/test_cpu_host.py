@@ -1,0 +1,99 @@
+"""CPU-only checks: the C-ABI library builds/loads and exports every declared symbol, the
+host-side layout/packing logic, and the ABI's argument validation (no kernel launches)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from amp_extensions_amd import _build, _native
+from amp_extensions_amd import synthetic as syn
+from amp_extensions_amd.ensemble import basic_mlp_layer_shapes, init_ensemble_weights, weights_from_state_dict
+from amp_extensions_amd.humanoid import TerminationConfig, FALL_BODIES
+
+
+@pytest.fixture(scope="module")
+def lib():
+    path = _build.build(verbose=False)
+    return _native.load(path)
+
+
+def test_library_exports_every_header_symbol(lib):
+    syms = _native.header_symbols()
+    assert len(syms) >= 20
+    raw = ctypes.CDLL(_build.LIB_PATH)
+    for s in syms:
+        assert hasattr(raw, s), s
+    # the Python binding declares exactly the header's functions
+    assert sorted(_native.SIGNATURES) == syms
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_build.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_abi_version_and_errors(lib):
+    assert lib.amx_abi_version() == 1
+    # bad dims are refused without touching the GPU
+    assert not lib.amx_create(0, 226, 28, 9, 512, 4, 512)   # > AMX_MAX_MODELS
+    assert b"bad dims" in lib.amx_last_error()
+    assert not lib.amx_create(0, 226, 28, 4, 500, 4, 512)   # hidden not a multiple of 128
+    # null-context calls fail with AMX_E_INVAL and a message
+    rc = lib.amx_gemm_bias_act(None, 1, 128, 128, 32, None, 32, 0, None, 32, 0, None, 0, None, 128, 0, 0, 1, None)
+    assert rc == -1
+    rc = lib.amx_step(None, None, 226, 0, None, None, None, None, None, None, None, 0, None, 1, None)
+    assert rc == -1 and b"amx_step" in lib.amx_last_error()
+
+
+def test_dense_layer_shapes_match_basicmlp():
+    # dynamics.py:412-420: input of layer i = concat of all previous widths
+    assert basic_mlp_layer_shapes(226, 28, [512] * 4) == [(512, 254), (512, 766), (512, 1278), (512, 1790),
+                                                          (226, 2302)]
+    macs = sum(o * i for o, i in basic_mlp_layer_shapes(226, 28, [512] * 4))
+    assert macs == 2613308
+    assert sum(o * i for o, i in basic_mlp_layer_shapes(197, 36, [512] * 4)) == 2499405
+
+
+def test_init_matches_oracle_rng_order():
+    from oracle import milo_ref as R
+    a = init_ensemble_weights(226, 28, [64] * 4, 2, 100)
+    b = R.init_ensemble_weights(226, 28, [64] * 4, 2, 100)
+    for ma, mb in zip(a, b):
+        for (wa, ba), (wb, bb) in zip(ma, mb):
+            assert torch.equal(wa, wb) and torch.equal(ba, bb)
+
+
+def test_state_dict_roundtrip():
+    w = init_ensemble_weights(20, 4, [16, 16], 1, 5)[0]
+    sd = {f"fc_layers.{i}.weight": W for i, (W, _) in enumerate(w)}
+    sd.update({f"fc_layers.{i}.bias": b for i, (_, b) in enumerate(w)})
+    back = weights_from_state_dict(sd)
+    assert all(torch.equal(x[0], y[0]) and torch.equal(x[1], y[1]) for x, y in zip(back, w))
+
+
+def test_termination_tables():
+    ids, shapes, p0, p1 = TerminationConfig().tables()
+    assert tuple(ids) == FALL_BODIES and len(ids) == 13
+    assert shapes.count(0) == 5 and shapes.count(1) == 8  # 5 spheres, 8 capsules (humanoid3d.txt)
+    assert max(9 * b + 5 for b in ids) < 197  # every index valid in both layouts
+
+
+def test_synthetic_reset_table_starts_standing():
+    t = syn.reset_table(512, 226, 1)
+    for b in FALL_BODIES:
+        assert (t[:, 9 * b + 2] >= 0.2).all()
+    s, a, s2 = syn.offline(64, 197, 36, 0)
+    assert s.shape == (64, 197) and a.shape == (64, 36)
+    assert syn.expert(32, 197).shape == (32, 394)
+
+
+def test_product_package_never_imports_oracle():
+    root = os.path.dirname(_build.PKG_DIR)
+    for dp, _, fs in os.walk(_build.PKG_DIR):
+        for f in fs:
+            if f.endswith(".py"):
+                src = open(os.path.join(dp, f)).read()
+                assert "import oracle" not in src and "from oracle" not in src, f
+    assert os.path.isdir(os.path.join(root, "oracle"))
