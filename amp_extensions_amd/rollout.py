@@ -27,6 +27,7 @@ import torch
 
 from . import _native as N
 from .costs import GAILCost, RBFLinearCost
+from .dist import feature_mean
 from .engine import DeviceEnsemble, round_up
 from .humanoid import TerminationConfig
 from .policy import DevicePolicy
@@ -35,7 +36,7 @@ from .policy import DevicePolicy
 class RolloutEngine:
     def __init__(self, ensemble: DeviceEnsemble, reset_table, lanes: int, term: TerminationConfig | None = None,
                  policy: DevicePolicy | None = None, cost=None, seed: int = 0, max_steps: int = 16,
-                 eval_mode: bool = False):
+                 eval_mode: bool = False, auto_reset: bool = True, record_means: bool = False):
         self.ens = ensemble
         self.ctx = c = ensemble.ctx
         self.term = term or TerminationConfig()
@@ -46,6 +47,7 @@ class RolloutEngine:
         self.policy = policy
         self.cost = cost
         self.eval_mode = eval_mode
+        self.auto_reset = auto_reset
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
         table = torch.as_tensor(reset_table, dtype=torch.float64)
@@ -69,6 +71,7 @@ class RolloutEngine:
         self.reset_count = z(B, dt=torch.int32)
         self.reset_rows = z(K, B, dt=torch.int32)
         self.cost_in = z(Bp, c.k_rff_pad)
+        self.means = z(K, B, A) if record_means else None
         if isinstance(cost, RBFLinearCost):
             self.phi = z(K, Bp, cost.feature_dim)
             self.partials = z(K, Bp // 128, cost.feature_dim, dt=torch.float64)
@@ -85,12 +88,19 @@ class RolloutEngine:
     # ------------------------------------------------------------------------------------
     def reset_all(self, rows: torch.Tensor | None = None) -> None:
         """SimEnv.reset on every lane (sim_env.py:270-285)."""
+        self.reset_lanes(None, rows)
+
+    def reset_lanes(self, mask: torch.Tensor | None, rows: torch.Tensor | None = None) -> None:
+        """SimEnv.reset on the lanes with mask != 0 (all lanes when mask is None); the lane
+        states are taken from (and written back to) slot 0 of a fresh rollout."""
         c = self.ctx
+        self.begin_rollout()
         dst = self.obs[0]
-        N.check(c.lib.amx_reset_lanes(c.h, None, self.table.data_ptr(), self.table.shape[0],
-                                      None if rows is None else rows.data_ptr(), self.seed, None, dst.data_ptr(),
-                                      self.num_steps.data_ptr(), self.model_idx.data_ptr(),
-                                      self.reset_count.data_ptr(), None, self.B, c.stream), "amx_reset_lanes")
+        N.check(c.lib.amx_reset_lanes(c.h, None if mask is None else mask.data_ptr(), self.table.data_ptr(),
+                                      self.table.shape[0], None if rows is None else rows.data_ptr(), self.seed,
+                                      dst.data_ptr(), dst.data_ptr(), self.num_steps.data_ptr(),
+                                      self.model_idx.data_ptr(), self.reset_count.data_ptr(), None, self.B,
+                                      c.stream), "amx_reset_lanes")
         self.t = 0
 
     def begin_rollout(self) -> None:
@@ -114,7 +124,8 @@ class RolloutEngine:
         else:
             if self.policy is None:
                 raise RuntimeError("no policy and no actions given")
-            self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode)
+            self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode,
+                            mean_out=None if self.means is None else self.means[t])
         preds = self.ens.forward_preds(ob, act, B)
         N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
@@ -125,11 +136,14 @@ class RolloutEngine:
         elif isinstance(self.cost, GAILCost):
             self.cost.rewards_from_input(self.cost_in, self.Bp, B, self.disc[t] if c.M >= 2 else None,
                                          out=self.rewards[t])
-        N.check(c.lib.amx_reset_lanes(c.h, self.done[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
-                                      None if reset_rows is None else reset_rows.data_ptr(), self.seed,
-                                      ob_next.data_ptr(), self.obs[t + 1].data_ptr(), self.num_steps.data_ptr(),
-                                      self.model_idx.data_ptr(), self.reset_count.data_ptr(),
-                                      self.reset_rows[t].data_ptr(), B, s), "amx_reset_lanes")
+        if self.auto_reset:
+            N.check(c.lib.amx_reset_lanes(c.h, self.done[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
+                                          None if reset_rows is None else reset_rows.data_ptr(), self.seed,
+                                          ob_next.data_ptr(), self.obs[t + 1].data_ptr(), self.num_steps.data_ptr(),
+                                          self.model_idx.data_ptr(), self.reset_count.data_ptr(),
+                                          self.reset_rows[t].data_ptr(), B, s), "amx_reset_lanes")
+        else:  # gym semantics: the caller resets (SimEnv facade)
+            self.obs[t + 1].copy_(ob_next)
         self.t += 1
         self.step_counter += 1
         return t
@@ -160,16 +174,10 @@ class RolloutEngine:
         if not isinstance(cost, RBFLinearCost):
             raise RuntimeError("relabel needs an RBFLinearCost or GAILCost")
         phi_sum = self.feature_sum()
-        if allreduce is not None:
-            # one collective per rollout: the fp64 feature sum and the sample count
-            cnt = torch.tensor([float(T * B)], dtype=torch.float64, device=c.device)
-            allreduce(phi_sum)
-            allreduce(cnt)
-            # amx_mmd_fit rounds (sum / count) to fp32; dividing on device first and passing
-            # count 1.0 gives the same value without a host round trip for the count
-            self.mb_mmd = cost.fit_w((phi_sum / cnt).contiguous(), 1.0)
-        else:
-            self.mb_mmd = cost.fit_w(phi_sum, float(T * B))
+        # one fused all-reduce of [sum phi, count] across ranks (dist.feature_mean); the
+        # fp64 mean is rounded to fp32 inside amx_mmd_fit (count passed as 1.0)
+        mean = feature_mean(phi_sum, float(T * B), allreduce if allreduce is not None else (lambda t: t))
+        self.mb_mmd = cost.fit_w(mean.contiguous(), 1.0)
         n = T * self.Bp
         N.check(c.lib.amx_mmd_reward(c.h, self.phi.data_ptr(), cost.feature_dim, cost.w.data_ptr(),
                                      cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),

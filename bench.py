@@ -35,7 +35,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20, help="timed rollouts")
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--lanes", type=int, default=4096, help="persistent env lanes per GPU")
+    p.add_argument("--lanes", type=int, default=8192, help="persistent env lanes per GPU")
     p.add_argument("--samples", type=int, default=40000, help="samples per rollout per GPU (weak scaling)")
     p.add_argument("--faithful", action="store_true", help="use the 226/28 state/action layout")
     p.add_argument("--cost", choices=["mmd", "gail"], default="mmd")
