@@ -36,7 +36,7 @@ SIGNATURES = {
     "amx_disagreement": (c_int, [vp, vp, c_int, c_ll, vp, c_int, vp]),
     "amx_reset_lanes": (c_int, [vp, vp, vp, c_int, vp, c_u64, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_policy_act": (c_int, [vp, vp, c_int, vp, vp, c_int, vp, vp, c_int, vp, vp, vp, vp, c_u64, c_u64,
-                               c_int, vp, vp, vp]),
+                               c_int, vp, vp, vp, c_ll, c_int, vp]),
     "amx_rff_features": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_flt, vp, c_int,
                                  vp, vp, vp]),
     "amx_sum_partials": (c_int, [vp, vp, c_int, c_int, vp, vp]),

@@ -74,14 +74,20 @@ class RBFLinearCost:
         """linear_cost.py:64-71."""
         return self.map.embed(x)[0]
 
-    def fit_w(self, phi_sum: torch.Tensor, count: float) -> float:
-        """Closed-form witness from an (already all-reduced) fp64 feature sum."""
+    def fit_w_device(self, phi_sum: torch.Tensor, count: float) -> torch.Tensor:
+        """Closed-form witness from an (already all-reduced) fp64 feature sum; returns w.w as
+        a 1-element device tensor (no host synchronisation)."""
         c = self.ctx
-        self.w = torch.empty(self.feature_dim, dtype=torch.float32, device=c.device)
-        mmd = torch.empty(1, dtype=torch.float32, device=c.device)
+        if self.w is None:
+            self.w = torch.empty(self.feature_dim, dtype=torch.float32, device=c.device)
+            self._mmd = torch.empty(1, dtype=torch.float32, device=c.device)
         N.check(c.lib.amx_mmd_fit(c.h, phi_sum.data_ptr(), float(count), self.phi_e.data_ptr(), self.feature_dim,
-                                  self.w.data_ptr(), mmd.data_ptr(), c.stream), "amx_mmd_fit")
-        return float(mmd.item())
+                                  self.w.data_ptr(), self._mmd.data_ptr(), c.stream), "amx_mmd_fit")
+        return self._mmd
+
+    def fit_w(self, phi_sum: torch.Tensor, count: float) -> float:
+        """fit_w_device + the reference's Python-float return (linear_cost.py:94)."""
+        return float(self.fit_w_device(phi_sum, count).item())
 
     def fit_cost(self, data_pi: torch.Tensor) -> float:
         """linear_cost.py:84-94: w = mean phi(data_pi) - phi_e; returns w.w."""

@@ -9,27 +9,42 @@
 // C[r][n] = sum_k A[r][k] * W[n][k]: both operands are K-contiguous ("NT"), which is the
 // torch nn.Linear weight layout, so weights are used as stored.
 //
-// Tile: 128x128 per workgroup, BK = 32, 4 waves in 2x2, each wave 64x64 = 2x2 MFMA
-// 32x32 tiles.  Operands are register-staged through LDS (double buffer, one barrier per
-// K-tile).  Lane l of an MFMA supplies k-slot h = l>>5; we map slot h of MFMA step s to
-// k = 16h + s so that each lane reads 16 consecutive floats of its row with 4
-// ds_read_b128 (the same permutation on A and W keeps the contraction exact).  LDS rows
-// are padded to 36 floats: rows 16 apart land on distinct 16-byte bank slots, so the
-// 16-lane groups of ds_read_b128 are conflict-free.
+// Tile family Tile<WM, WN, TM, TN>: WM x WN waves, each owning TM x TN MFMA 32x32 tiles, so
+// the workgroup tile is (32*WM*TM) x (32*WN*TN) with BK = 32.  Operands are register-staged
+// through LDS (double buffer, one barrier per K-tile, the next tile's global loads issued
+// before the MFMA block).  Lane l of an MFMA supplies k-slot h = l>>5; slot h of MFMA step s
+// is mapped to k = 16h + s, so each lane reads 16 consecutive floats of its row with 4
+// ds_read_b128 (the same permutation on A and W keeps the contraction exact).  LDS rows are
+// padded to 36 floats: rows 16 apart land on distinct 16-byte bank slots, so the 16-lane
+// groups of ds_read_b128 are conflict-free.
 #include "amx_common.h"
 
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+// native vector (HIP's float4 is a wrapper struct: arrays of it were not promoted to registers)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128;
-constexpr int BN = 128;
 constexpr int BK = 32;
-constexpr int LDS_LD = BK + 4;                          // floats per LDS row
-constexpr int TILE_FLOATS = (BM + BN) * LDS_LD;         // one stage (A + W)
-constexpr size_t LDS_BYTES = 2 * TILE_FLOATS * sizeof(float);  // 73,728 B: 2 WGs per CU
+constexpr int LDS_LD = BK + 4;  // floats per LDS row
 
 enum { EPI_BIAS_ACT = 0, EPI_UNNORM = 1, EPI_RFF = 2 };
+
+template <int WM_, int WN_, int TM_, int TN_, int STAGES_ = 2, int OCC_ = 2>
+struct Tile {
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_;
+  static constexpr int STAGES = STAGES_;  // 2: double-buffered LDS, 1 barrier / K-tile;
+                                          // 1: single buffer, 2 barriers / K-tile, half the LDS
+  static constexpr int OCC = OCC_;        // __launch_bounds__ waves-per-SIMD target
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  static constexpr int STAGE = (BM + BN) * LDS_LD;          // floats of one stage (A + W)
+  static constexpr size_t LDS = STAGES * STAGE * sizeof(float);
+  static constexpr int ROW_STEP = NT / 8;                   // staging rows covered per pass
+  static constexpr int VA = BM / ROW_STEP, VW = BN / ROW_STEP;
+  static_assert(BM % ROW_STEP == 0 && BN % ROW_STEP == 0, "staging map");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
 
 struct GemmArgs {
   const float* A; long long strideA; int lda;
@@ -65,8 +80,10 @@ __device__ inline void map_tile(const GemmArgs& a, int& g, int& tm, int& tn) {
   g = rest / a.tiles_m;
 }
 
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
+template <int EPI, class TL>
+__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
+  constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW;
+  constexpr int STAGE = TL::STAGE, RS = TL::ROW_STEP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int g, tm, tn;
   map_tile(a, g, tm, tn);
@@ -77,107 +94,106 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = t >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
   const int li = lane & 31, lh = lane >> 5;
 
-  // staging map: float4 index q = t + 256*j (j < 4) -> row q>>3, column 4*(q&7).
-  // The stage registers are named scalars (not an array captured by a lambda: that put
-  // them in scratch and made every iteration wait for its own prefetch).
+  // staging map: float4 q = t + NT*j -> row (t>>3) + RS*j, column 4*(t&7).  The stage
+  // registers stay in registers: the loops below are fully unrolled with constant indices
+  // and no lambda captures them (a captured array went to scratch in an earlier version).
   const int st_r = t >> 3, st_c = (t & 7) * 4;
   const float* a_src = Ag + (long long)st_r * a.lda + st_c;
   const float* w_src = Wg + (long long)st_r * a.ldw + st_c;
-  const long long a_step = 32LL * a.lda, w_step = 32LL * a.ldw;
+  const long long a_step = (long long)RS * a.lda, w_step = (long long)RS * a.ldw;
   float* const a_dst0 = smem + st_r * LDS_LD + st_c;
   float* const w_dst0 = smem + BM * LDS_LD + st_r * LDS_LD + st_c;
 
-  float4 ra0, ra1, ra2, ra3, rw0, rw1, rw2, rw3;
-#define AMX_GLOAD(k0)                                                             \
-  do {                                                                            \
-    ra0 = *reinterpret_cast<const float4*>(a_src + (k0));                         \
-    ra1 = *reinterpret_cast<const float4*>(a_src + a_step + (k0));                \
-    ra2 = *reinterpret_cast<const float4*>(a_src + 2 * a_step + (k0));            \
-    ra3 = *reinterpret_cast<const float4*>(a_src + 3 * a_step + (k0));            \
-    rw0 = *reinterpret_cast<const float4*>(w_src + (k0));                         \
-    rw1 = *reinterpret_cast<const float4*>(w_src + w_step + (k0));                \
-    rw2 = *reinterpret_cast<const float4*>(w_src + 2 * w_step + (k0));            \
-    rw3 = *reinterpret_cast<const float4*>(w_src + 3 * w_step + (k0));            \
-  } while (0)
-#define AMX_LSTORE(buf)                                                           \
-  do {                                                                            \
-    float* ad = a_dst0 + (buf) * TILE_FLOATS;                                     \
-    float* wd = w_dst0 + (buf) * TILE_FLOATS;                                     \
-    *reinterpret_cast<float4*>(ad) = ra0;                                         \
-    *reinterpret_cast<float4*>(ad + 32 * LDS_LD) = ra1;                           \
-    *reinterpret_cast<float4*>(ad + 64 * LDS_LD) = ra2;                           \
-    *reinterpret_cast<float4*>(ad + 96 * LDS_LD) = ra3;                           \
-    *reinterpret_cast<float4*>(wd) = rw0;                                         \
-    *reinterpret_cast<float4*>(wd + 32 * LDS_LD) = rw1;                           \
-    *reinterpret_cast<float4*>(wd + 64 * LDS_LD) = rw2;                           \
-    *reinterpret_cast<float4*>(wd + 96 * LDS_LD) = rw3;                           \
-  } while (0)
-
-  f32x16 acc[2][2];
+  f32x4 ra[VA], rw[VW];
+  f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = a.K / BK;
-  AMX_GLOAD(0);
-  AMX_LSTORE(0);
+#pragma unroll
+  for (int j = 0; j < VA; ++j) ra[j] = *reinterpret_cast<const f32x4*>(a_src + j * a_step);
+#pragma unroll
+  for (int j = 0; j < VW; ++j) rw[j] = *reinterpret_cast<const f32x4*>(w_src + j * w_step);
+#pragma unroll
+  for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + j * RS * LDS_LD) = ra[j];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + j * RS * LDS_LD) = rw[j];
   __syncthreads();
 
-  const int a_off = (wm * 64 + li) * LDS_LD + lh * 16;
-  const int w_off = BM * LDS_LD + (wn * 64 + li) * LDS_LD + lh * 16;
+  const int a_off = (wm * TM * 32 + li) * LDS_LD + lh * 16;
+  const int w_off = BM * LDS_LD + (wn * TN * 32 + li) * LDS_LD + lh * 16;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = (TL::STAGES == 2) ? (kt & 1) : 0;
+    if constexpr (TL::STAGES == 1) {
+      // single buffer: tile kt is in registers; publish it, then prefetch kt+1 behind the MFMAs
+      if (kt > 0) {
+        __syncthreads();  // everyone finished reading tile kt-1
+#pragma unroll
+        for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + j * RS * LDS_LD) = ra[j];
+#pragma unroll
+        for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + j * RS * LDS_LD) = rw[j];
+        __syncthreads();
+      }
+    }
     // prefetch the next K-tile (the last iteration re-reads its own tile: branch-free loop)
     const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
-    AMX_GLOAD(kn);
+#pragma unroll
+    for (int j = 0; j < VA; ++j) ra[j] = *reinterpret_cast<const f32x4*>(a_src + j * a_step + kn);
+#pragma unroll
+    for (int j = 0; j < VW; ++j) rw[j] = *reinterpret_cast<const f32x4*>(w_src + j * w_step + kn);
     // keep the prefetch ahead of the MFMA block (hipcc otherwise sinks the loads to their
     // consumer, the LDS store after the MFMAs, and the latency is exposed every K-tile)
     __builtin_amdgcn_sched_barrier(0);
 
-    const float* As = smem + cur * TILE_FLOATS + a_off;
-    const float* Ws = smem + cur * TILE_FLOATS + w_off;
+    const float* As = smem + cur * STAGE + a_off;
+    const float* Ws = smem + cur * STAGE + w_off;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const float4 fa0 = *reinterpret_cast<const float4*>(As + v * 4);
-      const float4 fa1 = *reinterpret_cast<const float4*>(As + 32 * LDS_LD + v * 4);
-      const float4 fb0 = *reinterpret_cast<const float4*>(Ws + v * 4);
-      const float4 fb1 = *reinterpret_cast<const float4*>(Ws + 32 * LDS_LD + v * 4);
+      f32x4 fa[TM], fb[TN];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float a0 = fa0[e], a1 = fa1[e];
-        const float b0 = fb0[e], b1 = fb1[e];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-      }
+      for (int m = 0; m < TM; ++m) fa[m] = *reinterpret_cast<const f32x4*>(As + m * 32 * LDS_LD + v * 4);
+#pragma unroll
+      for (int n = 0; n < TN; ++n) fb[n] = *reinterpret_cast<const f32x4*>(Ws + n * 32 * LDS_LD + v * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[m][e], fb[n][e], acc[m][n], 0, 0, 0);
     }
-    AMX_LSTORE(cur ^ 1);
-    __syncthreads();
+    if constexpr (TL::STAGES == 2) {
+      const int nb = (cur ^ 1) * STAGE;
+#pragma unroll
+      for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + nb + j * RS * LDS_LD) = ra[j];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + nb + j * RS * LDS_LD) = rw[j];
+      __syncthreads();
+    }
   }
-#undef AMX_GLOAD
-#undef AMX_LSTORE
+  if constexpr (TL::STAGES == 1) __syncthreads();  // epilogues reuse the LDS
 
   // ---- epilogue ---------------------------------------------------------------------
   // C/D map of 32x32 f32 MFMA: column = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
-  const int row0 = tm * BM + wm * 64;
-  const int col0 = tn * BN + wn * 64;
+  const int row0 = tm * BM + wm * TM * 32;
+  const int col0 = tn * BN + wn * TN * 32;
 
   if constexpr (EPI == EPI_BIAS_ACT) {
     const float* bias = a.bias + (long long)g * a.strideBias;
     float* Cg = a.C + (long long)g * a.strideC;
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
+    for (int n = 0; n < TN; ++n) {
       const int col = col0 + n * 32 + li;
       const float bv = bias[col];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
+      for (int m = 0; m < TM; ++m) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
@@ -191,13 +207,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
     const float* bias = a.bias + (long long)g * a.strideBias;
     float* Cg = a.C + (long long)g * a.strideC;
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
+    for (int n = 0; n < TN; ++n) {
       const int col = col0 + n * 32 + li;
       if (col < a.n_valid) {
         const float bv = bias[col];
         const float sc = a.scale[col], sh = a.shift[col];
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
+        for (int m = 0; m < TM; ++m) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
@@ -208,20 +224,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
         }
       }
     }
-  } else {  // EPI_RFF
+  } else {  // EPI_RFF (instantiated for the 128x128 tile only)
+    static_assert(BM == 128 && BN == 128 && TL::NT == 256, "RFF epilogue assumes the 128x128 tile");
     // Stage the raw 128x128 tile through LDS, then one column per thread: coalesced phi
     // rows, one (non-unrolled) cos call site instead of 64 inlined copies, and the fp64
     // column sum of the valid rows in fixed row order (deterministic).
     constexpr int CLD = BN + 4;
     float* Cs = smem;  // [BM][CLD] = 67,584 B, reuses the stage buffers (last barrier passed)
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < TN; ++n)
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < TM; ++m)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int r = wm * 64 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-          Cs[r * CLD + wn * 64 + n * 32 + li] = acc[m][n][e];
+          const int r = wm * TM * 32 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
         }
     __syncthreads();
     const int c = t & (BN - 1), half = t >> 7;
@@ -247,31 +264,73 @@ __global__ __launch_bounds__(256, 2) void k_gemm_nt(GemmArgs a) {
   }
 }
 
-int launch_gemm(int epi, GemmArgs& a, hipStream_t stream) {
-  a.tiles_m = a.rows / BM;
-  a.tiles_n = (epi == EPI_UNNORM) ? amx::round_up(a.n_valid, BN) / BN : a.N / BN;
+// ---- tile selection -------------------------------------------------------------------------
+using T128 = Tile<2, 2, 2, 2>;        // 128x128, 256 threads, 2 WGs / CU
+using T128x256 = Tile<2, 2, 2, 4>;    // 128x256, 256 threads, wave 64x128
+using T128x256w8 = Tile<2, 4, 2, 2>;  // 128x256, 512 threads, wave 64x64
+using T256 = Tile<4, 2, 2, 4>;        // 256x256, 512 threads, wave 64x128
+using T256x128 = Tile<4, 2, 2, 2>;    // 256x128, 512 threads, wave 64x64
+using T128x224 = Tile<4, 1, 1, 7>;    // 128x224, 256 threads, wave 32x224 (output layer, S <= 224)
+using T128s1 = Tile<2, 2, 2, 2, 1, 4>;    // 128x128, single-buffered LDS (37 KB): 4 WGs / CU
+using T128x256s1 = Tile<2, 4, 2, 2, 1, 2>;  // 128x256, 8 waves, single-buffered (55 KB): 2 WGs / CU
+
+int g_variant = -1;  // -1: automatic; >= 0 forces a tile for A/B tests (amx__set_gemm_variant)
+
+template <int EPI, class TL>
+int launch_tile(GemmArgs& a, hipStream_t stream) {
+  a.tiles_m = a.rows / TL::BM;
+  a.tiles_n = a.N / TL::BN;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  dim3 grid(nwg), block(256);
-  switch (epi) {
-    case EPI_BIAS_ACT:
-      hipLaunchKernelGGL(k_gemm_nt<EPI_BIAS_ACT>, grid, block, LDS_BYTES, stream, a);
-      break;
-    case EPI_UNNORM:
-      hipLaunchKernelGGL(k_gemm_nt<EPI_UNNORM>, grid, block, LDS_BYTES, stream, a);
-      break;
-    default:
-      hipLaunchKernelGGL(k_gemm_nt<EPI_RFF>, grid, block, LDS_BYTES, stream, a);
-      break;
-  }
+  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
+}
+
+template <int EPI>
+int launch_variant(int v, GemmArgs& a, hipStream_t s) {
+  switch (v) {
+    case 1: return launch_tile<EPI, T128x256>(a, s);
+    case 2: return launch_tile<EPI, T128x256w8>(a, s);
+    case 3: return launch_tile<EPI, T256>(a, s);
+    case 4: return launch_tile<EPI, T256x128>(a, s);
+    case 5: return launch_tile<EPI, T128s1>(a, s);
+    case 6: return launch_tile<EPI, T128x256s1>(a, s);
+    default: return launch_tile<EPI, T128>(a, s);
+  }
+}
+
+bool variant_fits(int v, const GemmArgs& a) {
+  const int bm = (v == 3 || v == 4) ? 256 : 128;
+  const int bn = (v == 1 || v == 2 || v == 3 || v == 6) ? 256 : 128;
+  return a.rows % bm == 0 && a.N % bn == 0;
+}
+
+int launch_gemm(int epi, GemmArgs& a, hipStream_t stream) {
+  if (epi == EPI_RFF) return launch_tile<EPI_RFF, T128>(a, stream);
+  if (epi == EPI_UNNORM) {
+    const int n32 = amx::round_up(a.n_valid, 32);
+    if (g_variant < 0 && n32 > 128 && n32 <= 224) {  // one 224-wide tile instead of two 128s
+      a.N = 224;
+      return launch_tile<EPI_UNNORM, T128x224>(a, stream);
+    }
+    a.N = amx::round_up(a.n_valid, 128);
+    const int v = (g_variant >= 0 && variant_fits(g_variant, a)) ? g_variant : 0;
+    return launch_variant<EPI_UNNORM>(v, a, stream);
+  }
+  // automatic: 256x128 with 8 waves of 64x64 (one WG per CU, 110 KB LDS) when rows allow:
+  // +1-2% over 128x128 both per layer (tools/gemm_variants.py) and on the whole rollout
+  // (tools/rollout_ab.py, same process); single-buffered and 256-wide tiles measured slower.
+  int v = g_variant < 0 ? 4 : g_variant;
+  if (!variant_fits(v, a)) v = 0;
+  return launch_variant<EPI_BIAS_ACT>(v, a, stream);
 }
 
 int check_common(const char* fn, int groups, int rows, int K, const float* A, int lda, const float* W,
                  int ldw) {
   AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
-  AMX_CHECK_ARG(rows >= 0 && rows % BM == 0, "%s: rows=%d must be a multiple of %d", fn, rows, BM);
+  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
+                AMX_ROW_TILE);
   AMX_CHECK_ARG(K > 0 && K % BK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, BK);
   AMX_CHECK_ARG(A && W, "%s: null operand", fn);
   AMX_CHECK_ARG(amx::aligned16(A) && amx::aligned16(W), "%s: operands must be 16-byte aligned", fn);
@@ -282,6 +341,12 @@ int check_common(const char* fn, int groups, int rows, int K, const float* A, in
 
 }  // namespace
 
+// Internal (not in the public header): force a tile variant for A/B measurements.
+extern "C" int amx__set_gemm_variant(int v) {
+  g_variant = v;
+  return AMX_OK;
+}
+
 extern "C" int amx_gemm_bias_act(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
                                  long long strideA, const float* W, int ldw, long long strideW,
                                  const float* bias, long long strideBias, float* C, int ldc, long long strideC,
@@ -289,7 +354,7 @@ extern "C" int amx_gemm_bias_act(amx_ctx* ctx, int groups, int rows, int N, int 
   AMX_CHECK_ARG(ctx, "amx_gemm_bias_act: null ctx");
   int rc = check_common("amx_gemm_bias_act", groups, rows, K, A, lda, W, ldw);
   if (rc) return rc;
-  AMX_CHECK_ARG(N > 0 && N % BN == 0, "amx_gemm_bias_act: N=%d must be a multiple of %d", N, BN);
+  AMX_CHECK_ARG(N > 0 && N % 128 == 0, "amx_gemm_bias_act: N=%d must be a multiple of 128", N);
   AMX_CHECK_ARG(bias && C, "amx_gemm_bias_act: null bias/C");
   AMX_CHECK_ARG(col_off >= 0 && col_off + N <= ldc, "amx_gemm_bias_act: col_off=%d N=%d ldc=%d", col_off, N, ldc);
   AMX_CHECK_ARG(act == AMX_ACT_NONE || act == AMX_ACT_RELU, "amx_gemm_bias_act: act=%d", act);
@@ -316,7 +381,7 @@ extern "C" int amx_gemm_out_unnorm(amx_ctx* ctx, int groups, int rows, int n_val
   a.W = W; a.strideW = strideW; a.ldw = ldw;
   a.bias = bias; a.strideBias = strideBias;
   a.C = preds; a.strideC = strideP; a.ldc = ldp;
-  a.rows = rows; a.N = amx::round_up(n_valid, BN); a.K = K; a.groups = groups;
+  a.rows = rows; a.K = K; a.groups = groups;
   a.n_valid = n_valid;
   const int S = ctx->S, Ad = ctx->A;
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
@@ -330,7 +395,7 @@ extern "C" int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int 
   AMX_CHECK_ARG(ctx, "amx_rff_features: null ctx");
   int rc = check_common("amx_rff_features", 1, rows, K, x, ldx, W, ldw);
   if (rc) return rc;
-  AMX_CHECK_ARG(F > 0 && F % BN == 0, "amx_rff_features: F=%d must be a multiple of %d", F, BN);
+  AMX_CHECK_ARG(F > 0 && F % 128 == 0, "amx_rff_features: F=%d must be a multiple of 128", F);
   AMX_CHECK_ARG(b && phi && col_partials && ldphi >= F, "amx_rff_features: null b/phi/partials or ldphi");
   AMX_CHECK_ARG(n_valid >= 0 && n_valid <= rows, "amx_rff_features: n_valid=%d rows=%d", n_valid, rows);
   GemmArgs a = {};

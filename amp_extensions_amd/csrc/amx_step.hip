@@ -81,19 +81,31 @@ __device__ inline float lane_disagreement(const float* __restrict__ preds, long 
   return best;
 }
 
+// Generic member count: one pair at a time (re-reads the L2-hot rows), few registers.
+__device__ inline float lane_disagreement_any(const float* __restrict__ preds, long long strideP, int ldp, int b,
+                                              int S, int M, int lane) {
+  float best = 0.f;
+  bool first = true;
+  for (int i = 0; i < M; ++i)
+    for (int k = i + 1; k < M; ++k) {
+      double acc = 0.0;
+      for (int j = lane; j < S; j += 64) {
+        const float d = preds[i * strideP + (long long)b * ldp + j] - preds[k * strideP + (long long)b * ldp + j];
+        acc += (double)d * (double)d;
+      }
+      const float n = (float)sqrt(wave_sum(acc));
+      best = (first || n > best) ? n : best;
+      first = false;
+    }
+  return best;
+}
+
+// M = 4 (the MILO ensemble) gets the fused 6-pair pass; other sizes the generic loop.
+// (A switch over every M would size the register file for M = 8 in every caller.)
 __device__ inline float disagreement_dispatch(int M, const float* preds, long long strideP, int ldp, int b, int S,
                                               int lane) {
-  switch (M) {
-    case 2: return lane_disagreement<2>(preds, strideP, ldp, b, S, lane);
-    case 3: return lane_disagreement<3>(preds, strideP, ldp, b, S, lane);
-    case 4: return lane_disagreement<4>(preds, strideP, ldp, b, S, lane);
-    case 5: return lane_disagreement<5>(preds, strideP, ldp, b, S, lane);
-    case 6: return lane_disagreement<6>(preds, strideP, ldp, b, S, lane);
-    case 7: return lane_disagreement<7>(preds, strideP, ldp, b, S, lane);
-    case 8: return lane_disagreement<8>(preds, strideP, ldp, b, S, lane);
-    default: return 0.f;  // a single model has no pairs: torch max over an empty dim errors;
-                          // the host refuses M == 1 for disagreement.
-  }
+  if (M == 4) return lane_disagreement<4>(preds, strideP, ldp, b, S, lane);
+  return M >= 2 ? lane_disagreement_any(preds, strideP, ldp, b, S, M, lane) : 0.f;
 }
 
 __global__ __launch_bounds__(256) void k_disagreement(const float* __restrict__ preds, long long strideP, int ldp,
@@ -117,10 +129,14 @@ struct StepArgs {
   amx_termination term;
 };
 
+// NIT = ceil(S/64) state elements per lane, kept in registers: all loads of the row are
+// issued up front, and the fall check reads the few values it needs from the owning lanes
+// with shuffles instead of re-loading them (the kernel is latency-bound, not HBM-bound).
+template <int NIT>
 __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (b >= a.B) return;
+  if (b >= a.B) return;  // wave-uniform
   const amx_termination& T = a.term;
   const int S = a.S;
   const int k = a.model_idx[b];
@@ -128,54 +144,67 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   const double* ob = a.ob + (long long)b * S;
   double* on = a.ob_next + (long long)b * S;
 
+  double o[NIT], x[NIT];
+  float p[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int j = lane + 64 * it;
+    o[it] = j < S ? ob[j] : 0.0;
+    p[it] = j < S ? pk[j] : 0.f;
+  }
   // sim_env.py:158  ob += state_diff (float32 -> float64), then the in-place velocity
   // rescale of check_velocity (:264-267) when RecordVelAsPos and the check are enabled.
   const bool vscale = T.vel_check && T.record_vel_as_pos;
   bool vel_bad = false, bad = false;
-  for (int j = lane; j < S; j += 64) {
-    double x = ob[j] + (double)pk[j];
-    if (vscale && j >= T.vel_offset) x = x / T.sampling_rate;
-    on[j] = x;
-    if (T.vel_check && j >= T.vel_offset) vel_bad |= fabs(x) > T.vel_thresh;
-    bad |= !isfinite(x);
-    if (a.cost_in) {
-      a.cost_in[(long long)b * a.ldc + j] = (float)ob[j];
-      a.cost_in[(long long)b * a.ldc + S + j] = (float)x;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int j = lane + 64 * it;
+    double v = o[it] + (double)p[it];
+    if (vscale && j >= T.vel_offset) v = v / T.sampling_rate;
+    x[it] = v;
+    if (j < S) {
+      on[j] = v;
+      if (T.vel_check && j >= T.vel_offset) vel_bad |= fabs(v) > T.vel_thresh;
+      bad |= !isfinite(v);
+      if (a.cost_in) {
+        a.cost_in[(long long)b * a.ldc + j] = (float)o[it];
+        a.cost_in[(long long)b * a.ldc + S + j] = (float)v;
+      }
     }
   }
   if (a.cost_in) {  // zero the K padding of the cost-input row
     for (int j = 2 * S + lane; j < a.ldc; j += 64) a.cost_in[(long long)b * a.ldc + j] = 0.f;
   }
 
-  // fall check (sim_env.py:175-257): lane i < n evaluates body i from recomputed values
-  // (identical fp64 ops as the stores above, so the same bits).
+  // fall check (sim_env.py:175-257): lane i < n evaluates body i; every lane takes part
+  // in the shuffles that fetch ob'[j] from the lane that owns element j.
+  auto fetch = [&](int j) -> double {
+    const int src = j & 63, itj = j >> 6;
+    double r = 0.0;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const double v = __shfl(x[it], src);
+      r = (itj == it) ? v : r;
+    }
+    return r;
+  };
+  const int bi = lane < T.n ? lane : 0;
+  const double root_y = fetch(0);
+  const double rel_y = fetch(T.y_index[bi]);
+  const double ny = fetch(T.shape[bi] == AMX_SHAPE_CAPSULE ? T.ny_index[bi] : 0);
   bool hit = false;
-  if (lane < T.n) {
-    const int i = lane;
-    auto val = [&](int j) {
-      double x = ob[j] + (double)pk[j];
-      if (vscale && j >= T.vel_offset) x = x / T.sampling_rate;
-      return x;
-    };
-    if (T.shape[i] == AMX_SHAPE_SPHERE || T.shape[i] == AMX_SHAPE_CAPSULE) {
-      double y;
-      if (T.list_index_world[i]) {
-        y = val(T.y_index[i]);
-      } else {
-        y = val(0) + val(T.y_index[i]);
-      }
-      if (T.shape[i] == AMX_SHAPE_SPHERE) {
-        hit = y <= T.thresh[i];
-      } else {
-        const double ny = val(T.ny_index[i]);
-        const double top = T.half_h[i] * ny;
-        const double bot = T.neg_half_h[i] * ny;
-        const double ytop = y + top;
-        const double ybot = y + bot;
-        hit = (ytop <= T.thresh[i]) || (ybot <= T.thresh[i]);
-      }
-    }  // box: check_box always False (sim_env.py:238-244)
-  }
+  if (lane < T.n && (T.shape[bi] == AMX_SHAPE_SPHERE || T.shape[bi] == AMX_SHAPE_CAPSULE)) {
+    const double y = T.list_index_world[bi] ? rel_y : root_y + rel_y;
+    if (T.shape[bi] == AMX_SHAPE_SPHERE) {
+      hit = y <= T.thresh[bi];
+    } else {
+      const double top = T.half_h[bi] * ny;
+      const double bot = T.neg_half_h[bi] * ny;
+      const double ytop = y + top;
+      const double ybot = y + bot;
+      hit = (ytop <= T.thresh[bi]) || (ybot <= T.thresh[bi]);
+    }
+  }  // box: check_box always False (sim_env.py:238-244)
   const bool collided = __ballot(hit) != 0ull;
   const bool vexp = __ballot(vel_bad) != 0ull;
   const bool nf = __ballot(bad) != 0ull;
@@ -229,76 +258,174 @@ __global__ __launch_bounds__(256) void k_reset(const uint8_t* __restrict__ mask,
 }
 
 // ---- policy ----------------------------------------------------------------------------------
-// One workgroup = 256 threads = 16 lanes x 16 threads; every thread owns hidden units
-// u = t16, t16+16, ...  Layer inputs are staged in LDS per lane.
+// One workgroup = 256 threads serving POL_LANES = 16 lanes, POL_TPL = 16 threads per lane.
+// The whole MLP (W1 [H1][S], W2, W3) and the lanes' float32 observations are staged in LDS
+// once per workgroup.  Thread (lane l, u0) owns output units u = u0 + 16q of every layer; each
+// inner step loads one float4 of the lane's input row (broadcast over the lane's 16 threads)
+// and one float4 of each owned weight row — all loads issued before the FMAs, so the LDS
+// latency overlaps (rows beyond H are clamped to a valid row and their results dropped).
+// W rows use a padded stride (16-byte slots of rows 0..15 land on distinct banks).
 constexpr int POL_LANES = 16;
+constexpr int POL_TPL = 16;
 constexpr int POL_MAXH = 256;
 
-__global__ __launch_bounds__(256) void k_policy(const double* __restrict__ ob, const float* __restrict__ W1,
-                                                const float* __restrict__ b1, int H1, const float* __restrict__ W2,
-                                                const float* __restrict__ b2, int H2, const float* __restrict__ W3,
-                                                const float* __restrict__ b3, const double* __restrict__ nscale,
-                                                const double* __restrict__ noise, uint32_t k0, uint32_t k1,
-                                                uint32_t ctr_lo, uint32_t ctr_hi, int eval_mode,
-                                                double* __restrict__ act, float* __restrict__ mean_out, int S,
-                                                int A, int B) {
+__host__ __device__ inline int pol_stride(int k) {  // row stride (floats) for a [*, k] LDS matrix
+  const int r = (k + 3) & ~3;
+  return (r % 8 == 0) ? r + 4 : r;
+}
+
+__host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A) {
+  const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
+  const size_t fl = (size_t)H1 * s1 + H2 * s2 + A * s3 + H1 + H2 + A + POL_LANES * (s1 + s2 + s3 + A);
+  return fl * sizeof(float);
+}
+
+struct PolicyArgs {
+  const double* ob; const float* W1; const float* b1; int H1; const float* W2; const float* b2; int H2;
+  const float* W3; const float* b3; const double* nscale; const double* noise;
+  uint32_t k0, k1, ctr_lo, ctr_hi; int eval_mode;
+  double* act; float* mean_out;
+  float* x0; long long stride_m; int ldk; int k0_pad; int M; const float* norm;
+  int S, A, B;
+};
+
+typedef float pf4 __attribute__((ext_vector_type(4)));
+
+template <int Q>
+__device__ inline void pol_layer(const float* __restrict__ w, int ws, const float* __restrict__ x, int n4,
+                                 const float* __restrict__ bias, int H, int u0, float (&out)[Q], bool tanh_act) {
+  float acc[Q];
+  const float* wr[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    acc[q] = 0.f;
+    const int u = u0 + POL_TPL * q;
+    wr[q] = w + (u < H ? u : H - 1) * ws;
+  }
+#pragma unroll 2
+  for (int k = 0; k < n4; ++k) {
+    const pf4 v = *reinterpret_cast<const pf4*>(x + 4 * k);
+    pf4 a[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) a[q] = *reinterpret_cast<const pf4*>(wr[q] + 4 * k);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      acc[q] = fmaf(a[q].x, v.x, acc[q]);
+      acc[q] = fmaf(a[q].y, v.y, acc[q]);
+      acc[q] = fmaf(a[q].z, v.z, acc[q]);
+      acc[q] = fmaf(a[q].w, v.w, acc[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int u = u0 + POL_TPL * q;
+    const float z = acc[q] + bias[u < H ? u : H - 1];
+    out[q] = tanh_act ? tanhf(z) : z;
+  }
+}
+
+template <int QH, int QA>
+__global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   extern __shared__ __attribute__((aligned(16))) float psm[];
-  // [POL_LANES][S] observations, then [POL_LANES][H1] and [POL_LANES][H2]
-  float* so = psm;
-  float* sh1 = so + POL_LANES * S;
-  float* sh2 = sh1 + POL_LANES * H1;
+  const int S = p.S, A = p.A, H1 = p.H1, H2 = p.H2;
+  const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
+  float* w1 = psm;                       // [H1][s1]
+  float* w2 = w1 + H1 * s1;              // [H2][s2]
+  float* w3 = w2 + H2 * s2;              // [A][s3]
+  float* bb1 = w3 + A * s3;
+  float* bb2 = bb1 + H1;
+  float* bb3 = bb2 + H2;
+  float* so = bb3 + A;                   // [POL_LANES][s1]
+  float* h1 = so + POL_LANES * s1;       // [POL_LANES][s2]
+  float* h2 = h1 + POL_LANES * s2;       // [POL_LANES][s3]
+  float* xa_s = h2 + POL_LANES * s3;     // [POL_LANES][A] float32 actions for the fused assembly
   const int t = threadIdx.x;
-  const int lb = t >> 4, u0 = t & 15;
   const int b0 = blockIdx.x * POL_LANES;
-  for (int i = t; i < POL_LANES * S; i += 256) {
-    const int l = i / S, j = i - l * S;
+  // zero-padded staging (the pad columns take part in the float4 dot products)
+  for (int r = t >> 5; r < H1; r += 8)
+    for (int c = t & 31; c < s1; c += 32) w1[r * s1 + c] = c < S ? p.W1[(long long)r * S + c] : 0.f;
+  for (int r = t >> 5; r < H2; r += 8)
+    for (int c = t & 31; c < s2; c += 32) w2[r * s2 + c] = c < H1 ? p.W2[r * H1 + c] : 0.f;
+  for (int r = t >> 5; r < A; r += 8)
+    for (int c = t & 31; c < s3; c += 32) w3[r * s3 + c] = c < H2 ? p.W3[r * H2 + c] : 0.f;
+  for (int i = t; i < H1; i += 256) bb1[i] = p.b1[i];
+  for (int i = t; i < H2; i += 256) bb2[i] = p.b2[i];
+  for (int i = t; i < A; i += 256) bb3[i] = p.b3[i];
+  for (int l = t >> 5; l < POL_LANES; l += 8) {
     const int b = b0 + l;
-    so[i] = (b < B) ? (float)ob[(long long)b * S + j] : 0.f;  // np.float32(observation)
+    for (int c = t & 31; c < s1; c += 32)
+      so[l * s1 + c] = (b < p.B && c < S) ? (float)p.ob[(long long)b * S + c] : 0.f;  // np.float32(observation)
+  }
+  for (int i = t; i < POL_LANES * (s2 + s3); i += 256) h1[i] = 0.f;  // pads of h1/h2
+  __syncthreads();
+
+  const int l = t / POL_TPL, u0 = t % POL_TPL;
+  const int b = b0 + l;
+  {
+    float o[QH];
+    pol_layer<QH>(w1, s1, so + l * s1, (S + 3) >> 2, bb1, H1, u0, o, true);
+#pragma unroll
+    for (int q = 0; q < QH; ++q) if (u0 + POL_TPL * q < H1) h1[l * s2 + u0 + POL_TPL * q] = o[q];
   }
   __syncthreads();
-  const int b = b0 + lb;
-  for (int u = u0; u < H1; u += 16) {
-    float s = 0.f;
-    const float* w = W1 + (long long)u * S;
-    for (int j = 0; j < S; ++j) s = fmaf(w[j], so[lb * S + j], s);
-    sh1[lb * H1 + u] = tanhf(s + b1[u]);
+  {
+    float o[QH];
+    pol_layer<QH>(w2, s2, h1 + l * s2, (H1 + 3) >> 2, bb2, H2, u0, o, true);
+#pragma unroll
+    for (int q = 0; q < QH; ++q) if (u0 + POL_TPL * q < H2) h2[l * s3 + u0 + POL_TPL * q] = o[q];
   }
   __syncthreads();
-  for (int u = u0; u < H2; u += 16) {
-    float s = 0.f;
-    const float* w = W2 + (long long)u * H1;
-    for (int j = 0; j < H1; ++j) s = fmaf(w[j], sh1[lb * H1 + j], s);
-    sh2[lb * H2 + u] = tanhf(s + b2[u]);
-  }
-  __syncthreads();
-  if (b >= B) return;
-  for (int u = u0; u < A; u += 16) {
-    float s = 0.f;
-    const float* w = W3 + (long long)u * H2;
-    for (int j = 0; j < H2; ++j) s = fmaf(w[j], sh2[lb * H2 + j], s);
-    const float m = s + b3[u];  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
-    if (mean_out) mean_out[(long long)b * A + u] = m;
+  float o[QA];
+  pol_layer<QA>(w3, s3, h2 + l * s3, (H2 + 3) >> 2, bb3, A, u0, o, false);
+#pragma unroll
+  for (int q = 0; q < QA; ++q) {
+    const int u = u0 + POL_TPL * q;
+    if (u >= A || b >= p.B) continue;
+    const float m = o[q];  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
+    if (p.mean_out) p.mean_out[(long long)b * A + u] = m;
     double a_out;
-    if (eval_mode) {
+    if (p.eval_mode) {
       a_out = (double)m;
     } else {
       double n;
-      if (noise) {
-        n = noise[(long long)b * A + u];
+      if (p.noise) {
+        n = p.noise[(long long)b * A + u];
       } else {
-        // Box-Muller on one Philox block: pair p = u/2 yields normals for u = 2p, 2p+1
-        const int p = u >> 1;
-        const amx::u32x4 r =
-            amx::philox4x32_10({(uint32_t)b, ctr_lo, ((uint32_t)p << 8) | (ctr_hi & 0xffu), amx::kTagPolicy}, k0, k1);
+        // Box-Muller on one Philox block: pair u/2 yields the normals of u = 2p, 2p+1
+        const int pr = u >> 1;
+        const amx::u32x4 r = amx::philox4x32_10(
+            {(uint32_t)b, p.ctr_lo, ((uint32_t)pr << 8) | (p.ctr_hi & 0xffu), amx::kTagPolicy}, p.k0, p.k1);
         const double u1 = 1.0 - amx::u53(r.x, r.y);  // (0, 1]
         const double u2 = amx::u53(r.z, r.w);
         const double rad = sqrt(-2.0 * log(u1));
         const double ang = 6.283185307179586 * u2;
         n = (u & 1) ? rad * sin(ang) : rad * cos(ang);
       }
-      a_out = (double)m + nscale[u] * n;  // gaussian_mlp.py:102-103 (float32 + float64)
+      a_out = (double)m + p.nscale[u] * n;  // gaussian_mlp.py:102-103 (float32 mean + float64 noise)
     }
-    act[(long long)b * A + u] = a_out;
+    p.act[(long long)b * A + u] = a_out;
+    if (p.x0) xa_s[l * A + u] = (float)a_out;
+  }
+  if (!p.x0) return;
+  __syncthreads();
+  // fused amx_assemble_input (dynamics.py:225-227): the block's POL_LANES rows of x0 for every
+  // model, written row-contiguously (consecutive threads -> consecutive columns)
+  const float* mu_s = p.norm;
+  const float* sd_s = p.norm + S;
+  const float* mu_a = p.norm + 2 * S;
+  const float* sd_a = p.norm + 2 * S + A;
+  const int k0 = p.k0_pad;
+  for (int i = t; i < POL_LANES * k0; i += 256) {
+    const int ll = i / k0, j = i - ll * k0;
+    const int bb = b0 + ll;
+    if (bb >= p.B) continue;
+    float x = 0.f;
+    if (j < S) {
+      x = (so[ll * s1 + j] - mu_s[j]) / sd_s[j];
+    } else if (j < S + A) {
+      x = (xa_s[ll * A + j - S] - mu_a[j - S]) / sd_a[j - S];
+    }
+    for (int mm = 0; mm < p.M; ++mm) p.x0[mm * p.stride_m + (long long)bb * p.ldk + j] = x;
   }
 }
 
@@ -354,7 +481,15 @@ extern "C" int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long str
   a.num_steps = num_steps; a.done = done; a.disc = disc;
   a.cost_in = cost_in; a.ldc = ldc; a.nonfinite = nonfinite;
   a.S = ctx->S; a.M = ctx->M; a.B = B; a.term = ctx->term;
-  hipLaunchKernelGGL(k_step, lanes_grid(B), dim3(256), 0, (hipStream_t)stream, a);
+  const int nit = (ctx->S + 63) / 64;
+  switch (nit) {
+#define AMX_STEP_CASE(N) \
+  case N: hipLaunchKernelGGL(k_step<N>, lanes_grid(B), dim3(256), 0, (hipStream_t)stream, a); break;
+    AMX_STEP_CASE(1) AMX_STEP_CASE(2) AMX_STEP_CASE(3) AMX_STEP_CASE(4)
+    AMX_STEP_CASE(5) AMX_STEP_CASE(6) AMX_STEP_CASE(7) AMX_STEP_CASE(8)
+#undef AMX_STEP_CASE
+    default: AMX_CHECK_ARG(false, "amx_step: S=%d exceeds 512", ctx->S);
+  }
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -388,18 +523,36 @@ extern "C" int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* 
 extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* W1, const float* b1, int H1,
                               const float* W2, const float* b2, int H2, const float* W3, const float* b3,
                               const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
-                              int eval_mode, double* act, float* mean, void* stream) {
+                              int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
+                              void* stream) {
   AMX_CHECK_ARG(ctx && ob && W1 && b1 && W2 && b2 && W3 && b3 && act, "amx_policy_act: null pointer");
   AMX_CHECK_ARG(eval_mode || noise_scale, "amx_policy_act: noise_scale required unless eval_mode");
-  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH, "amx_policy_act: H1=%d H2=%d", H1, H2);
+  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH,
+                "amx_policy_act: H1=%d H2=%d A=%d (max %d)", H1, H2, ctx->A, POL_MAXH);
   AMX_CHECK_ARG(B >= 0, "amx_policy_act: B=%d", B);
+  AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
+                            (ctx->M == 1 || stride_m >= (long long)ldk * B)),
+                "amx_policy_act: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B");
   if (B == 0) return AMX_OK;
-  const size_t lds = sizeof(float) * POL_LANES * (ctx->S + H1 + H2);
-  AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S too large for LDS staging");
+  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
+  AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S/H too large for LDS staging (%zu B)", lds);
+  PolicyArgs p;
+  p.ob = ob; p.W1 = W1; p.b1 = b1; p.H1 = H1; p.W2 = W2; p.b2 = b2; p.H2 = H2; p.W3 = W3; p.b3 = b3;
+  p.nscale = noise_scale; p.noise = noise;
+  p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32); p.ctr_lo = (uint32_t)counter;
+  p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode;
+  p.act = act; p.mean_out = mean;
+  p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
+  p.S = ctx->S; p.A = ctx->A; p.B = B;
   dim3 grid((B + POL_LANES - 1) / POL_LANES);
-  hipLaunchKernelGGL(k_policy, grid, dim3(256), lds, (hipStream_t)stream, ob, W1, b1, H1, W2, b2, H2, W3, b3,
-                     noise_scale, noise, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)counter,
-                     (uint32_t)(counter >> 32), eval_mode, act, mean, ctx->S, ctx->A, B);
+  // outputs per thread, rounded up to a compiled width: hidden layers QH, action layer QA
+  const int qh = ((H1 > H2 ? H1 : H2) + POL_TPL - 1) / POL_TPL;
+  const int qa = (ctx->A + POL_TPL - 1) / POL_TPL;
+  hipStream_t st = (hipStream_t)stream;
+  if (qh <= 2 && qa <= 2) hipLaunchKernelGGL((k_policy<2, 2>), grid, dim3(256), lds, st, p);
+  else if (qh <= 2 && qa <= 3) hipLaunchKernelGGL((k_policy<2, 3>), grid, dim3(256), lds, st, p);
+  else if (qh <= 4 && qa <= 4) hipLaunchKernelGGL((k_policy<4, 4>), grid, dim3(256), lds, st, p);
+  else hipLaunchKernelGGL((k_policy<16, 16>), grid, dim3(256), lds, st, p);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

@@ -154,7 +154,8 @@ class DeviceEnsemble:
             self._ws[Bp] = ws
         return ws
 
-    def forward_preds(self, ob: torch.Tensor, act: torch.Tensor, B: int | None = None) -> torch.Tensor:
+    def forward_preds(self, ob: torch.Tensor, act: torch.Tensor, B: int | None = None,
+                      assembled: bool = False) -> torch.Tensor:
         """All members' un-normalised deltas for rows [0, B): returns preds [M, Bp, S] (view
         of the workspace; rows >= B are padding).  ob/act fp64 or fp32 on the device."""
         c = self.ctx
@@ -169,8 +170,9 @@ class DeviceEnsemble:
         Bp, buf, preds = ws["Bp"], ws["act"], ws["preds"]
         dt = N.AMX_IN_F64 if ob.dtype == torch.float64 else N.AMX_IN_F32
         s = c.stream
-        N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
-                                         c.ldk, B, s), "amx_assemble_input")
+        if not assembled:  # (the device policy can write x0 itself: amx_policy_act's fused assembly)
+            N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
+                                             c.ldk, B, s), "amx_assemble_input")
         self._mlp(buf, preds, Bp, s)
         return preds
 

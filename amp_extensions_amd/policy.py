@@ -54,12 +54,16 @@ class DevicePolicy:
         self.noise_scale = torch.from_numpy(np.exp(ls)).to(dev)
 
     def act(self, ob: torch.Tensor, B: int, out: torch.Tensor, counter: int, noise: torch.Tensor | None = None,
-            eval_mode: bool = False, mean_out: torch.Tensor | None = None) -> torch.Tensor:
+            eval_mode: bool = False, mean_out: torch.Tensor | None = None, x0: torch.Tensor | None = None
+            ) -> torch.Tensor:
+        """Actions of B lanes into `out` [B, A] f64.  `x0` (the ensemble workspace's activation
+        buffer [M, B_pad, ldk]) fuses the ensemble's input assembly into the same launch."""
         c = self.ctx
         N.check(c.lib.amx_policy_act(
             c.h, ob.data_ptr(), B, self.W[0].data_ptr(), self.b[0].data_ptr(), self.H1, self.W[1].data_ptr(),
             self.b[1].data_ptr(), self.H2, self.W[2].data_ptr(), self.b[2].data_ptr(), self.noise_scale.data_ptr(),
             None if noise is None else noise.data_ptr(), self.seed, int(counter) & 0xFFFFFFFFFFFFFFFF,
-            int(eval_mode), out.data_ptr(), None if mean_out is None else mean_out.data_ptr(), c.stream),
-            "amx_policy_act")
+            int(eval_mode), out.data_ptr(), None if mean_out is None else mean_out.data_ptr(),
+            None if x0 is None else x0.data_ptr(), 0 if x0 is None else x0.stride(0),
+            0 if x0 is None else x0.stride(1), c.stream), "amx_policy_act")
         return out

@@ -70,6 +70,8 @@ class RolloutEngine:
         self.model_idx = z(B, dt=torch.int32)
         self.reset_count = z(B, dt=torch.int32)
         self.reset_rows = z(K, B, dt=torch.int32)
+        # [s, s'] cost-input rows.  (A side-stream reward pass overlapping the next step's
+        # GEMMs was measured: no gain, the ensemble GEMMs already fill every CU — bench r1f.)
         self.cost_in = z(Bp, c.k_rff_pad)
         self.means = z(K, B, A) if record_means else None
         if isinstance(cost, RBFLinearCost):
@@ -124,6 +126,8 @@ class RolloutEngine:
         else:
             if self.policy is None:
                 raise RuntimeError("no policy and no actions given")
+            # (amx_policy_act can also write the ensemble's x0 rows itself, but measured slower
+            # than the separate row-per-wave assembly kernel: 36.5 vs 20.4 + 8.6 us at 8192 lanes)
             self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode,
                             mean_out=None if self.means is None else self.means[t])
         preds = self.ens.forward_preds(ob, act, B)
@@ -177,7 +181,7 @@ class RolloutEngine:
         # one fused all-reduce of [sum phi, count] across ranks (dist.feature_mean); the
         # fp64 mean is rounded to fp32 inside amx_mmd_fit (count passed as 1.0)
         mean = feature_mean(phi_sum, float(T * B), allreduce if allreduce is not None else (lambda t: t))
-        self.mb_mmd = cost.fit_w(mean.contiguous(), 1.0)
+        self.mb_mmd = cost.fit_w_device(mean.contiguous(), 1.0)  # device tensor: no host sync
         n = T * self.Bp
         N.check(c.lib.amx_mmd_reward(c.h, self.phi.data_ptr(), cost.feature_dim, cost.w.data_ptr(),
                                      cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),

@@ -126,8 +126,8 @@ def main():
 
     def one_rollout():
         eng.rollout(T)
+        eng.relabel(allreduce)  # MMD: feature mean + rewards; GAIL: joins the side-stream rewards
         if args.cost == "mmd":
-            eng.relabel(allreduce)
             cost.get_expert_cost()
         return T * B
 

@@ -271,6 +271,26 @@ def test_policy_action(amx, norms):
                                np.exp(np.float64(log_std.numpy())) * z, rtol=1e-12, atol=1e-12)
 
 
+def test_policy_fused_assembly_bit_exact(amx, norms):
+    """amx_policy_act's fused x0 rows == amx_assemble_input on the same (ob, act)."""
+    from amp_extensions_amd import _native as N
+    ctx, _, ens = make_ensemble(amx, [64] * 4, norms)
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    pol = amx.DevicePolicy(ctx, pw, log_std, seed=9)
+    B = 300
+    ob = torch.from_numpy(np.random.RandomState(1).randn(B, S)).to(DEV)
+    act = torch.empty(B, A, dtype=torch.float64, device=DEV)
+    ws = ens.workspace(B)
+    ws["act"].fill_(7.0)
+    pol.act(ob, B, act, counter=5, x0=ws["act"])
+    fused = ws["act"][:, :B, :ctx.k0_pad].clone()
+    ws["act"].fill_(-3.0)
+    N.check(ctx.lib.amx_assemble_input(ctx.h, ob.data_ptr(), act.data_ptr(), 0, ws["act"].data_ptr(),
+                                       ws["Bp"] * ctx.ldk, ctx.ldk, B, ctx.stream))
+    ref = ws["act"][:, :B, :ctx.k0_pad]
+    assert torch.equal(fused, ref)
+
+
 def test_rollout_matches_simenv_oracle(amx, norms):
     """End-to-end lanes vs per-lane SimEnvRef with the same actions and reset rows."""
     ctx, ens_w, ens = make_ensemble(amx, [512] * 4, norms)
@@ -326,7 +346,7 @@ def test_rollout_relabel_mmd(amx, norms):
     acts = eng.acts.cpu().numpy().reshape(-1, A)
     ref = R.RBFLinearCostRef(expert, feature_dim=512, bw_quantile=0.1, lambda_b=0.0025, seed=100)
     mmd = ref.fit_cost(torch.from_numpy(np.concatenate([obs, nxt], 1)).float())
-    np.testing.assert_allclose(info["mb_mmd"], mmd, rtol=1e-3)
+    np.testing.assert_allclose(float(info["mb_mmd"]), mmd, rtol=1e-3)
     disc_fn = lambda st, ac: R.compute_discrepancy(ens_w, norms, st, ac)
     cst, ci = ref.get_bonus_costs(torch.from_numpy(obs).float(), torch.from_numpy(acts).float(), disc_fn, thr,
                                   next_states=torch.from_numpy(nxt).float())
