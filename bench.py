@@ -43,6 +43,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
     p.add_argument("--cpu-samples", type=int, default=0)
+    p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     return p.parse_args()
 
 
@@ -92,10 +93,16 @@ def main():
     from amp_extensions_amd import synthetic as syn
     from amp_extensions_amd.policy import init_mlp_policy_params
 
+    # one rank per GPU; (local % device_count) only matters for a gloo rehearsal of several
+    # ranks on one card
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     allreduce = (lambda t: dist.all_reduce(t)) if world > 1 else None
 
     # ---- model + data setup (untimed) -------------------------------------------------------
