@@ -30,9 +30,13 @@ constexpr int LDS_LD = BK + 4;  // floats per LDS row
 
 enum { EPI_BIAS_ACT = 0, EPI_UNNORM = 1, EPI_RFF = 2 };
 
-template <int WM_, int WN_, int TM_, int TN_, int STAGES_ = 2, int OCC_ = 2>
+template <int WM_, int WN_, int TM_, int TN_, int STAGES_ = 2, int OCC_ = 2, bool PIPE_ = false>
 struct Tile {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_;
+  // PIPE: one wave per SIMD, software-pipelined: fragments of step v+1 are read while the
+  // MFMAs of step v run, and the next K-tile's LDS publish + barrier + first fragment read
+  // sit under the last MFMA group of the current tile.
+  static constexpr bool PIPE = PIPE_;
   static constexpr int STAGES = STAGES_;  // 2: double-buffered LDS, 1 barrier / K-tile;
                                           // 1: single buffer, 2 barriers / K-tile, half the LDS
   static constexpr int OCC = OCC_;        // __launch_bounds__ waves-per-SIMD target
@@ -60,6 +64,7 @@ struct GemmArgs {
   double* col_partials;    // EPI_RFF: [rows/128][N]
   const uint8_t* row_mask; // EPI_RFF: nullable
   int tiles_m, tiles_n, groups;
+  long long* clock_probe;  // internal diagnostics: per-WG {s_memtime, s_memrealtime} at start / end
 };
 
 // Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over
@@ -87,6 +92,11 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int g, tm, tn;
   map_tile(a, g, tm, tn);
+  long long clk0 = 0, rt0 = 0;
+  if (a.clock_probe) {
+    clk0 = (long long)__builtin_amdgcn_s_memtime();
+    rt0 = (long long)__builtin_amdgcn_s_memrealtime();
+  }
 
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const float* __restrict__ Wg = a.W + (long long)g * a.strideW + (long long)tn * BN * a.ldw;
@@ -129,6 +139,62 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
 
   const int a_off = (wm * TM * 32 + li) * LDS_LD + lh * 16;
   const int w_off = BM * LDS_LD + (wn * TN * 32 + li) * LDS_LD + lh * 16;
+  if constexpr (TL::PIPE) {
+    static_assert(TL::STAGES == 2, "PIPE needs the double buffer");
+    f32x4 fa[2][TM], fb[2][TN];
+    auto mfma_e = [&](int p, int e) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int n = 0; n < TN; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[p][m][e], fb[p][n][e], acc[m][n], 0, 0, 0);
+    };
+#pragma unroll
+    for (int m = 0; m < TM; ++m) fa[0][m] = *reinterpret_cast<const f32x4*>(smem + a_off + m * 32 * LDS_LD);
+#pragma unroll
+    for (int n = 0; n < TN; ++n) fb[0][n] = *reinterpret_cast<const f32x4*>(smem + w_off + n * 32 * LDS_LD);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
+#pragma unroll
+      for (int j = 0; j < VA; ++j) ra[j] = *reinterpret_cast<const f32x4*>(a_src + j * a_step + kn);
+#pragma unroll
+      for (int j = 0; j < VW; ++j) rw[j] = *reinterpret_cast<const f32x4*>(w_src + j * w_step + kn);
+      __builtin_amdgcn_sched_barrier(0);
+      const float* As = smem + cur * STAGE + a_off;
+      const float* Ws = smem + cur * STAGE + w_off;
+#pragma unroll
+      for (int v = 0; v < 3; ++v) {
+        const int p = v & 1;
+#pragma unroll
+        for (int m = 0; m < TM; ++m) fa[p ^ 1][m] = *reinterpret_cast<const f32x4*>(As + m * 32 * LDS_LD + (v + 1) * 4);
+#pragma unroll
+        for (int n = 0; n < TN; ++n) fb[p ^ 1][n] = *reinterpret_cast<const f32x4*>(Ws + n * 32 * LDS_LD + (v + 1) * 4);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mfma_e(p, e);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // step 3 (fragments in set 1): three MFMA groups, then publish the prefetched tile,
+      // barrier, read step 0 of the next tile into set 0, last MFMA group
+#pragma unroll
+      for (int e = 0; e < 3; ++e) mfma_e(1, e);
+      __builtin_amdgcn_sched_barrier(0);
+      const int nb = (cur ^ 1) * STAGE;
+#pragma unroll
+      for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + nb + j * RS * LDS_LD) = ra[j];
+#pragma unroll
+      for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + nb + j * RS * LDS_LD) = rw[j];
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < TM; ++m) fa[0][m] = *reinterpret_cast<const f32x4*>(smem + nb + a_off + m * 32 * LDS_LD);
+#pragma unroll
+      for (int n = 0; n < TN; ++n) fb[0][n] = *reinterpret_cast<const f32x4*>(smem + nb + w_off + n * 32 * LDS_LD);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_e(1, 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = (TL::STAGES == 2) ? (kt & 1) : 0;
     if constexpr (TL::STAGES == 1) {
@@ -178,8 +244,15 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
       __syncthreads();
     }
   }
+  }
   if constexpr (TL::STAGES == 1) __syncthreads();  // epilogues reuse the LDS
 
+  if (a.clock_probe && threadIdx.x == 0) {
+    long long* p = a.clock_probe + 4LL * blockIdx.x;
+    p[0] = clk0; p[1] = rt0;
+    p[2] = (long long)__builtin_amdgcn_s_memtime();
+    p[3] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
   // ---- epilogue ---------------------------------------------------------------------
   // C/D map of 32x32 f32 MFMA: column = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
   const int row0 = tm * BM + wm * TM * 32;
@@ -273,13 +346,16 @@ using T256x128 = Tile<4, 2, 2, 2>;    // 256x128, 512 threads, wave 64x64
 using T128x224 = Tile<4, 1, 1, 7>;    // 128x224, 256 threads, wave 32x224 (output layer, S <= 224)
 using T128s1 = Tile<2, 2, 2, 2, 1, 4>;    // 128x128, single-buffered LDS (37 KB): 4 WGs / CU
 using T128x256s1 = Tile<2, 4, 2, 2, 1, 2>;  // 128x256, 8 waves, single-buffered (55 KB): 2 WGs / CU
+using T256x128p = Tile<2, 2, 4, 2, 2, 1, true>;  // 256x128, 4 waves of 128x64, pipelined, 1 wave/SIMD
 
 int g_variant = -1;  // -1: automatic; >= 0 forces a tile for A/B tests (amx__set_gemm_variant)
+long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
 
 template <int EPI, class TL>
 int launch_tile(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
   a.tiles_n = a.N / TL::BN;
+  a.clock_probe = g_clock_probe;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
   hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
@@ -296,12 +372,13 @@ int launch_variant(int v, GemmArgs& a, hipStream_t s) {
     case 4: return launch_tile<EPI, T256x128>(a, s);
     case 5: return launch_tile<EPI, T128s1>(a, s);
     case 6: return launch_tile<EPI, T128x256s1>(a, s);
+    case 9: return launch_tile<EPI, T256x128p>(a, s);
     default: return launch_tile<EPI, T128>(a, s);
   }
 }
 
 bool variant_fits(int v, const GemmArgs& a) {
-  const int bm = (v == 3 || v == 4) ? 256 : 128;
+  const int bm = (v == 3 || v == 4 || v == 9) ? 256 : 128;
   const int bn = (v == 1 || v == 2 || v == 3 || v == 6) ? 256 : 128;
   return a.rows % bm == 0 && a.N % bn == 0;
 }
@@ -344,6 +421,14 @@ int check_common(const char* fn, int groups, int rows, int K, const float* A, in
 // Internal (not in the public header): force a tile variant for A/B measurements.
 extern "C" int amx__set_gemm_variant(int v) {
   g_variant = v;
+  return AMX_OK;
+}
+
+// Internal: device buffer of >= 4 * n_workgroups int64 receiving each workgroup's
+// {s_memtime, s_memrealtime} at start and at the end of its main loop (shader clock =
+// cycles / (realtime ticks / 100 MHz)); nullptr disables.
+extern "C" int amx__set_gemm_clock_probe(long long* buf) {
+  g_clock_probe = buf;
   return AMX_OK;
 }
 

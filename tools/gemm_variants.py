@@ -7,6 +7,7 @@ usage: python tools/gemm_variants.py [lanes] [S] [A]
 import ctypes
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -19,7 +20,7 @@ from amp_extensions_amd.ensemble import init_ensemble_weights  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 197
 A = int(sys.argv[3]) if len(sys.argv) > 3 else 36
-VARIANTS = [0, 2, 4, 5, 6]
+VARIANTS = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0, 4, 9]
 ROUNDS, REPS = 7, 5
 
 torch.manual_seed(0)
@@ -53,6 +54,33 @@ def alg_flops(i):
     Nalg = 512 if i < ctx.L else S
     return 2.0 * 4 * B * Nalg * Kalg
 
+
+# every variant must reproduce variant 0 bit for bit (same per-element k order)
+buf0 = buf.clone()
+ref = None
+for v in [0] + VARIANTS + ["auto"]:
+    setv(-1 if v == "auto" else v)
+    buf.copy_(buf0)
+    preds.zero_()
+    for i in range(ctx.L + 1):
+        layer(i)
+    torch.cuda.synchronize()
+    if ref is None:
+        ref = (buf.clone(), preds.clone())
+    else:
+        ok = torch.equal(buf, ref[0]) and torch.equal(preds, ref[1])
+        print(f"variant {v}: {'bit-exact vs variant 0' if ok else 'MISMATCH vs variant 0'}", flush=True)
+        if not ok:
+            raise SystemExit(1)
+
+# settle the clock: the chip ramps its clock over tens of ms of sustained MFMA load
+# (tools/mfma_ceiling.hip), so measure only after ~0.5 s of back-to-back work
+setv(-1)
+t_end = time.perf_counter() + 0.5
+while time.perf_counter() < t_end:
+    for i in range(ctx.L + 1):
+        layer(i)
+    torch.cuda.synchronize()
 
 res = {(v, i): [] for v in VARIANTS + ["auto"] for i in range(ctx.L + 1)}
 seq = {v: [] for v in VARIANTS + ["auto"]}

@@ -49,6 +49,11 @@ for v in VARIANTS:
     setv(v)
     rollout()
 torch.cuda.synchronize()
+setv(-1)
+t_end = time.perf_counter() + 0.5  # clock settle (tools/mfma_ceiling.hip)
+while time.perf_counter() < t_end:
+    rollout()
+    torch.cuda.synchronize()
 res = {v: [] for v in VARIANTS}
 for r in range(6):
     for v in VARIANTS:
