@@ -4,7 +4,8 @@ The gym_simenv learned-dynamics step (4-model dense-MLP ensemble), the MILO RFF-
 cost with the ensemble-disagreement bonus, the AMP/GAIL least-squares discriminator
 reward and the humanoid3d fall/horizon termination, as hand-written HIP kernels for
 gfx950 behind a C ABI (include/amx_hip.h, libamx_hip.so) and the reference's Python
-surfaces (SimEnv, sample_points, RBFLinearCost, GAILCost, DynamicsEnsemble).
+surfaces (SimEnv, sample_points, RBFLinearCost, GAILCost, DynamicsEnsemble), plus the
+sampler's consumer: returns, MLP value baseline and GAE (mjrl process_samples).
 
 The native library is loaded on first use; there is no CPU fallback.
 """
@@ -12,7 +13,7 @@ from .humanoid import TerminationConfig  # noqa: F401
 
 __all__ = [
     "AmxContext", "DeviceEnsemble", "RffMap", "RolloutEngine", "RBFLinearCost", "GAILCost", "DevicePolicy",
-    "TerminationConfig", "SimEnv", "BatchedSimEnv", "sample_points",
+    "TerminationConfig", "SimEnv", "BatchedSimEnv", "sample_points", "DeviceMLPBaseline", "process_samples",
 ]
 
 
@@ -32,6 +33,9 @@ def __getattr__(name):
     if name in ("SimEnv", "BatchedSimEnv"):
         from . import sim_env
         return getattr(sim_env, name)
+    if name in ("DeviceMLPBaseline", "process_samples"):
+        from . import gae
+        return getattr(gae, name)
     if name == "sample_points":
         from .sampler import sample_points
         return sample_points

@@ -44,6 +44,10 @@ SIGNATURES = {
     "amx_mmd_reward": (c_int, [vp, vp, c_int, vp, c_int, vp, c_flt, c_dbl, c_flt, c_flt, vp, vp, vp, c_int, vp]),
     "amx_expert_cost": (c_int, [vp, vp, c_int, vp, c_int, c_int, c_flt, c_flt, vp, vp]),
     "amx_amp_reward": (c_int, [vp, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
+    "amx_value_features": (c_int, [vp, c_int, c_int, vp, vp, vp, c_ll, vp, vp, c_int, vp, c_int, vp]),
+    "amx_value_head": (c_int, [vp, c_int, vp, c_int, c_int, vp, vp, vp, vp]),
+    "amx_gae": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, vp, c_ll, vp, c_dbl, c_dbl, vp, vp, vp]),
+    "amx_adv_whiten": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, c_dbl, vp, vp, vp]),
     "amx_philox": (c_int, [vp, c_u64, c_u32, c_u32, c_u32, vp, c_int, vp]),
 }
 

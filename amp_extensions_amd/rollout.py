@@ -67,6 +67,7 @@ class RolloutEngine:
         self.wbonus = z(K, Bp)
         self.nonfinite = z(K, B, dt=torch.uint8)
         self.num_steps = z(B, dt=torch.int32)
+        self.steps0 = z(B, dt=torch.int32)  # in-trajectory position of slot 0 (value features)
         self.model_idx = z(B, dt=torch.int32)
         self.reset_count = z(B, dt=torch.int32)
         self.reset_rows = z(K, B, dt=torch.int32)
@@ -120,6 +121,8 @@ class RolloutEngine:
         if t >= self.K:
             raise RuntimeError(f"rollout buffer full ({self.K} steps): call begin_rollout()")
         s = c.stream
+        if t == 0:
+            self.steps0.copy_(self.num_steps)
         ob, ob_next, act = self.obs[t], self.next_obs[t], self.acts[t]
         if actions is not None:
             act.copy_(actions)
@@ -188,6 +191,29 @@ class RolloutEngine:
                                      cost.lambda_b, cost.c_min, cost.c_max, self.rewards.data_ptr(),
                                      self.ipm.data_ptr(), self.wbonus.data_ptr(), n, c.stream), "amx_mmd_reward")
         return {"mb_mmd": self.mb_mmd}
+
+    def advantages(self, baseline, gamma: float = 0.995, gae_lambda=0.97, whiten: bool = False,
+                   eps: float = 1e-6) -> dict:
+        """Returns, baseline values and GAE advantages of the recorded steps
+        (process_samples.py:3-35 over the lane buffers): trajectories end at done flags
+        (terminated: bootstrap 0); a lane's trajectory still running at the end of the buffer
+        is bootstrapped with its last baseline value (mjrl's non-terminated rule).
+        `whiten` applies process_paths' (adv - mean) / (std + eps) (batch_reinforce.py:284-285).
+        All outputs are device tensors [T, B] (values f32, returns/advantages f64)."""
+        from .gae import gae_grid, whiten_grid
+        c, T, B = self.ctx, self.t, self.B
+        rows = T * B
+        obs = self.obs[:T].reshape(rows, c.S)
+        end = self.done[:T].reshape(rows)
+        v = baseline.predict_grid(rows, T, B, obs, c.S, end, B, t0=self.steps0)
+        ret = torch.empty(T, B, dtype=torch.float64, device=c.device)
+        adv = torch.empty_like(ret)
+        gae_grid(c, T, B, end, self.rewards, self.Bp, v, gamma, gae_lambda, B, ret, adv)
+        out = {"values": v[:rows].view(T, B), "returns": ret, "advantages": adv}
+        if whiten:
+            out["advantages_whitened"], out["adv_stats"] = whiten_grid(c, T, B, adv, B, eps=eps,
+                                                                       out=torch.empty_like(adv))
+        return out
 
     def bonus_mmd(self) -> float:
         """infos['bonus_mmd'] = mean(-rewards) - expert cost (batch_reinforce.py:169)."""

@@ -213,6 +213,52 @@ int amx_amp_reward(amx_ctx* ctx, const float* h, int ldh, int Hd, const float* w
                    const float* disc, double lambda_b, float* reward, float* logits, int n,
                    void* stream);
 
+/* ---- returns / value baseline / GAE (the sampler's consumer) ------------------ */
+
+/* Trajectory layout shared by the calls below ("segment grid"): L lanes of up to T
+ * rows.  Lane l owns rows r(t, l) = base[l] + t * stride for t < len[l] (base NULL ->
+ * base[l] = l; len NULL -> T).  end[r] closes a trajectory at row r: 0 = continues,
+ * 1 = terminated (bootstrap 0), 2 = ends without termination (bootstrap with the
+ * row's own baseline, mjrl's non-terminated rule); a lane's last row with end 0 is
+ * treated as 2.  t0[l] (NULL -> 0) is the position of the lane's first row inside its
+ * trajectory.  Engine buffers: base NULL, stride = lanes, end = done flags;
+ * concatenated mjrl paths: base = path offsets, stride = 1, end = 1/2 at path ends. */
+
+/* MLPBaseline._features (mjrl/mjrl/baselines/mlp_baseline.py:36-59): row r of feat
+ * [.., ldf] f32 = [clip(obs[r], -10, 10) / 10, (tpos/1000)^1..4, 0 ...] computed in
+ * fp64 and rounded to f32 (featmat.astype('float32'), :100); tpos = row position in
+ * its trajectory.  Columns [S + 4, kf) are zeroed, kf = round_up(S + 4, 32). */
+int amx_value_features(amx_ctx* ctx, int T, int L, const int32_t* len, const int32_t* t0,
+                       const int64_t* base, long long stride, const uint8_t* end,
+                       const double* obs, int ldo, float* feat, int ldf, void* stream);
+
+/* Last Linear(H -> 1) of the MLPBaseline model (mlp_baseline.py:20-27, predict :99-108):
+ * v[r] = b[0] + sum_k h[r][k] * w[k] (f32) for r < rows; H a multiple of 4. */
+int amx_value_head(amx_ctx* ctx, int rows, const float* h, int ldh, int H, const float* w,
+                   const float* b, float* v, void* stream);
+
+/* compute_returns + compute_advantages (mjrl/mjrl/utils/process_samples.py:3-45):
+ * per trajectory, in fp64 (numpy 1.21 promotion of the pinned reference env):
+ *   ret[t] = rew[t] + gamma * ret[t+1]                            (discount_sum)
+ *   GAE (gamma_lambda >= 0): delta[t] = (rew[t] + gamma * b1[t+1]) - b[t],
+ *        adv[t] = delta[t] + gamma_lambda * adv[t+1]; b1 = b + [0 | b[-1]] at the end;
+ *        delta is float64 for terminated trajectories and float32 arithmetic otherwise
+ *        (np.append keeps b1 float32 when the appended value is b[-1])
+ *   standard (gamma_lambda < 0): adv[t] = ret[t] - b[t].
+ * rew (f32) is read at rbase[l] + t * rstride (rbase NULL -> l); v, ret, adv use r(t, l).
+ * gamma_lambda = gamma * gae_lambda formed by the caller in double. */
+int amx_gae(amx_ctx* ctx, int T, int L, const int32_t* len, const int64_t* base, long long stride,
+            const uint8_t* end, const float* rew, const int64_t* rbase, long long rstride,
+            const float* v, double gamma, double gamma_lambda, double* ret, double* adv,
+            void* stream);
+
+/* Advantage whitening of BatchREINFORCE.process_paths (mjrl/mjrl/algos/batch_reinforce.py:
+ * 280-285): over the grid's rows, out = (adv - mean) / (std + eps) (population std);
+ * stats[0..1] = mean, std (fp64, fixed reduction order).  out may alias adv. */
+int amx_adv_whiten(amx_ctx* ctx, int T, int L, const int32_t* len, const int64_t* base,
+                   long long stride, const double* adv, double eps, double* out, double* stats,
+                   void* stream);
+
 /* ---- RNG ----------------------------------------------------------------------- */
 
 /* Philox4x32-10 block for (key = seed, counter = {ctr0, ctr1, ctr2, ctr3}), written

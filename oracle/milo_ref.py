@@ -569,3 +569,123 @@ def sample_points(ens, norms, pweights, log_std, num_to_collect: int, base_seed:
     for p, _ in results:
         paths.extend(p)
     return paths
+
+
+# --------------------------------------------------------------------------------------
+# returns / MLP value baseline / GAE — mjrl/mjrl/utils/process_samples.py:3-45,
+# mjrl/mjrl/baselines/mlp_baseline.py:10-108, mjrl/mjrl/algos/batch_reinforce.py:271-297
+# Promotion follows the reference's pinned numpy 1.21 (environment.yml): scalar float32 +
+# Python float -> float64, so discount_sum accumulates in float64 (its input is widened up
+# front; under numpy >= 2 / NEP 50 the same source would accumulate in float32).  Array-array
+# promotion is the same in both: a terminated path's b1 = append(b, 0.0) is float64 (so its
+# deltas are float64), a non-terminated path's b1 = append(b, b[-1]) stays float32 and so do
+# its deltas (float32 rewards + float32(gamma) * b1[1:] - b1[:-1]).
+# --------------------------------------------------------------------------------------
+
+
+def init_mlp_baseline(inp_dim: int, hidden=(128, 128), seed: int | None = None):
+    """MLPBaseline.model layers (mlp_baseline.py:20-27): Linear(n+4 -> h1) ReLU ... Linear(-> 1),
+    default torch init in layer order."""
+    if seed is not None:
+        torch.manual_seed(seed)
+    sizes = (inp_dim + 4,) + tuple(hidden) + (1,)
+    layers = [nn.Linear(sizes[i], sizes[i + 1]) for i in range(len(sizes) - 1)]
+    return [(l.weight.data.clone(), l.bias.data.clone()) for l in layers]
+
+
+def mlp_baseline_features(paths) -> np.ndarray:
+    """MLPBaseline._features (mlp_baseline.py:36-59) for inp='obs', as float32 (:100).  A path
+    may carry 't0' (engine lanes: a trajectory begun in an earlier rollout); mjrl paths
+    always start at 0."""
+    o = np.concatenate([p["observations"] for p in paths])
+    o = np.clip(o, -10, 10) / 10.0
+    N_, n = o.shape
+    feat = np.ones((N_, n + 4))
+    feat[:, :n] = o
+    k = 0
+    for p in paths:
+        l = len(p["rewards"])
+        al = (np.arange(l) + p.get("t0", 0)) / 1000.0
+        for j in range(4):
+            feat[k:k + l, -4 + j] = al ** (j + 1)
+        k += l
+    return feat.astype("float32")
+
+
+def mlp_baseline_predict(layers, feat: np.ndarray) -> np.ndarray:
+    """model(feat) (mlp_baseline.py:99-108): Linear/ReLU chain in fp32."""
+    x = torch.from_numpy(feat)
+    for i, (W, b) in enumerate(layers):
+        x = F.linear(x, W, b)
+        if i < len(layers) - 1:
+            x = torch.relu(x)
+    return x.detach().numpy().ravel()
+
+
+def discount_sum(x, gamma: float, terminal: float = 0.0) -> np.ndarray:
+    """process_samples.py:37-45 with numpy-1.21 scalar promotion (float64 accumulation)."""
+    x = np.asarray(x, dtype=np.float64)
+    y = []
+    run_sum = terminal
+    for t in range(len(x) - 1, -1, -1):
+        run_sum = x[t] + gamma * run_sum
+        y.append(run_sum)
+    return np.array(y[::-1])
+
+
+def compute_returns(paths, gamma: float) -> None:
+    """process_samples.py:3-5."""
+    for p in paths:
+        p["returns"] = discount_sum(p["rewards"], gamma)
+
+
+def compute_advantages(paths, predict, gamma: float, gae_lambda=None, normalize: bool = False) -> None:
+    """process_samples.py:7-35; `predict(path)` returns the path's baseline (float32)."""
+    if gae_lambda is None or gae_lambda < 0.0 or gae_lambda > 1.0:
+        for p in paths:
+            p["baseline"] = predict(p)
+            p["advantages"] = p["returns"] - p["baseline"]
+        if normalize:
+            alladv = np.concatenate([p["advantages"] for p in paths])
+            mean_adv, std_adv = alladv.mean(), alladv.std()
+            for p in paths:
+                p["advantages"] = (p["advantages"] - mean_adv) / (std_adv + 1e-8)
+    else:
+        for p in paths:
+            b = p["baseline"] = predict(p)
+            b1 = np.append(b, 0.0 if p["terminated"] else b[-1])
+            td = p["rewards"] + gamma * b1[1:] - b1[:-1]
+            p["advantages"] = discount_sum(td, gamma * gae_lambda)
+        if normalize:
+            alladv = np.concatenate([p["advantages"] for p in paths])
+            mean_adv, std_adv = alladv.mean(), alladv.std()
+            for p in paths:
+                p["advantages"] = (p["advantages"] - mean_adv) / (std_adv + 1e-8)
+
+
+def whiten_advantages(paths, eps: float = 1e-6):
+    """BatchREINFORCE.process_paths advantage whitening + return stats
+    (batch_reinforce.py:280-293)."""
+    adv = np.concatenate([p["advantages"] for p in paths])
+    adv = (adv - np.mean(adv)) / (np.std(adv) + eps)
+    # sum() of float32 scalars accumulates in float64 under numpy 1.21 (scalar promotion)
+    path_returns = [sum(np.asarray(p["rewards"], dtype=np.float64)) for p in paths]
+    return adv, [np.mean(path_returns), np.std(path_returns), np.amin(path_returns), np.amax(path_returns)]
+
+
+def lanes_to_paths(done: np.ndarray, rewards: np.ndarray, obs: np.ndarray, steps0: np.ndarray):
+    """Split rollout-engine lane buffers [T, B] into mjrl-style paths (test helper): a lane's
+    trajectory ends at a done flag (terminated) or at the end of the buffer (not
+    terminated).  Returns (paths, rows) with rows[i] = the (t, b) pairs of path i."""
+    T, B = done.shape
+    paths, rows = [], []
+    for b in range(B):
+        start = 0
+        for t in range(T):
+            if done[t, b] or t == T - 1:
+                ts = np.arange(start, t + 1)
+                paths.append(dict(observations=obs[ts, b], rewards=rewards[ts, b], terminated=bool(done[t, b]),
+                                  t0=int(steps0[b]) if start == 0 else 0))
+                rows.append((ts, b))
+                start = t + 1
+    return paths, rows

@@ -283,8 +283,69 @@ def main():
                         means=np.concatenate([p["agent_infos"]["mean"] for p in paths]),
                         terminated=np.array([p["terminated"] for p in paths]),
                         pol_w0=pol_w[0][0][:4, :8])
+    make_g9()
     print("[make_golden] wrote fixtures to", OUT)
     return 0
+
+
+def g9_paths(seed=9):
+    """Synthetic paths for G9: ragged lengths (incl. 1), observations beyond the +-10 clip,
+    one path not terminated; float32 rewards as the relabel leaves them."""
+    rs = np.random.RandomState(seed)
+    lens = [1, 5, 17, 40, 3, 64, 2, 9]
+    paths = []
+    for i, l in enumerate(lens):
+        obs = rs.randn(l, S) * 4.0
+        obs[:, 3] *= 6.0  # some |x| > 10
+        paths.append(dict(observations=obs, actions=np.zeros((l, A)), rewards=(rs.randn(l) * 0.3).astype(np.float32),
+                          terminated=(i != 3)))
+    return paths
+
+
+def make_g9():
+    """G9: returns / MLPBaseline / GAE / whitening (mjrl process_samples.py, mlp_baseline.py,
+    batch_reinforce.py:271-297), run through the reference code.  The reference pins numpy
+    1.21 (environment.yml), where a float32 scalar + Python float promotes to float64, so
+    discount_sum accumulates in float64; numpy >= 2 here (NEP 50) would keep float32.  To
+    record the pinned behaviour, discount_sum's input is widened to float64 (exact) before the
+    reference loop runs, and process_paths sums path rewards as float64 for the same reason.
+    Array-array arithmetic (the float32 deltas of non-terminated paths, whose b1 stays
+    float32) promotes identically in both numpy versions and is left as is."""
+    import copy
+    import mjrl.utils.process_samples as ps
+    from mjrl.algos.batch_reinforce import BatchREINFORCE
+    from mjrl.baselines.mlp_baseline import MLPBaseline
+
+    torch.manual_seed(500)
+    bl = MLPBaseline(inp_dim=S, hidden_sizes=(128, 128))
+    layers = [(m.weight.detach().numpy(), m.bias.detach().numpy()) for m in bl.model if isinstance(m, torch.nn.Linear)]
+    paths = g9_paths()
+    out = {}
+    orig_discount_sum = ps.discount_sum
+    ps.discount_sum = lambda x, gamma, terminal=0.0: orig_discount_sum(np.asarray(x, dtype=np.float64), gamma,
+                                                                      terminal)
+    for mode, lam in (("gae", 0.97), ("std", None)):
+        pp = copy.deepcopy(paths)
+        ps.compute_returns(pp, 0.995)
+        ps.compute_advantages(pp, bl, 0.995, lam)
+        out[f"returns_{mode}"] = np.concatenate([p["returns"] for p in pp])
+        out[f"baseline_{mode}"] = np.concatenate([p["baseline"] for p in pp])
+        out[f"adv_{mode}"] = np.concatenate([p["advantages"] for p in pp])
+        if mode == "gae":
+            stub = types.SimpleNamespace(running_score=None)
+            pp64 = [dict(p, rewards=p["rewards"].astype(np.float64)) for p in pp]
+            _, _, adv_w, base_stats, _ = BatchREINFORCE.process_paths(stub, pp64)
+            out["adv_whitened"] = adv_w
+            out["base_stats"] = np.array(base_stats, dtype=np.float64)
+    feat = bl._features(paths).astype(np.float32)
+    out["features_head"], out["features_time"] = feat[:, :8], feat[:, -4:]
+    np.savez_compressed(os.path.join(OUT, "g9_gae.npz"), seed=9, baseline_seed=500, gamma=0.995, gae_lambda=0.97,
+                        lengths=np.array([len(p["rewards"]) for p in paths]),
+                        terminated=np.array([p["terminated"] for p in paths]),
+                        observations=np.concatenate([p["observations"] for p in paths]),
+                        rewards=np.concatenate([p["rewards"] for p in paths]),
+                        w0_head=layers[0][0][:4, :8], w2=layers[2][0], **out)
+    ps.discount_sum = orig_discount_sum
 
 
 if __name__ == "__main__":

@@ -174,3 +174,43 @@ def test_philox_known_answers():
 def test_policy_noise_is_standard_normal():
     z = R.policy_noise(seed=1234, counter=7, B=4096, A=28)
     assert abs(z.mean()) < 0.01 and abs(z.std() - 1.0) < 0.01
+
+
+# ---- G9: returns / MLP baseline / GAE / whitening (mjrl process_samples, mlp_baseline) ----
+def g9_paths(g):
+    lens, term = g["lengths"], g["terminated"]
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    return [dict(observations=g["observations"][o:o + l], rewards=g["rewards"][o:o + l], terminated=bool(t),
+                 actions=np.zeros((l, A))) for o, l, t in zip(offs, lens, term)]
+
+
+def test_g9_baseline_features_and_predict(golden):
+    g = golden("g9_gae.npz")
+    layers = R.init_mlp_baseline(S, (128, 128), seed=int(g["baseline_seed"]))
+    np.testing.assert_array_equal(layers[0][0].numpy()[:4, :8], g["w0_head"])
+    np.testing.assert_array_equal(layers[2][0].numpy(), g["w2"])
+    paths = g9_paths(g)
+    feat = R.mlp_baseline_features(paths)
+    np.testing.assert_array_equal(feat[:, :8], g["features_head"])
+    np.testing.assert_array_equal(feat[:, -4:], g["features_time"])
+    assert feat[:, 3].max() == 1.0 and feat[:, 3].min() == -1.0  # the clip is exercised
+    v = R.mlp_baseline_predict(layers, feat)
+    close(v, g["baseline_gae"])
+
+
+@pytest.mark.parametrize("mode,lam", [("gae", 0.97), ("std", None)])
+def test_g9_returns_advantages(golden, mode, lam):
+    g = golden("g9_gae.npz")
+    paths = g9_paths(g)
+    base = g[f"baseline_{mode}"]
+    offs = np.concatenate([[0], np.cumsum(g["lengths"])])
+    by_id = {id(p): base[offs[i]:offs[i + 1]] for i, p in enumerate(paths)}
+    R.compute_returns(paths, float(g["gamma"]))
+    R.compute_advantages(paths, lambda p: by_id[id(p)], float(g["gamma"]), lam)
+    # fp64 algebra in the reference's order: bit-exact given the same baseline values
+    np.testing.assert_array_equal(np.concatenate([p["returns"] for p in paths]), g[f"returns_{mode}"])
+    np.testing.assert_array_equal(np.concatenate([p["advantages"] for p in paths]), g[f"adv_{mode}"])
+    if mode == "gae":
+        adv_w, stats = R.whiten_advantages(paths)
+        np.testing.assert_array_equal(adv_w, g["adv_whitened"])
+        np.testing.assert_array_equal(np.array(stats), g["base_stats"])
