@@ -66,6 +66,7 @@ def install_stubs():
     tkm = types.ModuleType("tkinter.messagebox")
     tkm.NO = "no"
     tk.messagebox = tkm
+    tk.E = "e"  # unused `from tkinter import E` of milo/milo/utils.py:1
     sys.modules["tkinter"], sys.modules["tkinter.messagebox"] = tk, tkm
     tb = types.ModuleType("torch.utils.tensorboard")
     tb.SummaryWriter = object
@@ -284,6 +285,7 @@ def main():
                         terminated=np.array([p["terminated"] for p in paths]),
                         pol_w0=pol_w[0][0][:4, :8])
     make_g9()
+    make_g10()
     print("[make_golden] wrote fixtures to", OUT)
     return 0
 
@@ -350,3 +352,57 @@ def make_g9():
 
 if __name__ == "__main__":
     sys.exit(main())
+
+
+def g10_dbs(seed=10):
+    """Synthetic trajectory databases in the reference's on-disk layout (collect_data.py /
+    collect_expert.py): offline [{'episode': (states, actions, rewards), 'dtw_cost', 'ep_rew'}],
+    expert [{'episode': states}], numpy arrays as the collectors save them."""
+    rs = np.random.RandomState(seed)
+    offline = []
+    for T in (5, 1, 12, 7):
+        offline.append({"episode": (rs.randn(T + 1, S), rs.randn(T, A).astype(np.float32), rs.randn(T)),
+                        "dtw_cost": float(rs.rand()), "ep_rew": np.float64(rs.randn())})
+    expert = [{"episode": rs.randn(T + 1, S)} for T in (4, 9, 2)]
+    return offline, expert
+
+
+def make_g10():
+    """G10: milo/milo/utils.py get_db_mjrl / get_paths_mjrl / convert_to_veltopos on files
+    written with torch.save, read back by the reference loaders (torch.load under an
+    allow-list of numpy's reconstructors: torch >= 2.6 defaults to weights_only)."""
+    import tempfile
+    import milo.utils as U
+    from amp_extensions_amd.datasets import _numpy_safe_globals
+
+    offline, expert = g10_dbs()
+    out = {}
+    with tempfile.TemporaryDirectory() as d, torch.serialization.safe_globals(_numpy_safe_globals()):
+        fo, fe = os.path.join(d, "offline.pt"), os.path.join(d, "expert.pt")
+        torch.save(offline, fo)
+        torch.save(expert, fe)
+        for tag, kw in (("amp", dict(imitate_amp=True)), ("rew", dict(imitate_amp=False)),
+                        ("n2", dict(num_trajs=2)), ("idx", dict(idx=2, num_trajs="all"))):
+            if tag == "idx":
+                continue  # utils.py:253 iterates the selected dict's keys (crashes): not recorded
+            s_, a_, s2_ = U.get_db_mjrl(fo, **kw)
+            out[f"db_{tag}_s"], out[f"db_{tag}_a"], out[f"db_{tag}_s2"] = s_.numpy(), a_.numpy(), s2_.numpy()
+        es, es2 = U.get_db_mjrl(fe, expert=True)
+        out["ex_s"], out["ex_s2"] = es.numpy(), es2.numpy()
+        paths = U.get_paths_mjrl(fo, idx=1)
+        out["paths_idx1_obs"], out["paths_idx1_act"] = paths[0]["observations"], paths[0]["actions"]
+        paths = U.get_paths_mjrl(fe, expert=True)
+        out["paths_ex_nobs"] = np.concatenate([p["next_observation"] for p in paths])
+
+        class Core:
+            def get_vel_offset(self):
+                return 136
+
+            def get_agent_update_rate(self):
+                return 30
+
+        x = U.convert_to_veltopos(fo, Core(), False, False)
+        out["v2p_offline"] = np.concatenate([t["episode"][0] for t in x])
+        x = U.convert_to_veltopos(fe, Core(), False, True)
+        out["v2p_expert"] = np.concatenate([t["episode"] for t in x])
+    np.savez_compressed(os.path.join(OUT, "g10_db.npz"), seed=10, **out)

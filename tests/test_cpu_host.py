@@ -97,3 +97,64 @@ def test_product_package_never_imports_oracle():
                 src = open(os.path.join(dp, f)).read()
                 assert "import oracle" not in src and "from oracle" not in src, f
     assert os.path.isdir(os.path.join(root, "oracle"))
+
+
+# ---- on-disk trajectory databases (milo/milo/utils.py:222-305) vs the reference (G10) -------
+def _g10_dbs():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_golden", os.path.join(os.path.dirname(__file__), "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg.g10_dbs()
+
+
+def test_db_loaders_match_reference(golden, tmp_path):
+    import numpy as np
+    import torch
+    from amp_extensions_amd import datasets as D
+    g = golden("g10_db.npz")
+    offline, expert = _g10_dbs()
+    fo, fe = str(tmp_path / "offline.pt"), str(tmp_path / "expert.pt")
+    torch.save(offline, fo)
+    torch.save(expert, fe)
+    for tag, kw in (("amp", dict(imitate_amp=True)), ("rew", dict(imitate_amp=False)), ("n2", dict(num_trajs=2))):
+        s, a, s2 = D.get_db_mjrl(fo, verbose=False, **kw)
+        for x, k in ((s, "s"), (a, "a"), (s2, "s2")):
+            assert x.dtype == torch.float32
+            np.testing.assert_array_equal(x.numpy(), g[f"db_{tag}_{k}"])
+    es, es2 = D.get_db_mjrl(fe, expert=True)
+    np.testing.assert_array_equal(es.numpy(), g["ex_s"])
+    np.testing.assert_array_equal(es2.numpy(), g["ex_s2"])
+    p = D.get_paths_mjrl(fo, idx=1)
+    assert len(p) == 1
+    np.testing.assert_array_equal(p[0]["observations"], g["paths_idx1_obs"])
+    np.testing.assert_array_equal(p[0]["actions"], g["paths_idx1_act"])
+    p = D.get_paths_mjrl(fe, expert=True)
+    np.testing.assert_array_equal(np.concatenate([q["next_observation"] for q in p]), g["paths_ex_nobs"])
+    x = D.convert_to_veltopos(fo, vel_offset=136, dt=1 / 30)
+    np.testing.assert_array_equal(np.concatenate([t["episode"][0] for t in x]), g["v2p_offline"])
+    x = D.convert_to_veltopos(fe, is_expert=True, vel_offset=136, dt=1 / 30)
+    np.testing.assert_array_equal(np.concatenate([t["episode"] for t in x]), g["v2p_expert"])
+    # idx on get_db_mjrl selects one trajectory (the reference iterates that dict's keys)
+    s, a, s2 = D.get_db_mjrl(fo, idx=2, verbose=False)
+    T = offline[2]["episode"][1].shape[0]
+    assert s.shape == (T, offline[2]["episode"][0].shape[1]) and a.shape[0] == T
+
+
+def test_db_loader_refuses_arbitrary_callables(tmp_path):
+    import pickle
+
+    import pytest
+    import torch
+    from amp_extensions_amd import datasets as D
+
+    class Evil:
+        def __reduce__(self):
+            return (print, ("should not run",))
+
+    f = tmp_path / "evil.pt"
+    torch.save([{"episode": Evil()}], str(f), pickle_module=pickle)
+    with pytest.raises(Exception):
+        D.load_db(str(f))
