@@ -72,9 +72,8 @@ struct GemmArgs {
 // run of logical tiles (tile_n fastest: consecutive tiles reuse the same A row panel;
 // then tile_m: they reuse the same weight panels of one ensemble member).  Bijective for
 // any tile count (cdna_hip_programming.md T1).
-__device__ inline void map_tile(const GemmArgs& a, int& g, int& tm, int& tn) {
+__device__ inline void map_tile(const GemmArgs& a, int orig, int& g, int& tm, int& tn) {
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
-  const int orig = blockIdx.x;
   const int xcd = orig & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
@@ -85,13 +84,14 @@ __device__ inline void map_tile(const GemmArgs& a, int& g, int& tm, int& tn) {
   g = rest / a.tiles_m;
 }
 
+// One output tile (linear id `orig`, see map_tile) of the grouped GEMM.
 template <int EPI, class TL>
-__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
+__device__ __forceinline__ void gemm_tile(const GemmArgs& a, int orig) {
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW;
   constexpr int STAGE = TL::STAGE, RS = TL::ROW_STEP;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int g, tm, tn;
-  map_tile(a, g, tm, tn);
+  map_tile(a, orig, g, tm, tn);
   long long clk0 = 0, rt0 = 0;
   if (a.clock_probe) {
     clk0 = (long long)__builtin_amdgcn_s_memtime();
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
   if constexpr (TL::STAGES == 1) __syncthreads();  // epilogues reuse the LDS
 
   if (a.clock_probe && threadIdx.x == 0) {
-    long long* p = a.clock_probe + 4LL * blockIdx.x;
+    long long* p = a.clock_probe + 4LL * orig;
     p[0] = clk0; p[1] = rt0;
     p[2] = (long long)__builtin_amdgcn_s_memtime();
     p[3] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -337,6 +337,18 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
   }
 }
 
+// Grid = one workgroup per tile, or (persistent) fewer workgroups that each loop over tiles
+// id = blockIdx.x + j * gridDim.x (gridDim.x a multiple of 8 keeps every id on the XCD that
+// map_tile assigns it to): the epilogue stores of one tile then overlap the next tile's loads.
+template <int EPI, class TL>
+__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
+  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+  for (int id = blockIdx.x; id < nwg; id += gridDim.x) {
+    if (id != (int)blockIdx.x) __syncthreads();  // previous tile's last LDS reads are done
+    gemm_tile<EPI, TL>(a, id);
+  }
+}
+
 // ---- tile selection -------------------------------------------------------------------------
 using T128 = Tile<2, 2, 2, 2>;        // 128x128, 256 threads, 2 WGs / CU
 using T128x256 = Tile<2, 2, 2, 4>;    // 128x256, 256 threads, wave 64x128
@@ -349,6 +361,22 @@ using T128x256s1 = Tile<2, 4, 2, 2, 1, 2>;  // 128x256, 8 waves, single-buffered
 using T256x128p = Tile<2, 2, 4, 2, 2, 1, true>;  // 256x128, 4 waves of 128x64, pipelined, 1 wave/SIMD
 
 int g_variant = -1;  // -1: automatic; >= 0 forces a tile for A/B tests (amx__set_gemm_variant)
+int g_persistent = 0;  // amx__set_gemm_persistent: loop workgroups over tiles (A/B)
+int g_cus = 0;         // compute units of the current device (queried once)
+
+int resident_wgs(size_t lds, int nt, int occ) {
+  if (g_cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      g_cus = prop.multiProcessorCount;
+    if (g_cus <= 0) g_cus = 256;
+  }
+  const int by_lds = (int)((160 * 1024) / lds);
+  const int by_waves = (occ * 4) / (nt / 64);
+  const int per_cu = by_lds < by_waves ? by_lds : by_waves;
+  return (per_cu < 1 ? 1 : per_cu) * g_cus;
+}
 long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
 
 template <int EPI, class TL>
@@ -358,7 +386,12 @@ int launch_tile(GemmArgs& a, hipStream_t stream) {
   a.clock_probe = g_clock_probe;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  int grid = nwg;
+  if (g_persistent && EPI != EPI_RFF) {
+    const int slots = resident_wgs(TL::LDS, TL::NT, TL::OCC) / 8 * 8;
+    if (slots >= 8 && slots < nwg) grid = slots;
+  }
+  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(grid), dim3(TL::NT), TL::LDS, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -395,10 +428,12 @@ int launch_gemm(int epi, GemmArgs& a, hipStream_t stream) {
     const int v = (g_variant >= 0 && variant_fits(g_variant, a)) ? g_variant : 0;
     return launch_variant<EPI_UNNORM>(v, a, stream);
   }
-  // automatic: 256x128 with 8 waves of 64x64 (one WG per CU, 110 KB LDS) when rows allow:
-  // +1-2% over 128x128 both per layer (tools/gemm_variants.py) and on the whole rollout
-  // (tools/rollout_ab.py, same process); single-buffered and 256-wide tiles measured slower.
-  int v = g_variant < 0 ? 4 : g_variant;
+  // automatic: 128x128, 4 waves of 64x64, two WGs per CU.  Its main loop keeps the MFMA
+  // pipe busy 93-95% of cycles (tools/gemm_clock.py) and is then power-limited (the chip
+  // holds 2.1-2.3 GHz under it); the 1-WG/CU tiles (256x128, 128x256, 256x256, pipelined
+  // one-wave-per-SIMD) run at 2.38 GHz but only 82-87% busy.  Net, across four boxes:
+  // 128x128 ahead by 4% on two, behind by 1.5% on two (tools/gemm_variants.py, same process).
+  int v = g_variant < 0 ? 0 : g_variant;
   if (!variant_fits(v, a)) v = 0;
   return launch_variant<EPI_BIAS_ACT>(v, a, stream);
 }
@@ -424,7 +459,13 @@ extern "C" int amx__set_gemm_variant(int v) {
   return AMX_OK;
 }
 
-// Internal: device buffer of >= 4 * n_workgroups int64 receiving each workgroup's
+// Internal: persistent workgroups (1) or one workgroup per tile (0), for A/B measurements.
+extern "C" int amx__set_gemm_persistent(int on) {
+  g_persistent = on;
+  return AMX_OK;
+}
+
+// Internal: device buffer of >= 4 * n_tiles int64 receiving each workgroup's
 // {s_memtime, s_memrealtime} at start and at the end of its main loop (shader clock =
 // cycles / (realtime ticks / 100 MHz)); nullptr disables.
 extern "C" int amx__set_gemm_clock_probe(long long* buf) {

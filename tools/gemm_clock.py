@@ -25,7 +25,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 VARIANTS = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "0,4").split(",")]
 S, A = 197, 36
 # variant -> (BM, BN, co-resident WGs per CU) for the hidden layers
-TILES = {0: (128, 128, 2), 4: (256, 128, 1), 9: (256, 128, 1), -1: (256, 128, 1)}
+TILES = {0: (128, 128, 2), 1: (128, 256, 1), 3: (256, 256, 1), 4: (256, 128, 1), 9: (256, 128, 1), -1: (128, 128, 2)}
 
 torch.manual_seed(0)
 norms = [torch.zeros(S), torch.ones(S), torch.zeros(A), torch.ones(A), torch.zeros(S), torch.ones(S)]

@@ -20,7 +20,7 @@ from amp_extensions_amd.ensemble import init_ensemble_weights  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 197
 A = int(sys.argv[3]) if len(sys.argv) > 3 else 36
-VARIANTS = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0, 4, 9]
+VARIANTS = sys.argv[4].split(",") if len(sys.argv) > 4 else ["0", "4", "9"]
 ROUNDS, REPS = 7, 5
 
 torch.manual_seed(0)
@@ -28,8 +28,17 @@ norms = [torch.zeros(S), torch.ones(S), torch.zeros(A), torch.ones(A), torch.zer
 ctx = amx.AmxContext(S, A, 4, 512, 4, 512, device="cuda")
 ens = amx.DeviceEnsemble(ctx, init_ensemble_weights(S, A, [512] * 4, 4, 100), norms)
 lib = ctx.lib
-setv = lib.amx__set_gemm_variant
-setv.argtypes = [ctypes.c_int]
+_setv = lib.amx__set_gemm_variant
+_setv.argtypes = [ctypes.c_int]
+lib.amx__set_gemm_persistent.argtypes = [ctypes.c_int]
+
+def setv(v):
+    """'4' -> tile variant 4; a trailing 'p' -> persistent workgroups; 'auto'/'-1' -> automatic."""
+    s = str(v)
+    lib.amx__set_gemm_persistent(int(s.endswith("p")))
+    s = s.rstrip("p")
+    _setv(-1 if s in ("auto", "-1", "") else int(s))
+
 ws = ens.workspace(B)
 Bp, buf, preds = ws["Bp"], ws["act"], ws["preds"]
 buf.normal_()
@@ -58,8 +67,8 @@ def alg_flops(i):
 # every variant must reproduce variant 0 bit for bit (same per-element k order)
 buf0 = buf.clone()
 ref = None
-for v in [0] + VARIANTS + ["auto"]:
-    setv(-1 if v == "auto" else v)
+for v in ["0"] + VARIANTS + ["auto"]:
+    setv(v)
     buf.copy_(buf0)
     preds.zero_()
     for i in range(ctx.L + 1):
@@ -87,7 +96,7 @@ seq = {v: [] for v in VARIANTS + ["auto"]}
 for r in range(ROUNDS):
     # whole-forward sequence per variant (what the rollout runs)
     for v in VARIANTS + ["auto"]:
-        setv(-1 if v == "auto" else v)
+        setv(v)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(REPS):
@@ -97,7 +106,7 @@ for r in range(ROUNDS):
         torch.cuda.synchronize()
         seq[v].append(e0.elapsed_time(e1) / REPS * 1e-3)
     for v in VARIANTS + ["auto"]:
-        setv(-1 if v == "auto" else v)
+        setv(v)
         for i in range(ctx.L + 1):
             layer(i)  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

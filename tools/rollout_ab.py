@@ -20,7 +20,7 @@ from amp_extensions_amd.ensemble import init_ensemble_weights  # noqa: E402
 from amp_extensions_amd.policy import init_mlp_policy_params  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-VARIANTS = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "-1,0,2,4").split(",")]
+VARIANTS = (sys.argv[2] if len(sys.argv) > 2 else "-1,-1p,0,4").split(",")
 S, A = 197, 36
 dev = torch.device("cuda", 0)
 s, a, s2 = syn.offline(20000, S, A, 0)
@@ -35,8 +35,18 @@ pol = amx.DevicePolicy(ctx, pw, ls, seed=1)
 T = math.ceil(40000 / B)
 eng = amx.RolloutEngine(ens, syn.reset_table(65536, S, 1), lanes=B, policy=pol, cost=cost, seed=7, max_steps=T)
 eng.reset_all()
-setv = ctx.lib.amx__set_gemm_variant
-setv.argtypes = [ctypes.c_int]
+lib = ctx.lib
+_setv = lib.amx__set_gemm_variant
+_setv.argtypes = [ctypes.c_int]
+lib.amx__set_gemm_persistent.argtypes = [ctypes.c_int]
+
+def setv(v):
+    """'4' -> tile variant 4; a trailing 'p' -> persistent workgroups; 'auto'/'-1' -> automatic."""
+    s = str(v)
+    lib.amx__set_gemm_persistent(int(s.endswith("p")))
+    s = s.rstrip("p")
+    _setv(-1 if s in ("auto", "-1", "") else int(s))
+
 
 
 def rollout():
@@ -67,5 +77,5 @@ for r in range(6):
 setv(-1)
 print(f"lanes {B}: ms per {T * B}-sample rollout (median / min of 6 rounds x 4)")
 for v in VARIANTS:
-    print(f"variant {v:3d}: {np.median(res[v]) * 1e3:7.3f} {np.min(res[v]) * 1e3:7.3f}  -> "
+    print(f"variant {v:>4s}: {np.median(res[v]) * 1e3:7.3f} {np.min(res[v]) * 1e3:7.3f}  -> "
           f"{T * B / np.median(res[v]) / 1e6:.3f} M env-steps/s")
