@@ -274,15 +274,22 @@ __host__ __device__ inline int pol_stride(int k) {  // row stride (floats) for a
   return (r % 8 == 0) ? r + 4 : r;
 }
 
+// Packed weight image (amx_policy_pack): [W1 H1 x s1 | W2 H2 x s2 | W3 A x s3 | b1 | b2 | b3],
+// zero-padded rows, total rounded to whole float4s.  The action kernel copies it into LDS
+// as is.
+__host__ __device__ inline int pol_blob_floats(int S, int H1, int H2, int A) {
+  const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
+  return (H1 * s1 + H2 * s2 + A * s3 + H1 + H2 + A + 3) & ~3;
+}
+
 __host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A) {
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
-  const size_t fl = (size_t)H1 * s1 + H2 * s2 + A * s3 + H1 + H2 + A + POL_LANES * (s1 + s2 + s3 + A);
+  const size_t fl = (size_t)pol_blob_floats(S, H1, H2, A) + POL_LANES * (s1 + s2 + s3 + A);
   return fl * sizeof(float);
 }
 
 struct PolicyArgs {
-  const double* ob; const float* W1; const float* b1; int H1; const float* W2; const float* b2; int H2;
-  const float* W3; const float* b3; const double* nscale; const double* noise;
+  const double* ob; const float* blob; int H1; int H2; const double* nscale; const double* noise;
   uint32_t k0, k1, ctr_lo, ctr_hi; int eval_mode;
   double* act; float* mean_out;
   float* x0; long long stride_m; int ldk; int k0_pad; int M; const float* norm;
@@ -290,6 +297,52 @@ struct PolicyArgs {
 };
 
 typedef float pf4 __attribute__((ext_vector_type(4)));
+
+constexpr int POL_STAGE_W = 12;  // float4 loads of the weight image per thread per pass
+constexpr int POL_STAGE_O = 16;  // double loads of observations per thread per pass
+
+// zero the pad columns [cols, ds) of rows [0, rows)
+__device__ inline void pol_zero_pads(float* __restrict__ dst, int ds, int cols, int rows) {
+  const int w = ds - cols;
+  for (int i = threadIdx.x; i < rows * w; i += 256) dst[(i / w) * ds + cols + i % w] = 0.f;
+}
+
+// One pass issues every global load (weight image float4s, observation doubles) before
+// any LDS store: the staging costs one memory round trip instead of one per array.
+__device__ inline void pol_stage_all(float* __restrict__ img, const float* __restrict__ blob, int n4,
+                                     float* __restrict__ so, int s1, const double* __restrict__ ob, int n_ob,
+                                     int S) {
+  const int t = threadIdx.x;
+  for (int it = 0;; ++it) {
+    const int w0 = t + it * 256 * POL_STAGE_W, o0 = t + it * 256 * POL_STAGE_O;
+    if (w0 >= n4 && o0 >= n_ob) break;
+    pf4 wv[POL_STAGE_W];
+    double ov[POL_STAGE_O];
+#pragma unroll
+    for (int u = 0; u < POL_STAGE_W; ++u) {
+      const int i = w0 + u * 256;
+      if (i < n4) wv[u] = reinterpret_cast<const pf4*>(blob)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < POL_STAGE_O; ++u) {
+      const int i = o0 + u * 256;
+      if (i < n_ob) ov[u] = ob[i];
+    }
+#pragma unroll
+    for (int u = 0; u < POL_STAGE_W; ++u) {
+      const int i = w0 + u * 256;
+      if (i < n4) reinterpret_cast<pf4*>(img)[i] = wv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < POL_STAGE_O; ++u) {
+      const int i = o0 + u * 256;
+      if (i < n_ob) {
+        const int r = i / S, c = i - r * S;
+        so[r * s1 + c] = (float)ov[u];  // np.float32(observation)
+      }
+    }
+  }
+}
 
 template <int Q>
 __device__ inline void pol_layer(const float* __restrict__ w, int ws, const float* __restrict__ x, int n4,
@@ -329,33 +382,25 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   extern __shared__ __attribute__((aligned(16))) float psm[];
   const int S = p.S, A = p.A, H1 = p.H1, H2 = p.H2;
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
-  float* w1 = psm;                       // [H1][s1]
+  float* w1 = psm;                       // [H1][s1]   (packed image, amx_policy_pack)
   float* w2 = w1 + H1 * s1;              // [H2][s2]
   float* w3 = w2 + H2 * s2;              // [A][s3]
   float* bb1 = w3 + A * s3;
   float* bb2 = bb1 + H1;
   float* bb3 = bb2 + H2;
-  float* so = bb3 + A;                   // [POL_LANES][s1]
+  const int nblob = pol_blob_floats(S, H1, H2, A);
+  float* so = psm + nblob;               // [POL_LANES][s1]
   float* h1 = so + POL_LANES * s1;       // [POL_LANES][s2]
   float* h2 = h1 + POL_LANES * s2;       // [POL_LANES][s3]
   float* xa_s = h2 + POL_LANES * s3;     // [POL_LANES][A] float32 actions for the fused assembly
   const int t = threadIdx.x;
   const int b0 = blockIdx.x * POL_LANES;
-  // zero-padded staging (the pad columns take part in the float4 dot products)
-  for (int r = t >> 5; r < H1; r += 8)
-    for (int c = t & 31; c < s1; c += 32) w1[r * s1 + c] = c < S ? p.W1[(long long)r * S + c] : 0.f;
-  for (int r = t >> 5; r < H2; r += 8)
-    for (int c = t & 31; c < s2; c += 32) w2[r * s2 + c] = c < H1 ? p.W2[r * H1 + c] : 0.f;
-  for (int r = t >> 5; r < A; r += 8)
-    for (int c = t & 31; c < s3; c += 32) w3[r * s3 + c] = c < H2 ? p.W3[r * H2 + c] : 0.f;
-  for (int i = t; i < H1; i += 256) bb1[i] = p.b1[i];
-  for (int i = t; i < H2; i += 256) bb2[i] = p.b2[i];
-  for (int i = t; i < A; i += 256) bb3[i] = p.b3[i];
-  for (int l = t >> 5; l < POL_LANES; l += 8) {
-    const int b = b0 + l;
-    for (int c = t & 31; c < s1; c += 32)
-      so[l * s1 + c] = (b < p.B && c < S) ? (float)p.ob[(long long)b * S + c] : 0.f;  // np.float32(observation)
-  }
+  // staging: the packed weight image (pads already zero) and the block's observation rows;
+  // the observation pads / rows of lanes >= B are zeroed (they take part in the float4 dots)
+  const int nl = (p.B - b0) < POL_LANES ? (p.B - b0) : POL_LANES;  // valid lanes of this block
+  pol_zero_pads(so, s1, S, nl);
+  for (int i = t + nl * s1; i < POL_LANES * s1; i += 256) so[i] = 0.f;
+  pol_stage_all(psm, p.blob, nblob >> 2, so, s1, p.ob + (long long)b0 * S, nl * S, S);
   for (int i = t; i < POL_LANES * (s2 + s3); i += 256) h1[i] = 0.f;  // pads of h1/h2
   __syncthreads();
 
@@ -427,6 +472,36 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
     }
     for (int mm = 0; mm < p.M; ++mm) p.x0[mm * p.stride_m + (long long)bb * p.ldk + j] = x;
   }
+}
+
+// amx_policy_pack: nn.Linear weights -> the zero-padded LDS image (one thread per float).
+__global__ void k_policy_pack(const float* __restrict__ W1, const float* __restrict__ b1, int H1,
+                              const float* __restrict__ W2, const float* __restrict__ b2, int H2,
+                              const float* __restrict__ W3, const float* __restrict__ b3, int S, int A,
+                              float* __restrict__ blob) {
+  const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
+  const int n = pol_blob_floats(S, H1, H2, A);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int j = i;
+  float v = 0.f;
+  if (j < H1 * s1) {
+    const int r = j / s1, c = j % s1;
+    v = c < S ? W1[(long long)r * S + c] : 0.f;
+  } else if ((j -= H1 * s1) < H2 * s2) {
+    const int r = j / s2, c = j % s2;
+    v = c < H1 ? W2[r * H1 + c] : 0.f;
+  } else if ((j -= H2 * s2) < A * s3) {
+    const int r = j / s3, c = j % s3;
+    v = c < H2 ? W3[r * H2 + c] : 0.f;
+  } else if ((j -= A * s3) < H1) {
+    v = b1[j];
+  } else if ((j -= H1) < H2) {
+    v = b2[j];
+  } else if ((j -= H2) < A) {
+    v = b3[j];
+  }
+  blob[i] = v;
 }
 
 __global__ void k_philox(uint32_t k0, uint32_t k1, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t* out, int n) {
@@ -520,12 +595,31 @@ extern "C" int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* 
   return AMX_OK;
 }
 
-extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* W1, const float* b1, int H1,
-                              const float* W2, const float* b2, int H2, const float* W3, const float* b3,
+extern "C" long long amx_policy_blob_floats(const amx_ctx* ctx, int H1, int H2) {
+  if (!ctx || H1 <= 0 || H2 <= 0) return -1;
+  return pol_blob_floats(ctx->S, H1, H2, ctx->A);
+}
+
+extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, int H1, const float* W2,
+                               const float* b2, int H2, const float* W3, const float* b3, float* blob,
+                               void* stream) {
+  AMX_CHECK_ARG(ctx && W1 && b1 && W2 && b2 && W3 && b3 && blob, "amx_policy_pack: null pointer");
+  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH,
+                "amx_policy_pack: H1=%d H2=%d A=%d (max %d)", H1, H2, ctx->A, POL_MAXH);
+  AMX_CHECK_ARG(amx::aligned16(blob), "amx_policy_pack: blob must be 16-byte aligned");
+  const int n = pol_blob_floats(ctx->S, H1, H2, ctx->A);
+  hipLaunchKernelGGL(k_policy_pack, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, W1, b1, H1, W2, b2,
+                     H2, W3, b3, ctx->S, ctx->A, blob);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                               const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                               int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
                               void* stream) {
-  AMX_CHECK_ARG(ctx && ob && W1 && b1 && W2 && b2 && W3 && b3 && act, "amx_policy_act: null pointer");
+  AMX_CHECK_ARG(ctx && ob && blob && act, "amx_policy_act: null pointer");
+  AMX_CHECK_ARG(amx::aligned16(blob), "amx_policy_act: blob must be 16-byte aligned");
   AMX_CHECK_ARG(eval_mode || noise_scale, "amx_policy_act: noise_scale required unless eval_mode");
   AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH,
                 "amx_policy_act: H1=%d H2=%d A=%d (max %d)", H1, H2, ctx->A, POL_MAXH);
@@ -537,7 +631,7 @@ extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float
   const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S/H too large for LDS staging (%zu B)", lds);
   PolicyArgs p;
-  p.ob = ob; p.W1 = W1; p.b1 = b1; p.H1 = H1; p.W2 = W2; p.b2 = b2; p.H2 = H2; p.W3 = W3; p.b3 = b3;
+  p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;
   p.nscale = noise_scale; p.noise = noise;
   p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32); p.ctr_lo = (uint32_t)counter;
   p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode;

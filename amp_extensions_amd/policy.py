@@ -52,6 +52,14 @@ class DevicePolicy:
         ls = np.float64(torch.as_tensor(log_std).detach().cpu().numpy().ravel())
         self.log_std_val = ls
         self.noise_scale = torch.from_numpy(np.exp(ls)).to(dev)
+        c = self.ctx
+        n = int(c.lib.amx_policy_blob_floats(c.h, self.H1, self.H2))
+        if n <= 0:
+            raise ValueError("amx_policy_blob_floats failed")
+        self.blob = torch.empty(n, dtype=torch.float32, device=dev)
+        N.check(c.lib.amx_policy_pack(c.h, self.W[0].data_ptr(), self.b[0].data_ptr(), self.H1, self.W[1].data_ptr(),
+                                      self.b[1].data_ptr(), self.H2, self.W[2].data_ptr(), self.b[2].data_ptr(),
+                                      self.blob.data_ptr(), c.stream), "amx_policy_pack")
 
     def act(self, ob: torch.Tensor, B: int, out: torch.Tensor, counter: int, noise: torch.Tensor | None = None,
             eval_mode: bool = False, mean_out: torch.Tensor | None = None, x0: torch.Tensor | None = None
@@ -60,8 +68,7 @@ class DevicePolicy:
         buffer [M, B_pad, ldk]) fuses the ensemble's input assembly into the same launch."""
         c = self.ctx
         N.check(c.lib.amx_policy_act(
-            c.h, ob.data_ptr(), B, self.W[0].data_ptr(), self.b[0].data_ptr(), self.H1, self.W[1].data_ptr(),
-            self.b[1].data_ptr(), self.H2, self.W[2].data_ptr(), self.b[2].data_ptr(), self.noise_scale.data_ptr(),
+            c.h, ob.data_ptr(), B, self.blob.data_ptr(), self.H1, self.H2, self.noise_scale.data_ptr(),
             None if noise is None else noise.data_ptr(), self.seed, int(counter) & 0xFFFFFFFFFFFFFFFF,
             int(eval_mode), out.data_ptr(), None if mean_out is None else mean_out.data_ptr(),
             None if x0 is None else x0.data_ptr(), 0 if x0 is None else x0.stride(0),

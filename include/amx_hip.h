@@ -157,15 +157,28 @@ int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* table, int 
  *   mean = W3 tanh(W2 tanh(W1 float(ob) + b1) + b2) + b3   (float32)
  *   act  = (double)mean + noise_scale * n,  n ~ N(0,1) fp64 (philox(seed, b, counter)
  *          Box-Muller) or injected noise[b][A] (nullable).  eval_mode: act = mean.
+ * The weights come as the packed image of amx_policy_pack (re-pack after each policy
+ * update, e.g. after the learner's step; not per action).
  * noise_scale = exp(log_std) in fp64 (device, [A]).
  * x0_buf (nullable) fuses the ensemble's state assembly (amx_assemble_input with
  * AMX_IN_F64) for the same lanes: x0 = [(float(ob)-mu_s)/sd_s, (float(act)-mu_a)/sd_a, 0]
  * written to every model's activation row (stride_m, ldk as in amx_assemble_input). */
-int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* W1, const float* b1, int H1,
-                   const float* W2, const float* b2, int H2, const float* W3, const float* b3,
+int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                    const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                    int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
                    void* stream);
+
+/* Floats of the packed policy weight image for hidden widths H1, H2 (host query; -1 on a
+ * bad argument). */
+long long amx_policy_blob_floats(const amx_ctx* ctx, int H1, int H2);
+
+/* Pack the policy's three nn.Linear layers (W [out][in] row-major f32, b [out]; the
+ * FCNetwork fc_layers, mjrl/mjrl/utils/fc_network.py:24-31) into blob (device, 16-byte
+ * aligned, amx_policy_blob_floats floats): zero-padded rows in the layout amx_policy_act
+ * copies into LDS with one vector pass. */
+int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, int H1, const float* W2,
+                    const float* b2, int H2, const float* W3, const float* b3, float* blob,
+                    void* stream);
 
 /* ---- MILO RFF MMD cost -------------------------------------------------------- */
 
