@@ -5,12 +5,15 @@ One synchronous step (all lanes) is, in launch order on one HIP stream:
   2. assemble    amx_assemble_input    x0 = [(s-mu)/sd, (a-mu)/sd]               (dynamics.py:225-230)
   3. ensemble    L x amx_gemm_bias_act + amx_gemm_out_unnorm (all M members)     (dynamics.py:422-433)
   4. step        amx_step              s' = s + Δ_k (fp64), done, disagreement, [s, s'] f32 (sim_env.py:140-268)
-  5. reward      amx_rff_features      phi(s, s') + fp64 column sums             (linear_cost.py:64-94)
-             or  disc GEMMs + amx_amp_reward (AMP/GAIL path, fused reward)        (gail_cost.py:231-279)
-  6. auto-reset  amx_reset_lanes       done lanes <- reset-table row, model k+1  (sim_env.py:270-285)
-A rollout of K steps is followed by the relabel (batch_reinforce.py:103-169): ordered
-fp64 sum of the feature partials -> (all-reduce across ranks) -> w -> amx_mmd_reward over
-all K*B transitions -> expert cost.
+  5. auto-reset  amx_reset_lanes       done lanes <- reset-table row, model k+1  (sim_env.py:270-285)
+The step kernel records the float32 [s, s'] cost-input row of every transition; the
+reward pass runs once over all recorded transitions (`score`, at the end of `rollout` or
+on demand), as one batched launch instead of one per step:
+     amx_rff_features      phi(s, s') + fp64 column sums                 (linear_cost.py:64-94)
+  or disc GEMMs + amx_amp_reward (AMP/GAIL path, fused reward)            (gail_cost.py:231-279)
+(the reference scores transitions only in the relabel, batch_reinforce.py:103-169).  The
+relabel then does the ordered fp64 sum of the feature partials -> (all-reduce across
+ranks) -> w -> amx_mmd_reward over all K*B transitions -> expert cost.
 
 Lane semantics: every lane is a persistent SimEnv; a trajectory that ends (fall/horizon)
 auto-resets in the same step, exactly as `o = env.reset()` after `done` in get_samples
@@ -71,9 +74,13 @@ class RolloutEngine:
         self.model_idx = z(B, dt=torch.int32)
         self.reset_count = z(B, dt=torch.int32)
         self.reset_rows = z(K, B, dt=torch.int32)
-        # [s, s'] cost-input rows.  (A side-stream reward pass overlapping the next step's
-        # GEMMs was measured: no gain, the ensemble GEMMs already fill every CU — bench r1f.)
-        self.cost_in = z(Bp, c.k_rff_pad)
+        # [s, s'] cost-input rows of every recorded transition, scored in one batched pass
+        self.cost_in = z(K, Bp, c.k_rff_pad)
+        # rows t*Bp + b with b >= B are padding: excluded from the feature sums
+        self.row_mask = None
+        if B != Bp:
+            self.row_mask = ((torch.arange(K * Bp, device=dev) % Bp) < B).to(torch.uint8)
+        self._scored = 0  # steps of the current rollout already scored
         self.means = z(K, B, A) if record_means else None
         if isinstance(cost, RBFLinearCost):
             self.phi = z(K, Bp, cost.feature_dim)
@@ -111,6 +118,7 @@ class RolloutEngine:
         if self.t != 0:
             self.obs[0].copy_(self.obs[self.t])
         self.t = 0
+        self._scored = 0
 
     def step(self, actions: torch.Tensor | None = None, reset_rows: torch.Tensor | None = None,
              noise: torch.Tensor | None = None) -> int:
@@ -137,12 +145,8 @@ class RolloutEngine:
         N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
                                self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
-                               self.cost_in.data_ptr(), c.k_rff_pad, self.nonfinite[t].data_ptr(), B, s), "amx_step")
-        if isinstance(self.cost, RBFLinearCost):
-            self.cost.map.features(self.cost_in, self.Bp, B, self.phi[t], self.partials[t])
-        elif isinstance(self.cost, GAILCost):
-            self.cost.rewards_from_input(self.cost_in, self.Bp, B, self.disc[t] if c.M >= 2 else None,
-                                         out=self.rewards[t])
+                               self.cost_in[t].data_ptr(), c.k_rff_pad, self.nonfinite[t].data_ptr(), B, s),
+                "amx_step")
         if self.auto_reset:
             N.check(c.lib.amx_reset_lanes(c.h, self.done[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
                                           None if reset_rows is None else reset_rows.data_ptr(), self.seed,
@@ -156,16 +160,37 @@ class RolloutEngine:
         return t
 
     def rollout(self, K: int | None = None) -> int:
-        """K synchronous steps (default: the buffer depth).  Returns K*B transitions."""
+        """K synchronous steps (default: the buffer depth), then the batched reward pass.
+        Returns K*B transitions."""
         K = self.K if K is None else K
         self.begin_rollout()
         for _ in range(K):
             self.step()
+        self.score()
         return K * self.B
+
+    def score(self) -> None:
+        """Features (MMD) or discriminator rewards (GAIL) of the steps recorded since the last
+        call, in one launch over their T*B_pad cost-input rows."""
+        c, cost, t0, t1, Bp = self.ctx, self.cost, self._scored, self.t, self.Bp
+        if t1 <= t0 or cost is None:
+            self._scored = t1
+            return
+        rows = (t1 - t0) * Bp
+        x = self.cost_in[t0:t1].view(rows, c.k_rff_pad)
+        if isinstance(cost, RBFLinearCost):
+            mask = None if self.row_mask is None else self.row_mask[t0 * Bp:t1 * Bp]
+            cost.map.features(x, rows, rows, self.phi[t0:t1].view(rows, -1),
+                              self.partials[t0:t1].view(rows // 128, -1), row_mask=mask)
+        elif isinstance(cost, GAILCost):
+            cost.rewards_from_input(x, rows, rows, self.disc[t0:t1].view(rows) if c.M >= 2 else None,
+                                    out=self.rewards[t0:t1].view(rows))
+        self._scored = t1
 
     # ------------------------------------------------------------------------------------
     def feature_sum(self) -> torch.Tensor:
         """Ordered fp64 sum of this rank's RFF column partials over the recorded steps."""
+        self.score()
         c, cost = self.ctx, self.cost
         n_parts = self.t * (self.Bp // 128)
         N.check(c.lib.amx_sum_partials(c.h, self.partials.data_ptr(), n_parts, cost.feature_dim,
@@ -176,8 +201,9 @@ class RolloutEngine:
         """Relabel the recorded transitions (batch_reinforce.py:103-169, MMD + ensemble).
         `allreduce(tensor)` sums a device tensor across ranks in place (None: one rank)."""
         c, cost, T, B = self.ctx, self.cost, self.t, self.B
+        self.score()
         if isinstance(cost, GAILCost):
-            return {}  # rewards were produced per step
+            return {}  # rewards come from the discriminator pass
         if not isinstance(cost, RBFLinearCost):
             raise RuntimeError("relabel needs an RBFLinearCost or GAILCost")
         phi_sum = self.feature_sum()

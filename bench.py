@@ -133,7 +133,7 @@ def main():
 
     def one_rollout():
         eng.rollout(T)
-        eng.relabel(allreduce)  # MMD: feature mean + rewards; GAIL: joins the side-stream rewards
+        eng.relabel(allreduce)  # MMD: feature mean -> w -> rewards (GAIL: rewards already scored)
         if args.cost == "mmd":
             cost.get_expert_cost()
         return T * B
