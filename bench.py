@@ -52,7 +52,7 @@ def cpu_baseline_leg(S, A, args):
     Runs before anything touches the GPU (its worker pool forks)."""
     from oracle import cpu_baseline as cb
     workers = args.cpu_workers or min(16, os.cpu_count() or 1)
-    samples = args.cpu_samples or 8000 * workers
+    samples = args.cpu_samples or 14000 * workers  # ~15 s of CPU work on the GPU box
     r = cb.run(S, A, workers=workers, samples=samples, expert_rows=args.expert_rows)
     cpu = platform.processor() or platform.machine()
     try:
