@@ -65,7 +65,11 @@ struct GemmArgs {
   const uint8_t* row_mask; // EPI_RFF: nullable
   int tiles_m, tiles_n, groups;
   long long* clock_probe;  // internal diagnostics: per-WG {s_memtime, s_memrealtime} at start / end
+  const uint16_t* W3;      // bf16x6 path: 3-limb weight image [g][N][K/16][3][16] (amx_split_bf16x3)
+  long long strideW3;      //   elements between groups; a row is 3*K elements
 };
+
+long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
 
 // Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over
 // the 8 XCDs, so block ids congruent mod 8 share an L2.  We hand each XCD a contiguous
@@ -82,6 +86,100 @@ __device__ inline void map_tile(const GemmArgs& a, int orig, int& g, int& tm, in
   const int rest = logical / a.tiles_n;
   tm = rest % a.tiles_m;
   g = rest / a.tiles_m;
+}
+
+// ---- epilogue (shared by the f32 and the bf16x6 main loops: the 32x32 C/D register map
+// is dtype-independent on gfx950) ---------------------------------------------------------
+template <int EPI, class TL>
+__device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], int g, int tm, int tn) {
+  constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int li = lane & 31, lh = lane >> 5;
+  // C/D map of 32x32 f32 MFMA: column = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+  const int row0 = tm * BM + wm * TM * 32;
+  const int col0 = tn * BN + wn * TN * 32;
+
+  if constexpr (EPI == EPI_BIAS_ACT) {
+    const float* bias = a.bias + (long long)g * a.strideBias;
+    float* Cg = a.C + (long long)g * a.strideC;
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int col = col0 + n * 32 + li;
+      const float bv = bias[col];
+#pragma unroll
+      for (int m = 0; m < TM; ++m) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          float v = acc[m][n][e] + bv;
+          if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
+          Cg[(long long)row * a.ldc + a.col_off + col] = v;
+        }
+      }
+    }
+  } else if constexpr (EPI == EPI_UNNORM) {
+    const float* bias = a.bias + (long long)g * a.strideBias;
+    float* Cg = a.C + (long long)g * a.strideC;
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int col = col0 + n * 32 + li;
+      if (col < a.n_valid) {
+        const float bv = bias[col];
+        const float sc = a.scale[col], sh = a.shift[col];
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            const float y = acc[m][n][e] + bv;
+            const float prod = y * sc;    // two roundings, as torch's (y*scale)+mean
+            Cg[(long long)row * a.ldc + col] = prod + sh;
+          }
+        }
+      }
+    }
+  } else {  // EPI_RFF (instantiated for the 128x128 tile only)
+    static_assert(BM == 128 && BN == 128 && TL::NT == 256, "RFF epilogue assumes the 128x128 tile");
+    // Stage the raw 128x128 tile through LDS, then one column per thread: coalesced phi
+    // rows, one (non-unrolled) cos call site instead of 64 inlined copies, and the fp64
+    // column sum of the valid rows in fixed row order (deterministic).
+    constexpr int CLD = BN + 4;
+    float* Cs = smem;  // [BM][CLD] = 67,584 B, reuses the stage buffers (last barrier passed)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = wm * TM * 32 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
+        }
+    __syncthreads();
+    const int c = t & (BN - 1), half = t >> 7;
+    const int col = tn * BN + c;
+    const float bv = a.bias[col];
+    double csum = 0.0;
+    float* Cg = a.C;
+#pragma unroll 2
+    for (int i = 0; i < BM / 2; ++i) {
+      const int r = half * (BM / 2) + i;
+      const int row = tm * BM + r;
+      const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
+      const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
+      Cg[(long long)row * a.ldc + col] = phi;
+      const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
+      csum += valid ? (double)phi : 0.0;
+    }
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(smem);
+    if (half == 1) red[c] = csum;
+    __syncthreads();
+    if (half == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[c];
+  }
 }
 
 // One output tile (linear id `orig`, see map_tile) of the grouped GEMM.
@@ -253,88 +351,7 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int orig) {
     p[2] = (long long)__builtin_amdgcn_s_memtime();
     p[3] = (long long)__builtin_amdgcn_s_memrealtime();
   }
-  // ---- epilogue ---------------------------------------------------------------------
-  // C/D map of 32x32 f32 MFMA: column = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
-  const int row0 = tm * BM + wm * TM * 32;
-  const int col0 = tn * BN + wn * TN * 32;
-
-  if constexpr (EPI == EPI_BIAS_ACT) {
-    const float* bias = a.bias + (long long)g * a.strideBias;
-    float* Cg = a.C + (long long)g * a.strideC;
-#pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      const int col = col0 + n * 32 + li;
-      const float bv = bias[col];
-#pragma unroll
-      for (int m = 0; m < TM; ++m) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-          float v = acc[m][n][e] + bv;
-          if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
-          Cg[(long long)row * a.ldc + a.col_off + col] = v;
-        }
-      }
-    }
-  } else if constexpr (EPI == EPI_UNNORM) {
-    const float* bias = a.bias + (long long)g * a.strideBias;
-    float* Cg = a.C + (long long)g * a.strideC;
-#pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      const int col = col0 + n * 32 + li;
-      if (col < a.n_valid) {
-        const float bv = bias[col];
-        const float sc = a.scale[col], sh = a.shift[col];
-#pragma unroll
-        for (int m = 0; m < TM; ++m) {
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-            const float y = acc[m][n][e] + bv;
-            const float prod = y * sc;    // two roundings, as torch's (y*scale)+mean
-            Cg[(long long)row * a.ldc + col] = prod + sh;
-          }
-        }
-      }
-    }
-  } else {  // EPI_RFF (instantiated for the 128x128 tile only)
-    static_assert(BM == 128 && BN == 128 && TL::NT == 256, "RFF epilogue assumes the 128x128 tile");
-    // Stage the raw 128x128 tile through LDS, then one column per thread: coalesced phi
-    // rows, one (non-unrolled) cos call site instead of 64 inlined copies, and the fp64
-    // column sum of the valid rows in fixed row order (deterministic).
-    constexpr int CLD = BN + 4;
-    float* Cs = smem;  // [BM][CLD] = 67,584 B, reuses the stage buffers (last barrier passed)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int r = wm * TM * 32 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-          Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
-        }
-    __syncthreads();
-    const int c = t & (BN - 1), half = t >> 7;
-    const int col = tn * BN + c;
-    const float bv = a.bias[col];
-    double csum = 0.0;
-    float* Cg = a.C;
-#pragma unroll 2
-    for (int i = 0; i < BM / 2; ++i) {
-      const int r = half * (BM / 2) + i;
-      const int row = tm * BM + r;
-      const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
-      const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
-      Cg[(long long)row * a.ldc + col] = phi;
-      const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
-      csum += valid ? (double)phi : 0.0;
-    }
-    __syncthreads();
-    double* red = reinterpret_cast<double*>(smem);
-    if (half == 1) red[c] = csum;
-    __syncthreads();
-    if (half == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[c];
-  }
+  epilogue<EPI, TL>(a, acc, g, tm, tn);
 }
 
 // Grid = one workgroup per tile, or (persistent) fewer workgroups that each loop over tiles
@@ -347,6 +364,221 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
     if (id != (int)blockIdx.x) __syncthreads();  // previous tile's last LDS reads are done
     gemm_tile<EPI, TL>(a, id);
   }
+}
+
+// ==== bf16x6: the same fp32 GEMM on the bf16 matrix pipe ==================================
+// Each fp32 operand is split exactly into three bf16 limbs, x = x0 + x1 + x2 (RNE at each
+// step; |x1| <= 2^-8|x|, |x2| <= 2^-16|x|, the last remainder has <= 8 significant bits so
+// the split is exact for normal numbers).  The product a*b is then the six limb products of
+// degree <= 2: a0b0 + (a0b1 + a1b0) + (a1b1 + a0b2 + a2b0); the dropped a1b2 + a2b1 + a2b2
+// are <= 2^-23|ab| (typically ~2^-27), below the fp32 rounding of one fma.  Each limb
+// product of two bf16 is exact in fp32 and v_mfma_f32_32x32x16_bf16 accumulates in fp32, so
+// the result carries fp32-level error (measured against fp64: tools/x6_accuracy.py) at 6
+// bf16 MFMAs = 6 x 32 cycles per 32x32x16 block instead of 8 f32 MFMAs x 64 cycles: 2.67x
+// fewer matrix-pipe cycles per f32 MAC.
+//
+// Weights are split once (amx_split_bf16x3) into a K-tiled image [N][K/16][limb][16], so a
+// row's K-tile is 96 contiguous bytes; the fp32 activations are split while they are staged
+// into LDS.  BK = 16 fp32 k per K-tile; an LDS row holds [limb0 k0..15 | limb1 | limb2 | 8
+// pad] = 56 bf16 = 112 B (28 dwords: the 16-lane groups of ds_read_b128 hit all 64 banks
+// once).  Lane l of an MFMA reads row l&31, k-chunk 8*(l>>5) of the limb it needs.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int XBK = 16;  // fp32 k per K-tile
+constexpr int XLD = 56;  // bf16 per LDS row
+
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2>
+struct TileX6 {
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_;
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  static constexpr int STAGE = (BM + BN) * XLD;                // bf16 of one stage (A + W)
+  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t);  // double buffer
+  static constexpr int NA = BM * (XBK / 4);                    // f32x4 chunks of the A tile
+  static constexpr int NW = BN * 6;                            // 16-B chunks of the W tile
+  static constexpr int VA = (NA + NT - 1) / NT, VW = (NW + NT - 1) / NT;
+  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+};
+
+// x (4 consecutive k of one row) -> limbs packed as 4 bf16 each
+__device__ __forceinline__ void split3(f32x4 x, u32x2& l0, u32x2& l1, u32x2& l2) {
+  const bf16x4 h0 = __builtin_convertvector(x, bf16x4);
+  const f32x4 r1 = x - __builtin_convertvector(h0, f32x4);  // exact
+  const bf16x4 h1 = __builtin_convertvector(r1, bf16x4);
+  const f32x4 r2 = r1 - __builtin_convertvector(h1, f32x4);  // exact
+  const bf16x4 h2 = __builtin_convertvector(r2, bf16x4);     // exact (<= 8 significant bits)
+  l0 = __builtin_bit_cast(u32x2, h0);
+  l1 = __builtin_bit_cast(u32x2, h1);
+  l2 = __builtin_bit_cast(u32x2, h2);
+}
+
+template <int EPI, class TL>
+__device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
+  constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW;
+  constexpr int NT = TL::NT, STAGE = TL::STAGE;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
+  int g, tm, tn;
+  map_tile(a, orig, g, tm, tn);
+  long long clk0 = 0, rt0 = 0;
+  if (a.clock_probe) {
+    clk0 = (long long)__builtin_amdgcn_s_memtime();
+    rt0 = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+  const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
+  const long long ldw3 = 3LL * a.K;
+  const uint16_t* __restrict__ Wg = a.W3 + (long long)g * a.strideW3 + (long long)tn * TL::BN * ldw3;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // staging maps: A chunk q = t + NT*j -> row q>>2, k 4*(q&3); W chunk q -> row q/6, piece q%6
+  // (piece = limb*2 + half: 8 bf16 each), which is also its LDS position.
+  const float* a_src[VA];
+  int a_dst[VA];
+  bool a_ok[VA];
+#pragma unroll
+  for (int j = 0; j < VA; ++j) {
+    const int q = t + NT * j;
+    a_ok[j] = (TL::NA % NT == 0 || j + 1 < VA) ? true : q < TL::NA;  // compile-time true but for a ragged last pass
+    const int r = a_ok[j] ? (q >> 2) : 0, c = (q & 3) * 4;
+    a_src[j] = Ag + (long long)r * a.lda + c;
+    a_dst[j] = r * XLD + c;
+  }
+  const uint16_t* w_src[VW];
+  int w_dst[VW];
+  bool w_ok[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    const int q = t + NT * j;
+    w_ok[j] = (TL::NW % NT == 0 || j + 1 < VW) ? true : q < TL::NW;
+    const int r = w_ok[j] ? q / 6 : 0, p = q - (q / 6) * 6;
+    w_src[j] = Wg + (long long)r * ldw3 + p * 8;
+    w_dst[j] = BM * XLD + r * XLD + p * 8;
+  }
+
+  f32x4 ra[VA];
+  u32x4 rw[VW];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  auto publish = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < VA; ++j)
+      if (a_ok[j]) {
+        u32x2 l0, l1, l2;
+        split3(ra[j], l0, l1, l2);
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 32) = l2;
+      }
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+  };
+
+  const int nk = a.K / XBK;
+#pragma unroll
+  for (int j = 0; j < VA; ++j)
+    if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j]);
+#pragma unroll
+  for (int j = 0; j < VW; ++j)
+    if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j]);
+  publish(0);
+  __syncthreads();
+
+  const int a_off = (wm * TM * 32 + li) * XLD + lh * 8;
+  const int w_off = BM * XLD + (wn * TN * 32 + li) * XLD + lh * 8;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const int kn = (kt + 1 < nk ? kt + 1 : kt);
+#pragma unroll
+    for (int j = 0; j < VA; ++j)
+      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kn * XBK);
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+      if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kn * 48);
+    __builtin_amdgcn_sched_barrier(0);
+
+    const uint16_t* As = sm + cur * STAGE + a_off;
+    const uint16_t* Ws = sm + cur * STAGE + w_off;
+    bf16x8 fa[TM][3], fb[TN][3];
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int l = 0; l < 3; ++l) fa[m][l] = *reinterpret_cast<const bf16x8*>(As + m * 32 * XLD + l * 16);
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int l = 0; l < 3; ++l) fb[n][l] = *reinterpret_cast<const bf16x8*>(Ws + n * 32 * XLD + l * 16);
+    // small terms first: (a2,b0) (a0,b2) (a1,b1) (a1,b0) (a0,b1) (a0,b0)
+    constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int n = 0; n < TN; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
+    publish((cur ^ 1) * STAGE);
+    __syncthreads();
+  }
+
+  if (a.clock_probe && threadIdx.x == 0) {
+    long long* p = a.clock_probe + 4LL * orig;
+    p[0] = clk0; p[1] = rt0;
+    p[2] = (long long)__builtin_amdgcn_s_memtime();
+    p[3] = (long long)__builtin_amdgcn_s_memrealtime();
+  }
+  epilogue<EPI, TL>(a, acc, g, tm, tn);
+}
+
+template <int EPI, class TL>
+__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_x6(GemmArgs a) {
+  gemm_tile_x6<EPI, TL>(a, blockIdx.x);
+}
+
+// fp32 [g][rows][K] (ld, stride) -> 3-limb bf16 image [g][rows][K/16][3][16]
+__global__ void k_split_bf16x3(const float* __restrict__ W, int ldw, long long strideW, int rows, int K,
+                               uint16_t* __restrict__ W3, long long strideW3) {
+  const long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x;  // one f32x4 chunk
+  const int cpr = K / 4;
+  const int g = blockIdx.y;
+  if (q >= (long long)rows * cpr) return;
+  const int r = (int)(q / cpr), c = (int)(q % cpr) * 4;
+  const f32x4 x = *reinterpret_cast<const f32x4*>(W + g * strideW + (long long)r * ldw + c);
+  u32x2 l0, l1, l2;
+  split3(x, l0, l1, l2);
+  uint16_t* dst = W3 + g * strideW3 + (long long)r * 3 * K + (c / XBK) * 48 + (c % XBK);
+  *reinterpret_cast<u32x2*>(dst) = l0;
+  *reinterpret_cast<u32x2*>(dst + 16) = l1;
+  *reinterpret_cast<u32x2*>(dst + 32) = l2;
+}
+
+using X128 = TileX6<2, 2, 2, 2>;     // 128x128, 4 waves of 64x64, 57 KB LDS: 2 WGs / CU
+using X128x224 = TileX6<1, 7, 4, 1>; // 128x224 output layer (S <= 224), 7 waves of 128x32
+
+template <int EPI, class TL>
+int launch_x6(GemmArgs& a, hipStream_t stream) {
+  a.tiles_m = a.rows / TL::BM;
+  a.tiles_n = a.N / TL::BN;
+  a.clock_probe = g_clock_probe;
+  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+  if (nwg == 0) return AMX_OK;
+  hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
 }
 
 // ---- tile selection -------------------------------------------------------------------------
@@ -377,7 +609,6 @@ int resident_wgs(size_t lds, int nt, int occ) {
   const int per_cu = by_lds < by_waves ? by_lds : by_waves;
   return (per_cu < 1 ? 1 : per_cu) * g_cus;
 }
-long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
 
 template <int EPI, class TL>
 int launch_tile(GemmArgs& a, hipStream_t stream) {
@@ -532,4 +763,85 @@ extern "C" int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int 
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
   return launch_gemm(EPI_RFF, a, (hipStream_t)stream);
+}
+
+// ---- bf16x6 entry points ----------------------------------------------------------------
+extern "C" int amx_split_bf16x3(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw,
+                                long long strideW, uint16_t* W3, long long strideW3, void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_split_bf16x3: null ctx");
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS && rows > 0, "amx_split_bf16x3: groups=%d rows=%d", groups,
+                rows);
+  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "amx_split_bf16x3: K=%d must be a positive multiple of %d", K, XBK);
+  AMX_CHECK_ARG(W && W3 && amx::aligned16(W) && amx::aligned16(W3), "amx_split_bf16x3: null/unaligned operand");
+  AMX_CHECK_ARG(ldw >= K && ldw % 4 == 0 && strideW3 >= 3LL * K * rows && strideW3 % 8 == 0,
+                "amx_split_bf16x3: ldw=%d strideW3=%lld (K=%d rows=%d)", ldw, strideW3, K, rows);
+  const long long n = (long long)rows * (K / 4);
+  hipLaunchKernelGGL(k_split_bf16x3, dim3((unsigned)((n + 255) / 256), groups), dim3(256), 0, (hipStream_t)stream, W,
+                     ldw, strideW, rows, K, W3, strideW3);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+static int check_x6(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W3,
+                    long long strideW3) {
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
+  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
+                AMX_ROW_TILE);
+  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, XBK);
+  AMX_CHECK_ARG(A && W3 && amx::aligned16(A) && amx::aligned16(W3), "%s: null/unaligned operand", fn);
+  AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
+  AMX_CHECK_ARG(strideW3 % 8 == 0, "%s: strideW3=%lld must be a multiple of 8", fn, strideW3);
+  return AMX_OK;
+}
+
+extern "C" int amx_gemm_bias_act_x6(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
+                                    long long strideA, const uint16_t* W3, long long strideW3, const float* bias,
+                                    long long strideBias, float* C, int ldc, long long strideC, int col_off, int act,
+                                    void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_gemm_bias_act_x6: null ctx");
+  int rc = check_x6("amx_gemm_bias_act_x6", groups, rows, K, A, lda, W3, strideW3);
+  if (rc) return rc;
+  AMX_CHECK_ARG(N > 0 && N % 128 == 0, "amx_gemm_bias_act_x6: N=%d must be a multiple of 128", N);
+  AMX_CHECK_ARG(strideW3 >= 3LL * K * N || groups == 1, "amx_gemm_bias_act_x6: strideW3=%lld < 3*K*N", strideW3);
+  AMX_CHECK_ARG(bias && C, "amx_gemm_bias_act_x6: null bias/C");
+  AMX_CHECK_ARG(col_off >= 0 && col_off + N <= ldc, "amx_gemm_bias_act_x6: col_off=%d N=%d ldc=%d", col_off, N, ldc);
+  AMX_CHECK_ARG(act == AMX_ACT_NONE || act == AMX_ACT_RELU, "amx_gemm_bias_act_x6: act=%d", act);
+  GemmArgs a = {};
+  a.A = A; a.strideA = strideA; a.lda = lda;
+  a.W3 = W3; a.strideW3 = strideW3;
+  a.bias = bias; a.strideBias = strideBias;
+  a.C = C; a.strideC = strideC; a.ldc = ldc; a.col_off = col_off;
+  a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
+  return launch_x6<EPI_BIAS_ACT, X128>(a, (hipStream_t)stream);
+}
+
+extern "C" int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
+                                      int lda, long long strideA, const uint16_t* W3, long long strideW3,
+                                      const float* bias, long long strideBias, float* preds, int ldp,
+                                      long long strideP, void* stream) {
+  AMX_CHECK_ARG(ctx && ctx->have_norm, "amx_gemm_out_unnorm_x6: context has no normalizers");
+  int rc = check_x6("amx_gemm_out_unnorm_x6", groups, rows, K, A, lda, W3, strideW3);
+  if (rc) return rc;
+  AMX_CHECK_ARG(n_valid == ctx->S, "amx_gemm_out_unnorm_x6: n_valid=%d must equal S=%d", n_valid, ctx->S);
+  AMX_CHECK_ARG(bias && preds && ldp >= n_valid, "amx_gemm_out_unnorm_x6: null bias/preds or ldp=%d", ldp);
+  GemmArgs a = {};
+  a.A = A; a.strideA = strideA; a.lda = lda;
+  a.W3 = W3; a.strideW3 = strideW3;
+  a.bias = bias; a.strideBias = strideBias;
+  a.C = preds; a.strideC = strideP; a.ldc = ldp;
+  a.rows = rows; a.K = K; a.groups = groups;
+  a.n_valid = n_valid;
+  const int S = ctx->S, Ad = ctx->A;
+  a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
+  a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
+  // weight rows are padded to round_up(S, 128) (the f32 path's layout, amx_layout n_out_pad)
+  const int n32 = amx::round_up(n_valid, 32);
+  if (n32 > 128 && n32 <= 224) {
+    a.N = 224;
+    AMX_CHECK_ARG(strideW3 >= 3LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
+    return launch_x6<EPI_UNNORM, X128x224>(a, (hipStream_t)stream);
+  }
+  a.N = amx::round_up(n_valid, 128);
+  AMX_CHECK_ARG(strideW3 >= 3LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
+  return launch_x6<EPI_UNNORM, X128>(a, (hipStream_t)stream);
 }

@@ -100,7 +100,14 @@ class DeviceEnsemble:
     All members share the normalizers (DynamicsEnsemble.load_ensemble, dynamics.py:128-131).
     """
 
-    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0):
+    GEMM_PRECISIONS = ("bf16x6", "f32")
+
+    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "bf16x6"):
+        """gemm: "bf16x6" (fp32 operands split into 3 bf16 limbs, 6 limb products on the bf16
+        MFMA pipe: fp32-level error, amx_gemm_*_x6) or "f32" (v_mfma_f32_32x32x2_f32)."""
+        if gemm not in self.GEMM_PRECISIONS:
+            raise ValueError(f"gemm must be one of {self.GEMM_PRECISIONS}, got {gemm!r}")
+        self.gemm = gemm
         self.ctx = ctx
         S, A, M, Hp, L = ctx.S, ctx.A, ctx.M, ctx.Hp, ctx.L
         if len(weights) != M:
@@ -131,6 +138,9 @@ class DeviceEnsemble:
                 bp[m, :out_dim] = torch.as_tensor(b_m).float().cpu()
             self.W.append(Wp.to(dev).contiguous())
             self.b.append(bp.to(dev).contiguous())
+        self.W3 = None
+        if gemm == "bf16x6":
+            self.W3 = [self._split(W) for W in self.W]
         ctx.set_normalizers(norms)
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
@@ -138,6 +148,15 @@ class DeviceEnsemble:
         # optional timing hook: when a list, every forward appends a (start, end) pair of
         # torch.cuda.Events recorded on the launch stream around the L+1 GEMM launches
         self.gemm_events = None
+
+    def _split(self, W: torch.Tensor) -> torch.Tensor:
+        """3-limb bf16 image [M][rows][K/16][3][16] (as int16 bits) of a [M][rows][K] weight."""
+        c = self.ctx
+        M, rows, K = W.shape
+        W3 = torch.empty(M, rows, 3 * K, dtype=torch.int16, device=c.device)
+        N.check(c.lib.amx_split_bf16x3(c.h, M, rows, K, W.data_ptr(), K, rows * K, W3.data_ptr(), rows * 3 * K,
+                                       c.stream), "amx_split_bf16x3")
+        return W3
 
     @property
     def num_models(self) -> int:
@@ -185,13 +204,25 @@ class DeviceEnsemble:
             e0.record()
         for i in range(c.L):
             K = c.k0_pad + i * c.Hp
-            N.check(c.lib.amx_gemm_bias_act(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W[i].data_ptr(), K,
-                                            c.Hp * K, self.b[i].data_ptr(), c.Hp, buf.data_ptr(), c.ldk, sA,
-                                            K, N.AMX_ACT_RELU, s), "amx_gemm_bias_act")
-        N.check(c.lib.amx_gemm_out_unnorm(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
-                                          self.W[c.L].data_ptr(), c.ldk, c.n_out_pad * c.ldk,
-                                          self.b[c.L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, s),
-                "amx_gemm_out_unnorm")
+            if self.W3 is not None:
+                N.check(c.lib.amx_gemm_bias_act_x6(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA,
+                                                   self.W3[i].data_ptr(), c.Hp * 3 * K, self.b[i].data_ptr(), c.Hp,
+                                                   buf.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, s),
+                        "amx_gemm_bias_act_x6")
+            else:
+                N.check(c.lib.amx_gemm_bias_act(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W[i].data_ptr(),
+                                                K, c.Hp * K, self.b[i].data_ptr(), c.Hp, buf.data_ptr(), c.ldk, sA,
+                                                K, N.AMX_ACT_RELU, s), "amx_gemm_bias_act")
+        if self.W3 is not None:
+            N.check(c.lib.amx_gemm_out_unnorm_x6(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
+                                                 self.W3[c.L].data_ptr(), c.n_out_pad * 3 * c.ldk,
+                                                 self.b[c.L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
+                                                 Bp * c.S, s), "amx_gemm_out_unnorm_x6")
+        else:
+            N.check(c.lib.amx_gemm_out_unnorm(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
+                                              self.W[c.L].data_ptr(), c.ldk, c.n_out_pad * c.ldk,
+                                              self.b[c.L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, s),
+                    "amx_gemm_out_unnorm")
         if ev is not None:
             e1.record()
             ev.append((e0, e1, Bp))

@@ -28,6 +28,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), v_mfma_f32_32x32x2_f32
+# bf16 dense MFMA: 256 CUs x 4 SIMDs x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16: 32 cycles) x 2.4 GHz
+BF16_MFMA_PEAK_TFLOPS = 2516.6
+# the bf16x6 GEMM issues 6 bf16 limb products per f32 multiply-add: its f32-equivalent ceiling
+X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
 
 
 def parse():
@@ -39,6 +43,8 @@ def parse():
     p.add_argument("--samples", type=int, default=40000, help="samples per rollout per GPU (weak scaling)")
     p.add_argument("--faithful", action="store_true", help="use the 226/28 state/action layout")
     p.add_argument("--cost", choices=["mmd", "gail"], default="mmd")
+    p.add_argument("--gemm", choices=["bf16x6", "f32"], default="bf16x6",
+                   help="ensemble GEMM: 3-limb bf16 split on the bf16 MFMA pipe (fp32-level error) or f32 MFMA")
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
@@ -115,7 +121,7 @@ def main():
     from amp_extensions_amd.ensemble import init_ensemble_weights
     ens_w = init_ensemble_weights(S, A, hidden, M, base_seed=100)
     ctx = amx.AmxContext(S, A, n_models=M, hidden=512, n_hidden=4, feat_dim=512, device=dev)
-    ens = amx.DeviceEnsemble(ctx, ens_w, norms)
+    ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm)
     thr = ens.compute_threshold(st.to(dev), at.to(dev))
     expert = torch.from_numpy(syn.expert(args.expert_rows, S, 3))
     if args.cost == "mmd":
@@ -180,11 +186,13 @@ def main():
         try:
             with open(pmc_path) as f:
                 tj = json.load(f)
-            if tj.get("state_dim") == S and tj.get("lanes") == B:
+            if tj.get("state_dim") == S and tj.get("lanes") == B and tj.get("gemm", "f32") == args.gemm:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
+    x6 = args.gemm == "bf16x6"
+    peak = X6_PEAK_TFLOPS if x6 else F32_MFMA_PEAK_TFLOPS
     if rank == 0:
         out = {
             "metric": "learned-dynamics env steps/sec (humanoid3d, 40k-sample rollout)",
@@ -207,15 +215,21 @@ def main():
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
                 "parallelism": f"dp{world} (lane-sharded, 1 all-reduce/rollout)",
                 "termination_rate": round(term_rate, 5), "threshold": thr,
+                "gemm": ("bf16x6: fp32 operands split exactly into 3 bf16 limbs, 6 limb products per f32 MAC "
+                         "accumulated in fp32 (error vs fp64 = the f32 MFMA's, tools/x6_accuracy.py)") if x6
+                else "f32 MFMA (v_mfma_f32_32x32x2_f32)",
             },
             "roofline": {
-                "bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": F32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved_tflops / F32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": "k_gemm_nt (ensemble layers, f32 MFMA 32x32x2)",
+                "bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s" + (" (f32-equivalent; peak = bf16 dense 2516.6 / 6 limb products)" if x6 else ""),
+                "frac": round(achieved_tflops / peak, 4), "traffic": traffic,
+                "kernel": ("k_gemm_x6 (ensemble layers, v_mfma_f32_32x32x16_bf16 x 6 per f32 MAC)" if x6
+                           else "k_gemm_nt (ensemble layers, f32 MFMA 32x32x2)"),
+                "bf16_mfma_tflops": round(6 * achieved_tflops, 1) if x6 else None,
                 "avg_launch_us": round(gemm_ms * 1e3 / max(launches, 1), 2),
                 "flops_per_launch": flops_per_fwd / (ctx.L + 1),
             },
-            "step_flops_frac": round(value / world * step_flops / (F32_MFMA_PEAK_TFLOPS * 1e12), 4),
+            "step_flops_frac": round(value / world * step_flops / (peak * 1e12), 4),
             "cpu_baseline": cpu_base,
         }
         print(json.dumps(out), flush=True)

@@ -118,6 +118,27 @@ int amx_gemm_out_unnorm(amx_ctx* ctx, int groups, int rows, int n_valid, int K, 
                         const float* bias, long long strideBias, float* preds, int ldp,
                         long long strideP, void* stream);
 
+/* ---- bf16x6: the same fp32 GEMMs on the bf16 matrix pipe ------------------------
+ * Each fp32 operand is split exactly into three bf16 limbs (x = x0 + x1 + x2) and a*b is
+ * summed as the six limb products of degree <= 2 in fp32 MFMA accumulators: fp32-level
+ * error (the dropped terms are <= 2^-23 |ab|), 2.67x fewer matrix-pipe cycles than the f32
+ * MFMA.  Same semantics, layouts and epilogues as amx_gemm_bias_act / amx_gemm_out_unnorm
+ * (BasicMLP.forward, milo/milo/dynamics.py:422-433 + DynamicsModel.forward :231-232); only
+ * the weight operand differs: W3 is the image written by amx_split_bf16x3.  K % 16 == 0.
+ *
+ * amx_split_bf16x3: W [groups][rows][K] fp32 (row stride ldw, group stride strideW) ->
+ * W3 [groups][rows][K/16][3][16] bf16 bits (row stride 3K, group stride strideW3). */
+int amx_split_bf16x3(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw,
+                     long long strideW, uint16_t* W3, long long strideW3, void* stream);
+int amx_gemm_bias_act_x6(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
+                         long long strideA, const uint16_t* W3, long long strideW3, const float* bias,
+                         long long strideBias, float* C, int ldc, long long strideC, int col_off,
+                         int act, void* stream);
+int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
+                           int lda, long long strideA, const uint16_t* W3, long long strideW3,
+                           const float* bias, long long strideBias, float* preds, int ldp,
+                           long long strideP, void* stream);
+
 /* ---- step + termination ------------------------------------------------------- */
 
 /* One batched SimEnv.step after the forward (gym-simenv/gym_simenv/envs/sim_env.py:140-173):

@@ -203,3 +203,54 @@ def test_gail_rollout_rewards_match_oracle():
     ref = -cost.numpy()[:, 0]
     got = eng.rewards[:K, :B].cpu().numpy().reshape(-1)
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-4 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("S,A,hidden", [(197, 36, [512] * 4), (100, 20, [256] * 3), (300, 40, [128] * 2)])
+def test_bf16x6_ensemble_matches_oracle_and_f32(S, A, hidden):
+    """The bf16x6 GEMM path (3-limb split, 6 bf16 MFMA products) across output-tile shapes:
+    S=197 -> the 128x224 output tile, S=100 -> 128, S=300 -> 384 (three 128 tiles).  Same
+    tolerance as the f32 path (2e-5 of max(1, |ref|)), and within 1e-6 of the f32 path."""
+    import amp_extensions_amd as amx
+    s, a, s2 = offline(2048, 0, S, A)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
+    ens_w = R.init_ensemble_weights(S, A, hidden, 4, 100)
+    ctx = amx.AmxContext(S, A, n_models=4, hidden=hidden[0], n_hidden=len(hidden), feat_dim=512, device=DEV)
+    e6 = amx.DeviceEnsemble(ctx, ens_w, norms, gemm="bf16x6")
+    e32 = amx.DeviceEnsemble(ctx, ens_w, norms, gemm="f32")
+    B = 640
+    ob = torch.from_numpy(s[:B]).to(DEV)
+    ac = torch.from_numpy(a[:B]).to(DEV)
+    p6 = e6.forward_preds(ob, ac, B)[:, :B].cpu().numpy().astype(np.float64)
+    p32 = e32.forward_preds(ob, ac, B)[:, :B].cpu().numpy().astype(np.float64)
+    ref = R.ensemble_preds(ens_w, norms, torch.from_numpy(s[:B]).float(), torch.from_numpy(a[:B]).float()).numpy()
+    scale = max(1.0, np.abs(ref).max())
+    assert np.abs(p6 - ref).max() / scale <= 2e-5
+    assert np.abs(p32 - ref).max() / scale <= 2e-5
+    assert np.abs(p6 - p32).max() / scale <= 1e-6
+
+
+def test_bf16x6_split_is_exact_and_abi_checks():
+    """amx_split_bf16x3: limb0 + limb1 + limb2 == the fp32 weight exactly (normal numbers),
+    in the K-tiled [row][K/16][3][16] image; bad shapes are rejected."""
+    import amp_extensions_amd as amx
+    from amp_extensions_amd import _native as N
+    ctx = amx.AmxContext(226, 28, n_models=4, hidden=128, n_hidden=2, device=DEV)
+    rs = np.random.RandomState(5)
+    W = (rs.randn(2, 128, 64) * np.exp(rs.uniform(-20, 20, (2, 128, 64)))).astype(np.float32)
+    Wd = torch.from_numpy(W).to(DEV)
+    W3 = torch.empty(2, 128, 3 * 64, dtype=torch.int16, device=DEV)
+    N.check(ctx.lib.amx_split_bf16x3(ctx.h, 2, 128, 64, Wd.data_ptr(), 64, 128 * 64, W3.data_ptr(), 128 * 192,
+                                     ctx.stream))
+    torch.cuda.synchronize()
+    bits = W3.cpu().numpy().astype(np.uint16).reshape(2, 128, 4, 3, 16).astype(np.uint32) << 16
+    limbs = bits.view(np.float32).astype(np.float64)          # [g][r][kt][limb][16]
+    total = limbs.sum(axis=3).reshape(2, 128, 64)
+    np.testing.assert_array_equal(total, W.astype(np.float64))
+    assert (np.abs(limbs[..., 1, :]) <= np.abs(limbs[..., 0, :]) * 2.0 ** -8).all()
+    lib, s = ctx.lib, ctx.stream
+    buf = torch.zeros(1, 128, 64, dtype=torch.float32, device=DEV)
+    rc = lib.amx_split_bf16x3(ctx.h, 1, 128, 40, Wd.data_ptr(), 64, 0, W3.data_ptr(), 128 * 192, s)
+    assert rc == -1 and b"multiple of 16" in lib.amx_last_error()
+    rc = lib.amx_gemm_bias_act_x6(ctx.h, 1, 100, 128, 64, buf.data_ptr(), 64, 0, W3.data_ptr(), 128 * 192,
+                                  buf.data_ptr(), 0, buf.data_ptr(), 128, 0, 0, 1, s)
+    assert rc == -1 and b"multiple of 128" in lib.amx_last_error()

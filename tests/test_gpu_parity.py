@@ -43,10 +43,10 @@ def norms():
     return R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
 
 
-def make_ensemble(amx, hidden, norms, M=4):
+def make_ensemble(amx, hidden, norms, M=4, gemm="bf16x6"):
     ens_w = R.init_ensemble_weights(S, A, hidden, M, 100)
     ctx = amx.AmxContext(S, A, n_models=M, hidden=hidden[0], n_hidden=len(hidden), feat_dim=512, device=DEV)
-    return ctx, ens_w, amx.DeviceEnsemble(ctx, ens_w, norms)
+    return ctx, ens_w, amx.DeviceEnsemble(ctx, ens_w, norms, gemm=gemm)
 
 
 def rel_err(x, ref):
@@ -67,12 +67,13 @@ def test_philox_matches_oracle(amx):
     np.testing.assert_array_equal(got, ref)
 
 
+@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
 @pytest.mark.parametrize("tag", ["h64", "h512"])
-def test_ensemble_vs_reference_golden(amx, golden, norms, tag):
-    """Device ensemble vs the REFERENCE's own DynamicsModel.forward outputs."""
+def test_ensemble_vs_reference_golden(amx, golden, norms, tag, gemm):
+    """Device ensemble (both GEMM paths) vs the REFERENCE's own DynamicsModel.forward outputs."""
     g = golden(f"g1_ensemble_{tag}.npz")
     hidden = [int(x) for x in g["hidden"]]
-    ctx, _, ens = make_ensemble(amx, hidden, norms)
+    ctx, _, ens = make_ensemble(amx, hidden, norms, gemm=gemm)
     rs = np.random.RandomState(int(g["query_seed"]))
     B = int(g["B"])
     qs = torch.from_numpy(rs.randn(B, S) * 0.5).float()
@@ -86,9 +87,10 @@ def test_ensemble_vs_reference_golden(amx, golden, norms, tag):
     np.testing.assert_allclose(thr, float(g["threshold"]), rtol=1e-4)
 
 
-def test_ensemble_forward_f64_padding(amx, norms):
+@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
+def test_ensemble_forward_f64_padding(amx, norms, gemm):
     """fp64 state input (SimEnv's ob) with B not a multiple of 128, full [512]*4 ensemble."""
-    ctx, ens_w, ens = make_ensemble(amx, [512] * 4, norms)
+    ctx, ens_w, ens = make_ensemble(amx, [512] * 4, norms, gemm=gemm)
     rs = np.random.RandomState(11)
     B = 333
     ob = rs.randn(B, S) * 0.5
