@@ -19,6 +19,8 @@
 // groups of ds_read_b128 are conflict-free.
 #include "amx_common.h"
 
+#include <type_traits>
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -67,6 +69,8 @@ struct GemmArgs {
   long long* clock_probe;  // internal diagnostics: per-WG {s_memtime, s_memrealtime} at start / end
   const uint16_t* W3;      // bf16x6 path: 3-limb weight image [g][N][K/16][3][16] (amx_split_bf16x3)
   long long strideW3;      //   elements between groups; a row is 3*K elements
+  const uint16_t* A3;      // bf16x6 path, pre-split activations: [g][rows][lda/16][3][16]
+  long long strideA3;
 };
 
 long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
@@ -387,20 +391,30 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int XBK = 16;  // fp32 k per K-tile
-constexpr int XLD = 56;  // bf16 per LDS row
+constexpr int XBK = 16;  // granule of the weight image: 16 fp32 k per [limb][16] chunk
 
-template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2>
+// NSUB 16-k granules per K-tile (BK = 16*NSUB); LDS row = NSUB x [limb0 16 | limb1 | limb2]
+// + 8 bf16 pad (56 bf16 = 28 dwords at NSUB 1, 104 = 52 dwords at NSUB 2: both put the 16
+// rows of a ds_read_b128 lane group on distinct 4-bank slots).  STAGES 2: double-buffered
+// LDS, one barrier per K-tile; 1: single buffer, two barriers.  PF: K-tiles held in
+// registers ahead of the one being published (1 or 2).
+template <int WM_, int WN_, int TM_, int TN_, int NSUB_ = 1, int STAGES_ = 2, int PF_ = 1, int OCC_ = 2,
+          bool ALIMB_ = false>
 struct TileX6 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_;
+  // ALIMB: A arrives pre-split as a limb image like W3 (GemmArgs::A3), staged by plain copies
+  static constexpr bool ALIMB = ALIMB_;
+  static constexpr int NSUB = NSUB_, BK = 16 * NSUB_, STAGES = STAGES_, PF = PF_;
+  static constexpr int LD = NSUB * 48 + 8;                     // bf16 per LDS row
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
-  static constexpr int STAGE = (BM + BN) * XLD;                // bf16 of one stage (A + W)
-  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t);  // double buffer
-  static constexpr int NA = BM * (XBK / 4);                    // f32x4 chunks of the A tile
-  static constexpr int NW = BN * 6;                            // 16-B chunks of the W tile
+  static constexpr int STAGE = (BM + BN) * LD;                 // bf16 of one stage (A + W)
+  static constexpr size_t LDS = STAGES * STAGE * sizeof(uint16_t);
+  static constexpr int NA = ALIMB ? BM * NSUB * 6 : BM * (BK / 4);  // 16-B chunks of the A tile
+  static constexpr int NW = BN * NSUB * 6;                     // 16-B chunks of the W tile
   static constexpr int VA = (NA + NT - 1) / NT, VW = (NW + NT - 1) / NT;
-  static_assert(LDS <= 80 * 1024, "two workgroups per CU");
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(PF == 1 || (PF == 2 && STAGES == 2), "two register sets need the double buffer");
 };
 
 // x (4 consecutive k of one row) -> limbs packed as 4 bf16 each
@@ -415,10 +429,12 @@ __device__ __forceinline__ void split3(f32x4 x, u32x2& l0, u32x2& l1, u32x2& l2)
   l2 = __builtin_bit_cast(u32x2, h2);
 }
 
+template <int V> using IC = std::integral_constant<int, V>;
+
 template <int EPI, class TL>
 __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
-  constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW;
-  constexpr int NT = TL::NT, STAGE = TL::STAGE;
+  constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
+  constexpr int NT = TL::NT, STAGE = TL::STAGE, NSUB = TL::NSUB, BK = TL::BK, CPR = BK / 4;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
   int g, tm, tn;
@@ -438,18 +454,26 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
   const int wm = wave / TL::WN, wn = wave % TL::WN;
   const int li = lane & 31, lh = lane >> 5;
 
-  // staging maps: A chunk q = t + NT*j -> row q>>2, k 4*(q&3); W chunk q -> row q/6, piece q%6
-  // (piece = limb*2 + half: 8 bf16 each), which is also its LDS position.
-  const float* a_src[VA];
+  // staging maps: A chunk q = t + NT*j -> row q / CPR, k 4*(q % CPR) (granule (q%CPR)/4);
+  // W chunk q -> row q / (6*NSUB), 16-B piece p = q % (6*NSUB), stored in the image's order
+  using AP = std::conditional_t<TL::ALIMB, const uint16_t*, const float*>;
+  using AR = std::conditional_t<TL::ALIMB, u32x4, f32x4>;
+  AP a_src[VA];
   int a_dst[VA];
   bool a_ok[VA];
 #pragma unroll
   for (int j = 0; j < VA; ++j) {
     const int q = t + NT * j;
     a_ok[j] = (TL::NA % NT == 0 || j + 1 < VA) ? true : q < TL::NA;  // compile-time true but for a ragged last pass
-    const int r = a_ok[j] ? (q >> 2) : 0, c = (q & 3) * 4;
-    a_src[j] = Ag + (long long)r * a.lda + c;
-    a_dst[j] = r * XLD + c;
+    if constexpr (TL::ALIMB) {
+      const int r = a_ok[j] ? q / (6 * NSUB) : 0, p = q % (6 * NSUB);
+      a_src[j] = a.A3 + (long long)g * a.strideA3 + ((long long)tm * BM + r) * 3LL * a.lda + p * 8;
+      a_dst[j] = r * LD + p * 8;
+    } else {
+      const int r = a_ok[j] ? q / CPR : 0, c = q % CPR;
+      a_src[j] = Ag + (long long)r * a.lda + 4 * c;
+      a_dst[j] = r * LD + (c >> 2) * 48 + (c & 3) * 4;
+    }
   }
   const uint16_t* w_src[VW];
   int w_dst[VW];
@@ -458,13 +482,13 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
   for (int j = 0; j < VW; ++j) {
     const int q = t + NT * j;
     w_ok[j] = (TL::NW % NT == 0 || j + 1 < VW) ? true : q < TL::NW;
-    const int r = w_ok[j] ? q / 6 : 0, p = q - (q / 6) * 6;
+    const int r = w_ok[j] ? q / (6 * NSUB) : 0, p = q % (6 * NSUB);
     w_src[j] = Wg + (long long)r * ldw3 + p * 8;
-    w_dst[j] = BM * XLD + r * XLD + p * 8;
+    w_dst[j] = BM * LD + r * LD + p * 8;
   }
 
-  f32x4 ra[VA];
-  u32x4 rw[VW];
+  AR ra[TL::PF][VA];
+  u32x4 rw[TL::PF][VW];
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -473,66 +497,113 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  auto publish = [&](int base) {
+  const int nk = a.K / BK;
+  auto load = [&](auto set, int kt) {
+    constexpr int S = decltype(set)::value;
+    kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
 #pragma unroll
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) {
-        u32x2 l0, l1, l2;
-        split3(ra[j], l0, l1, l2);
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 32) = l2;
+        if constexpr (TL::ALIMB) ra[S][j] = *reinterpret_cast<const u32x4*>(a_src[j] + kt * 48 * NSUB);
+        else ra[S][j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
       }
 #pragma unroll
     for (int j = 0; j < VW; ++j)
-      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+      if (w_ok[j]) rw[S][j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 48 * NSUB);
   };
-
-  const int nk = a.K / XBK;
-#pragma unroll
-  for (int j = 0; j < VA; ++j)
-    if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j]);
-#pragma unroll
-  for (int j = 0; j < VW; ++j)
-    if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j]);
-  publish(0);
-  __syncthreads();
-
-  const int a_off = (wm * TM * 32 + li) * XLD + lh * 8;
-  const int w_off = BM * XLD + (wn * TN * 32 + li) * XLD + lh * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const int kn = (kt + 1 < nk ? kt + 1 : kt);
+  auto publish = [&](auto set, int base) {
+    constexpr int S = decltype(set)::value;
 #pragma unroll
     for (int j = 0; j < VA; ++j)
-      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kn * XBK);
+      if (a_ok[j]) {
+        if constexpr (TL::ALIMB) {
+          *reinterpret_cast<u32x4*>(sm + base + a_dst[j]) = ra[S][j];
+        } else {
+          u32x2 l0, l1, l2;
+          split3(ra[S][j], l0, l1, l2);
+          *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
+          *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+          *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 32) = l2;
+        }
+      }
 #pragma unroll
     for (int j = 0; j < VW; ++j)
-      if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kn * 48);
-    __builtin_amdgcn_sched_barrier(0);
-
-    const uint16_t* As = sm + cur * STAGE + a_off;
-    const uint16_t* Ws = sm + cur * STAGE + w_off;
-    bf16x8 fa[TM][3], fb[TN][3];
+      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[S][j];
+  };
+  const int a_off = (wm * TM * 32 + li) * LD + lh * 8;
+  const int w_off = BM * LD + (wn * TN * 32 + li) * LD + lh * 8;
+  auto compute = [&](int base) {
+    const uint16_t* As = sm + base + a_off;
+    const uint16_t* Ws = sm + base + w_off;
 #pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int l = 0; l < 3; ++l) fa[m][l] = *reinterpret_cast<const bf16x8*>(As + m * 32 * XLD + l * 16);
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-#pragma unroll
-      for (int l = 0; l < 3; ++l) fb[n][l] = *reinterpret_cast<const bf16x8*>(Ws + n * 32 * XLD + l * 16);
-    // small terms first: (a2,b0) (a0,b2) (a1,b1) (a1,b0) (a0,b1) (a0,b0)
-    constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
-#pragma unroll
-    for (int p = 0; p < 6; ++p)
+    for (int sub = 0; sub < NSUB; ++sub) {
+      bf16x8 fa[TM][3], fb[TN][3];
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int n = 0; n < TN; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
-    publish((cur ^ 1) * STAGE);
+        for (int l = 0; l < 3; ++l)
+          fa[m][l] = *reinterpret_cast<const bf16x8*>(As + m * 32 * LD + sub * 48 + l * 16);
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+#pragma unroll
+        for (int l = 0; l < 3; ++l)
+          fb[n][l] = *reinterpret_cast<const bf16x8*>(Ws + n * 32 * LD + sub * 48 + l * 16);
+      // small terms first: (a2,b0) (a0,b2) (a1,b1) (a1,b0) (a0,b1) (a0,b0)
+      constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+      for (int p = 0; p < 6; ++p)
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
+    }
+  };
+
+  if constexpr (TL::STAGES == 1) {
+    load(IC<0>{}, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt > 0) __syncthreads();  // everyone finished reading tile kt-1
+      publish(IC<0>{}, 0);
+      __syncthreads();
+      load(IC<0>{}, kt + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+    }
+    __syncthreads();  // the epilogue may reuse the LDS
+  } else if constexpr (TL::PF == 1) {
+    load(IC<0>{}, 0);
+    publish(IC<0>{}, 0);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      load(IC<0>{}, kt + 1);
+      // keep the prefetch ahead of the MFMA block (hipcc otherwise sinks the loads to
+      // their consumer, the LDS store after the MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur * STAGE);
+      publish(IC<0>{}, (cur ^ 1) * STAGE);
+      __syncthreads();
+    }
+  } else {
+    // two register sets: tile kt+2 is in flight while kt+1 is published and kt computed
+    load(IC<0>{}, 0);
+    publish(IC<0>{}, 0);
+    load(IC<1>{}, 1);
+    __syncthreads();
+    auto iter = [&](auto ldset, auto pubset, int kt) {
+      load(ldset, kt + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute((kt & 1) * STAGE);
+      publish(pubset, ((kt & 1) ^ 1) * STAGE);
+      __syncthreads();
+    };
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      iter(IC<0>{}, IC<1>{}, kt);
+      iter(IC<1>{}, IC<0>{}, kt + 1);
+    }
+    if (kt < nk) iter(IC<0>{}, IC<1>{}, kt);
   }
 
   if (a.clock_probe && threadIdx.x == 0) {
@@ -566,8 +637,28 @@ __global__ void k_split_bf16x3(const float* __restrict__ W, int ldw, long long s
   *reinterpret_cast<u32x2*>(dst + 32) = l2;
 }
 
-using X128 = TileX6<2, 2, 2, 2>;     // 128x128, 4 waves of 64x64, 57 KB LDS: 2 WGs / CU
-using X128x224 = TileX6<1, 7, 4, 1>; // 128x224 output layer (S <= 224), 7 waves of 128x32
+using X128 = TileX6<2, 2, 2, 2>;           // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
+using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
+using X128pf2 = TileX6<2, 2, 2, 2, 1, 2, 2>;  // two K-tiles in registers ahead
+using X128k32s1 = TileX6<2, 2, 2, 2, 2, 1>;   // BK 32, single LDS buffer (53 KB), 2 barriers / K-tile
+using X128k32 = TileX6<2, 2, 2, 2, 2, 2, 1, 1>;  // BK 32 double-buffered (106 KB): 1 WG / CU
+using X128x256w8 = TileX6<2, 4, 2, 2, 1, 2, 1, 2>;  // 128x256, 8 waves of 64x64 (86 KB): 1 WG / CU
+using X256x128w8 = TileX6<4, 2, 2, 2, 1, 2, 1, 2>;  // 256x128, 8 waves of 64x64
+using X128x256 = TileX6<2, 2, 2, 4, 1, 2, 1, 1>;    // 128x256, 4 waves of 64x128
+using X128a = TileX6<2, 2, 2, 2, 1, 2, 1, 2, true>;  // X128 on pre-split activations
+using X128x256w8a = TileX6<2, 4, 2, 2, 1, 2, 1, 2, true>;
+using X256w8 = TileX6<2, 4, 4, 2, 1, 2, 1, 2>;    // 256x256, 8 waves of 128x64 (115 KB): 1 WG / CU
+using X256w16 = TileX6<4, 4, 2, 2, 1, 2, 1, 4>;   // 256x256, 16 waves of 64x64
+using X256x128 = TileX6<2, 2, 4, 2, 1, 2, 1, 1>;  // 256x128, 4 waves of 128x64
+using X256w8pf2 = TileX6<2, 4, 4, 2, 1, 2, 2, 2>;  // + two K-tiles in registers
+using X256w8k32 = TileX6<2, 4, 4, 2, 2, 1, 1, 2>;  // BK 32, single LDS buffer (106 KB)
+const uint16_t* g_x6_a3 = nullptr;  // amx__set_x6_a3: pre-split activation image (A/B only)
+long long g_x6_a3_stride = 0;
+
+int g_x6_variant = -1;      // amx__set_x6_variant: hidden-layer tile (-1 automatic)
+int g_x6_out_variant = -1;  // amx__set_x6_out_variant: output-layer tile (-1 automatic)
+
+int resident_wgs(size_t lds, int nt, int occ);
 
 template <int EPI, class TL>
 int launch_x6(GemmArgs& a, hipStream_t stream) {
@@ -579,6 +670,34 @@ int launch_x6(GemmArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
+}
+
+template <int EPI>
+int launch_x6_variant(int v, GemmArgs& a, hipStream_t s) {
+  const bool m256 = a.rows % 256 == 0, n256 = a.N % 256 == 0;
+  switch (v) {
+    case 1: return launch_x6<EPI, X128pf2>(a, s);
+    case 2: return launch_x6<EPI, X128k32s1>(a, s);
+    case 3: return launch_x6<EPI, X128k32>(a, s);
+    case 4: if (n256) return launch_x6<EPI, X128x256w8>(a, s); break;
+    case 5: if (m256) return launch_x6<EPI, X256x128w8>(a, s); break;
+    case 6: if (n256) return launch_x6<EPI, X128x256>(a, s); break;
+    case 9: if (m256 && n256) return launch_x6<EPI, X256w8>(a, s); break;
+    case 10: if (m256 && n256) return launch_x6<EPI, X256w16>(a, s); break;
+    case 11: if (m256) return launch_x6<EPI, X256x128>(a, s); break;
+    case 12: if (m256 && n256) return launch_x6<EPI, X256w8pf2>(a, s); break;
+    case 13: if (m256 && n256) return launch_x6<EPI, X256w8k32>(a, s); break;
+    case 7: if (g_x6_a3) { a.A3 = g_x6_a3; a.strideA3 = g_x6_a3_stride; return launch_x6<EPI, X128a>(a, s); } break;
+    case 8: if (g_x6_a3 && n256) { a.A3 = g_x6_a3; a.strideA3 = g_x6_a3_stride; return launch_x6<EPI, X128x256w8a>(a, s); } break;
+    case 0: return launch_x6<EPI, X128>(a, s);
+    default: break;
+  }
+  // automatic: the 256x256 tile (8 waves of 128x64, one WG per CU) halves the operand bytes
+  // staged per MFMA against 128x128 and is 10-14% faster per hidden layer when its grid
+  // still fills the chip (tools/x6_variants.py); otherwise 128x128 (2 WGs per CU).
+  if (m256 && n256 && (long long)(a.rows / 256) * (a.N / 256) * a.groups >= resident_wgs(X256w8::LDS, X256w8::NT, 2))
+    return launch_x6<EPI, X256w8>(a, s);
+  return launch_x6<EPI, X128>(a, s);
 }
 
 // ---- tile selection -------------------------------------------------------------------------
@@ -766,6 +885,23 @@ extern "C" int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int 
 }
 
 // ---- bf16x6 entry points ----------------------------------------------------------------
+// Internal (not in the public header): force the x6 tile of the hidden layers / of the
+// output layer (0: 128x224 where S fits, k >= 1: hidden-layer variant k-1 on N padded to
+// 128) for A/B measurements.
+extern "C" int amx__set_x6_variant(int v) {
+  g_x6_variant = v;
+  return AMX_OK;
+}
+extern "C" int amx__set_x6_a3(const uint16_t* a3, long long stride) {
+  g_x6_a3 = a3;
+  g_x6_a3_stride = stride;
+  return AMX_OK;
+}
+extern "C" int amx__set_x6_out_variant(int v) {
+  g_x6_out_variant = v;
+  return AMX_OK;
+}
+
 extern "C" int amx_split_bf16x3(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw,
                                 long long strideW, uint16_t* W3, long long strideW3, void* stream) {
   AMX_CHECK_ARG(ctx, "amx_split_bf16x3: null ctx");
@@ -812,7 +948,7 @@ extern "C" int amx_gemm_bias_act_x6(amx_ctx* ctx, int groups, int rows, int N, i
   a.bias = bias; a.strideBias = strideBias;
   a.C = C; a.strideC = strideC; a.ldc = ldc; a.col_off = col_off;
   a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
-  return launch_x6<EPI_BIAS_ACT, X128>(a, (hipStream_t)stream);
+  return launch_x6_variant<EPI_BIAS_ACT>(g_x6_variant, a, (hipStream_t)stream);
 }
 
 extern "C" int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
@@ -836,12 +972,12 @@ extern "C" int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
   // weight rows are padded to round_up(S, 128) (the f32 path's layout, amx_layout n_out_pad)
   const int n32 = amx::round_up(n_valid, 32);
-  if (n32 > 128 && n32 <= 224) {
+  if (g_x6_out_variant <= 0 && n32 > 128 && n32 <= 224) {
     a.N = 224;
     AMX_CHECK_ARG(strideW3 >= 3LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
     return launch_x6<EPI_UNNORM, X128x224>(a, (hipStream_t)stream);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW3 >= 3LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
-  return launch_x6<EPI_UNNORM, X128>(a, (hipStream_t)stream);
+  return launch_x6_variant<EPI_UNNORM>(g_x6_out_variant > 0 ? g_x6_out_variant - 1 : 0, a, (hipStream_t)stream);
 }
