@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from . import _native as N
-from .engine import AmxContext, RffMap, round_up
+from .engine import AmxContext, RffMap, round_up, split_bf16x3
 
 
 class RBFLinearCost:
@@ -28,7 +28,9 @@ class RBFLinearCost:
 
     def __init__(self, expert_data: torch.Tensor, feature_dim=1024, input_type="ss", cost_range=(-1.0, 0.0),
                  bw_quantile=0.1, bw_samples=100000, lambda_b=1.0, lr=0.0, seed=100, ctx: AmxContext | None = None,
-                 device="cuda"):
+                 device="cuda", gemm: str = "bf16x6"):
+        """`gemm` selects the feature GEMM: "bf16x6" (3-limb bf16 split, fp32-level error) or
+        "f32" (f32 MFMA); everything else follows the reference constructor."""
         torch.manual_seed(seed)          # linear_cost.py:34-35
         np.random.seed(seed)
         expert_cpu = expert_data.detach().float().cpu()
@@ -53,7 +55,7 @@ class RBFLinearCost:
             S = input_dim // 2 if input_type == "ss" else input_dim
             ctx = AmxContext(S, 1, n_models=1, hidden=128, n_hidden=0, feat_dim=feature_dim, device=device)
         self.ctx = ctx
-        self.map = RffMap(ctx, self.rff_weight, self.rff_bias)
+        self.map = RffMap(ctx, self.rff_weight, self.rff_bias, gemm=gemm)
         self.w = None
         # expert features resident in HBM (:61-62); phi_e from fp64 column sums
         phi, tot = self.map.embed(expert_cpu)
@@ -148,7 +150,7 @@ class GAILCost:
     def __init__(self, expert_data: torch.Tensor, agent_rb=None, feature_dim: int = 1, hidden_dims=(1024, 512),
                  input_type: str = "ss", scaling_coef: float = 0.5, reg_coef: float = 0.05, lambda_b: float = 0.5,
                  seed=100, grad_lambda=10.0, disc_loss_type="least_squares", disc_opt="sgd", disc_opt_args=None,
-                 ctx: AmxContext | None = None, device="cuda"):
+                 ctx: AmxContext | None = None, device="cuda", gemm: str = "bf16x6"):
         if disc_loss_type != "least_squares":
             raise NotImplementedError("only the least-squares (AMP) discriminator reward is on the hot path")
         if feature_dim != 1:
@@ -172,6 +174,9 @@ class GAILCost:
             S = self.input_dim // 2
             ctx = AmxContext(S, 1, n_models=1, hidden=128, n_hidden=0, feat_dim=128, device=device)
         self.ctx = ctx
+        if gemm not in ("bf16x6", "f32"):
+            raise ValueError(f"gemm must be 'bf16x6' or 'f32', got {gemm!r}")
+        self.gemm = gemm
         self.load_weights(self.weights)
 
     def load_weights(self, weights) -> None:
@@ -187,7 +192,9 @@ class GAILCost:
             Wp[:out, :k_in] = W.float().cpu()
             bp = torch.zeros(out_p, dtype=torch.float32)
             bp[:out] = b.float().cpu()
-            self.dev_layers.append((Wp.to(dev).contiguous(), bp.to(dev).contiguous(), out_p, k_pad))
+            Wd = Wp.to(dev).contiguous()
+            W3 = split_bf16x3(self.ctx, Wd.unsqueeze(0))[0] if self.gemm == "bf16x6" else None
+            self.dev_layers.append((Wd, bp.to(dev).contiguous(), out_p, k_pad, W3))
             k_in, k_pad = out, out_p
         W3, b3 = weights[-1]
         w3 = torch.zeros(k_pad, dtype=torch.float32)
@@ -201,13 +208,18 @@ class GAILCost:
         c = self.ctx
         ws = self._ws.get(rows)
         if ws is None:
-            ws = [torch.empty(rows, out_p, dtype=torch.float32, device=c.device) for (_, _, out_p, _) in self.dev_layers]
+            ws = [torch.empty(rows, L[2], dtype=torch.float32, device=c.device) for L in self.dev_layers]
             self._ws[rows] = ws
         h = x_pad
-        for (Wp, bp, out_p, k_pad), o in zip(self.dev_layers, ws):
-            N.check(c.lib.amx_gemm_bias_act(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0, Wp.data_ptr(),
-                                            k_pad, 0, bp.data_ptr(), 0, o.data_ptr(), out_p, 0, 0, N.AMX_ACT_RELU,
-                                            c.stream), "amx_gemm_bias_act(disc)")
+        for (Wp, bp, out_p, k_pad, W3), o in zip(self.dev_layers, ws):
+            if W3 is not None:
+                N.check(c.lib.amx_gemm_bias_act_x6(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0,
+                                                   W3.data_ptr(), 0, bp.data_ptr(), 0, o.data_ptr(), out_p, 0, 0,
+                                                   N.AMX_ACT_RELU, c.stream), "amx_gemm_bias_act_x6(disc)")
+            else:
+                N.check(c.lib.amx_gemm_bias_act(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0,
+                                                Wp.data_ptr(), k_pad, 0, bp.data_ptr(), 0, o.data_ptr(), out_p, 0, 0,
+                                                N.AMX_ACT_RELU, c.stream), "amx_gemm_bias_act(disc)")
             h = o
         return h
 

@@ -639,6 +639,8 @@ __global__ void k_split_bf16x3(const float* __restrict__ W, int ldw, long long s
 
 using X128 = TileX6<2, 2, 2, 2>;           // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
 using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
+using X128x224o4 = TileX6<1, 7, 4, 1, 1, 2, 1, 4>;  // same, <= 128 VGPRs: two WGs (14 waves) per CU
+using X128x224w14 = TileX6<2, 7, 2, 1, 1, 2, 1, 4>; // 128x224, 14 waves of 64x32
 using X128pf2 = TileX6<2, 2, 2, 2, 1, 2, 2>;  // two K-tiles in registers ahead
 using X128k32s1 = TileX6<2, 2, 2, 2, 2, 1>;   // BK 32, single LDS buffer (53 KB), 2 barriers / K-tile
 using X128k32 = TileX6<2, 2, 2, 2, 2, 2, 1, 1>;  // BK 32 double-buffered (106 KB): 1 WG / CU
@@ -667,7 +669,9 @@ int launch_x6(GemmArgs& a, hipStream_t stream) {
   a.clock_probe = g_clock_probe;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
+  hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -972,12 +976,34 @@ extern "C" int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
   // weight rows are padded to round_up(S, 128) (the f32 path's layout, amx_layout n_out_pad)
   const int n32 = amx::round_up(n_valid, 32);
-  if (g_x6_out_variant <= 0 && n32 > 128 && n32 <= 224) {
+  if ((g_x6_out_variant < 0 || g_x6_out_variant == 0 || g_x6_out_variant >= 100) && n32 > 128 && n32 <= 224) {
     a.N = 224;
     AMX_CHECK_ARG(strideW3 >= 3LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
-    return launch_x6<EPI_UNNORM, X128x224>(a, (hipStream_t)stream);
+    if (g_x6_out_variant == 100) return launch_x6<EPI_UNNORM, X128x224o4>(a, (hipStream_t)stream);
+    if (g_x6_out_variant == 0) return launch_x6<EPI_UNNORM, X128x224>(a, (hipStream_t)stream);
+    // automatic: 14 waves of 64x32 (88 VGPRs), 3% ahead of 7 waves of 128x32 (tools/x6_variants.py)
+    return launch_x6<EPI_UNNORM, X128x224w14>(a, (hipStream_t)stream);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW3 >= 3LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
   return launch_x6_variant<EPI_UNNORM>(g_x6_out_variant > 0 ? g_x6_out_variant - 1 : 0, a, (hipStream_t)stream);
+}
+
+extern "C" int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
+                                   const uint16_t* W3, const float* b, float scale, float* phi, int ldphi,
+                                   double* col_partials, const uint8_t* row_mask, void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_rff_features_x6: null ctx");
+  int rc = check_x6("amx_rff_features_x6", 1, rows, K, x, ldx, W3, 0);
+  if (rc) return rc;
+  AMX_CHECK_ARG(F > 0 && F % 128 == 0, "amx_rff_features_x6: F=%d must be a multiple of 128", F);
+  AMX_CHECK_ARG(b && phi && col_partials && ldphi >= F, "amx_rff_features_x6: null b/phi/partials or ldphi");
+  AMX_CHECK_ARG(n_valid >= 0 && n_valid <= rows, "amx_rff_features_x6: n_valid=%d rows=%d", n_valid, rows);
+  GemmArgs a = {};
+  a.A = x; a.lda = ldx;
+  a.W3 = W3;
+  a.bias = b;
+  a.C = phi; a.ldc = ldphi;
+  a.rows = rows; a.N = F; a.K = K; a.groups = 1;
+  a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
+  return launch_x6<EPI_RFF, X128>(a, (hipStream_t)stream);
 }

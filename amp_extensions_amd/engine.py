@@ -86,6 +86,17 @@ class AmxContext:
                 "amx_gemm_bias_act")
 
 
+def split_bf16x3(ctx: AmxContext, W: torch.Tensor) -> torch.Tensor:
+    """3-limb bf16 image [G][rows][K/16][3][16] (int16 bits) of a [G][rows][K] fp32 device
+    weight (amx_split_bf16x3), the operand of the amx_*_x6 GEMMs."""
+    G, rows, K = W.shape
+    W = W.contiguous()
+    W3 = torch.empty(G, rows, 3 * K, dtype=torch.int16, device=ctx.device)
+    N.check(ctx.lib.amx_split_bf16x3(ctx.h, G, rows, K, W.data_ptr(), K, rows * K, W3.data_ptr(), rows * 3 * K,
+                                     ctx.stream), "amx_split_bf16x3")
+    return W3
+
+
 def _check_dev(t: torch.Tensor, dtype, name: str, device) -> None:
     if not isinstance(t, torch.Tensor) or t.device != device or t.dtype != dtype or not t.is_contiguous():
         raise ValueError(f"{name}: expected a contiguous {dtype} tensor on {device}, got "
@@ -140,7 +151,7 @@ class DeviceEnsemble:
             self.b.append(bp.to(dev).contiguous())
         self.W3 = None
         if gemm == "bf16x6":
-            self.W3 = [self._split(W) for W in self.W]
+            self.W3 = [split_bf16x3(ctx, W) for W in self.W]
         ctx.set_normalizers(norms)
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
@@ -148,15 +159,6 @@ class DeviceEnsemble:
         # optional timing hook: when a list, every forward appends a (start, end) pair of
         # torch.cuda.Events recorded on the launch stream around the L+1 GEMM launches
         self.gemm_events = None
-
-    def _split(self, W: torch.Tensor) -> torch.Tensor:
-        """3-limb bf16 image [M][rows][K/16][3][16] (as int16 bits) of a [M][rows][K] weight."""
-        c = self.ctx
-        M, rows, K = W.shape
-        W3 = torch.empty(M, rows, 3 * K, dtype=torch.int16, device=c.device)
-        N.check(c.lib.amx_split_bf16x3(c.h, M, rows, K, W.data_ptr(), K, rows * K, W3.data_ptr(), rows * 3 * K,
-                                       c.stream), "amx_split_bf16x3")
-        return W3
 
     @property
     def num_models(self) -> int:
@@ -272,7 +274,11 @@ class DeviceEnsemble:
 class RffMap:
     """phi(x) = cos(x W^T + b) * sqrt(2/F) on MFMA (linear_cost.py:64-71) with fp64 column sums."""
 
-    def __init__(self, ctx: AmxContext, W: torch.Tensor, b: torch.Tensor):
+    def __init__(self, ctx: AmxContext, W: torch.Tensor, b: torch.Tensor, gemm: str = "bf16x6"):
+        """gemm: "bf16x6" (amx_rff_features_x6 on the 3-limb image of W) or "f32"."""
+        if gemm not in DeviceEnsemble.GEMM_PRECISIONS:
+            raise ValueError(f"gemm must be one of {DeviceEnsemble.GEMM_PRECISIONS}, got {gemm!r}")
+        self.gemm = gemm
         self.ctx = ctx
         F, D = W.shape
         self.F, self.D = F, D
@@ -284,6 +290,7 @@ class RffMap:
         Wp[:, :D] = W.float().cpu()
         self.W = Wp.to(ctx.device).contiguous()
         self.b = b.float().to(ctx.device).contiguous()
+        self.W3 = split_bf16x3(ctx, self.W.unsqueeze(0))[0] if gemm == "bf16x6" else None
         # np.sqrt(2/F) is a float64 scalar; torch multiplies the fp32 tensor by it rounded to fp32
         self.scale = float(np.float32(np.sqrt(2 / F)))
 
@@ -291,6 +298,13 @@ class RffMap:
                  row_mask: torch.Tensor | None = None, ldx: int | None = None) -> None:
         c = self.ctx
         ldx = self.Kp if ldx is None else ldx
+        if self.W3 is not None:
+            N.check(c.lib.amx_rff_features_x6(c.h, rows, n_valid, self.F, self.Kp, x.data_ptr(), ldx,
+                                              self.W3.data_ptr(), self.b.data_ptr(), self.scale, phi.data_ptr(),
+                                              phi.shape[-1], partials.data_ptr(),
+                                              None if row_mask is None else row_mask.data_ptr(), c.stream),
+                    "amx_rff_features_x6")
+            return
         N.check(c.lib.amx_rff_features(c.h, rows, n_valid, self.F, self.Kp, x.data_ptr(), ldx, self.W.data_ptr(),
                                        self.Kp, self.b.data_ptr(), self.scale, phi.data_ptr(), phi.shape[-1],
                                        partials.data_ptr(), None if row_mask is None else row_mask.data_ptr(),

@@ -139,6 +139,12 @@ int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_valid, int 
                            const float* bias, long long strideBias, float* preds, int ldp,
                            long long strideP, void* stream);
 
+/* bf16x6 form of amx_rff_features (RBFLinearCost.get_rep, milo/milo/linear_cost.py:64-71):
+ * W3 = amx_split_bf16x3 image of the [F][K] RFF weight; same epilogue and outputs. */
+int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
+                        const uint16_t* W3, const float* b, float scale, float* phi, int ldphi,
+                        double* col_partials, const uint8_t* row_mask, void* stream);
+
 /* ---- step + termination ------------------------------------------------------- */
 
 /* One batched SimEnv.step after the forward (gym-simenv/gym_simenv/envs/sim_env.py:140-173):

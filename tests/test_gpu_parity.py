@@ -207,13 +207,16 @@ def test_reset_rows_and_model_rotation(amx, norms):
     np.testing.assert_array_equal(eng.num_steps.cpu().numpy(), np.zeros(300))
 
 
-def test_rff_mmd_vs_reference_golden(amx, golden, norms):
-    """Device RBFLinearCost vs the REFERENCE's outputs (bandwidth/W/b init bit-exact)."""
+@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
+def test_rff_mmd_vs_reference_golden(amx, golden, norms, gemm):
+    """Device RBFLinearCost (both feature-GEMM paths) vs the REFERENCE's outputs
+    (bandwidth/W/b init bit-exact)."""
     g = golden("g5_rff_mmd.npz")
     es, _, es2 = synthetic_offline(512, 3)
     expert = torch.cat([torch.from_numpy(es).float(), torch.from_numpy(es2).float()], dim=1)
     ctx, ens_w, ens = make_ensemble(amx, [64] * 4, norms)
-    cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, lambda_b=0.0025, seed=100, ctx=ctx)
+    cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, lambda_b=0.0025, seed=100, ctx=ctx,
+                             gemm=gemm)
     assert cost.bw == float(g["bw"])
     np.testing.assert_array_equal(cost.rff_weight.numpy()[:4, :8], g["W_head"])
     np.testing.assert_allclose(cost.phi_e.cpu().numpy(), g["phi_e"], atol=2e-6)
@@ -232,14 +235,15 @@ def test_rff_mmd_vs_reference_golden(amx, golden, norms):
     np.testing.assert_allclose(float(cost.get_expert_cost()), float(g["expert_cost"]), rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
 @pytest.mark.parametrize("tag", ["h64", "h1024"])
-def test_gail_vs_reference_golden(amx, golden, norms, tag):
+def test_gail_vs_reference_golden(amx, golden, norms, tag, gemm):
     g = golden(f"g6_gail_{tag}.npz")
     hid = [int(x) for x in g["hidden"]]
     es, _, es2 = synthetic_offline(512, 3)
     expert = torch.cat([torch.from_numpy(es).float(), torch.from_numpy(es2).float()], dim=1)
     ctx, ens_w, ens = make_ensemble(amx, [64] * 4, norms)
-    gc = amx.GAILCost(expert, hidden_dims=hid, lambda_b=float(g["lambda_b"]), seed=100, ctx=ctx)
+    gc = amx.GAILCost(expert, hidden_dims=hid, lambda_b=float(g["lambda_b"]), seed=100, ctx=ctx, gemm=gemm)
     ps, pa, ps2 = synthetic_offline(96, 4)
     ss = torch.cat([torch.from_numpy(ps), torch.from_numpy(ps2)], 1).float()
     logits = gc.disc_logits(ss.to(DEV)).cpu().numpy()
