@@ -8,9 +8,9 @@ one counter per pass, FETCH_SIZE counts half of the wide coalesced loads on gfx9
       python $R/bench.py --no-cpu-baseline --steps 3 --warmup 1
   rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- \
       python $R/bench.py --no-cpu-baseline --steps 3 --warmup 1
-  python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [lanes] [S] [A] > profiles/gemm_traffic.json
+  python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [lanes] [S] [A] [bf16x6|f32] > profiles/gemm_traffic.json
 
-The last L+1 ensemble-layer dispatches (k_gemm_nt with the BIAS_ACT / UNNORM epilogues, i.e.
+The last L+1 ensemble-layer dispatches (k_gemm_x6 / k_gemm_nt with the BIAS_ACT / UNNORM epilogues, i.e.
 the final step's forward) are taken; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch,
 against the algorithmic bytes (activation panel read + weights + output write).
 """
@@ -22,13 +22,13 @@ import re
 import sys
 
 
-def per_dispatch(d, counter):
+def per_dispatch(d, counter, kernel):
     path = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
     out = {}
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"k_gemm_nt<(\d)", r["Kernel_Name"])
+        m = re.search(kernel + r"<(\d)", r["Kernel_Name"])
         if not m or m.group(1) == "2":  # skip the RFF (EPI 2) GEMM
             continue
         k = int(r["Dispatch_Id"])
@@ -45,21 +45,24 @@ def main():
     k0 = (S + A + 31) // 32 * 32
     n_out_pad = (S + 127) // 128 * 128
     rows = M * B
-    f = per_dispatch(fetch_dir, "FETCH_SIZE")[-(L + 1):]
-    w = per_dispatch(write_dir, "WRITE_SIZE")[-(L + 1):]
+    gemm = sys.argv[6] if len(sys.argv) > 6 else "bf16x6"
+    kernel = "k_gemm_x6" if gemm == "bf16x6" else "k_gemm_nt"
+    wb = 6 if gemm == "bf16x6" else 4  # weight bytes per element as the kernel reads them (3 bf16 limbs)
+    f = per_dispatch(fetch_dir, "FETCH_SIZE", kernel)[-(L + 1):]
+    w = per_dispatch(write_dir, "WRITE_SIZE", kernel)[-(L + 1):]
     layers, tot_hbm, tot_alg = [], 0, 0
     for i in range(L + 1):
         K = k0 + i * H
         if i < L:
-            alg = rows * K * 4 + M * H * K * 4 + rows * H * 4
+            alg = rows * K * 4 + M * H * K * wb + rows * H * 4
         else:
-            alg = rows * K * 4 + M * n_out_pad * K * 4 + rows * S * 4
+            alg = rows * K * 4 + M * n_out_pad * K * wb + rows * S * 4
         hbm = int((2 * f[i] + w[i]) * 1024)
         layers.append({"layer": i, "K": K, "fetch_kb": f[i], "write_kb": w[i], "hbm_bytes": hbm, "alg_bytes": alg})
         tot_hbm += hbm
         tot_alg += alg
     print(json.dumps({
-        "kernel": "k_gemm_nt (ensemble layers)", "state_dim": S, "action_dim": A, "lanes": B,
+        "kernel": f"{kernel} (ensemble layers)", "gemm": gemm, "state_dim": S, "action_dim": A, "lanes": B,
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 3, last step",
         "method": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch (gfx950: FETCH_SIZE counts 1/2 of "
                   "wide coalesced loads, MI355X_MICROARCH.md HBM section); L2<->fabric traffic (Infinity-Cache "
