@@ -399,9 +399,13 @@ constexpr int XBK = 16;  // granule of the weight image: 16 fp32 k per [limb][16
 // LDS, one barrier per K-tile; 1: single buffer, two barriers.  PF: K-tiles held in
 // registers ahead of the one being published (1 or 2).
 template <int WM_, int WN_, int TM_, int TN_, int NSUB_ = 1, int STAGES_ = 2, int PF_ = 1, int OCC_ = 2,
-          bool ALIMB_ = false>
+          bool ALIMB_ = false, bool LATE_ = false>
 struct TileX6 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_;
+  // LATE: barrier -> publish tile t+1 -> issue the loads of t+2 -> compute t (the LDS writes
+  // drain under the MFMAs and the global loads get a whole K-tile to land) instead of
+  // loads(t+1) -> compute t -> publish t+1 -> barrier
+  static constexpr bool LATE = LATE_;
   // ALIMB: A arrives pre-split as a limb image like W3 (GemmArgs::A3), staged by plain copies
   static constexpr bool ALIMB = ALIMB_;
   static constexpr int NSUB = NSUB_, BK = 16 * NSUB_, STAGES = STAGES_, PF = PF_;
@@ -571,6 +575,19 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
       compute(0);
     }
     __syncthreads();  // the epilogue may reuse the LDS
+  } else if constexpr (TL::LATE) {
+    load(IC<0>{}, 0);
+    publish(IC<0>{}, 0);
+    load(IC<0>{}, 1);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      __syncthreads();  // tile kt visible in buffer cur; everyone is done reading buffer cur^1
+      publish(IC<0>{}, (cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
+      load(IC<0>{}, kt + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur * STAGE);
+    }
+    __syncthreads();  // the epilogue may reuse the LDS
   } else if constexpr (TL::PF == 1) {
     load(IC<0>{}, 0);
     publish(IC<0>{}, 0);
@@ -654,6 +671,8 @@ using X256w16 = TileX6<4, 4, 2, 2, 1, 2, 1, 4>;   // 256x256, 16 waves of 64x64
 using X256x128 = TileX6<2, 2, 4, 2, 1, 2, 1, 1>;  // 256x128, 4 waves of 128x64
 using X256w8pf2 = TileX6<2, 4, 4, 2, 1, 2, 2, 2>;  // + two K-tiles in registers
 using X256w8k32 = TileX6<2, 4, 4, 2, 2, 1, 1, 2>;  // BK 32, single LDS buffer (106 KB)
+using X256w8late = TileX6<2, 4, 4, 2, 1, 2, 1, 2, false, true>;
+using X128late = TileX6<2, 2, 2, 2, 1, 2, 1, 2, false, true>;
 const uint16_t* g_x6_a3 = nullptr;  // amx__set_x6_a3: pre-split activation image (A/B only)
 long long g_x6_a3_stride = 0;
 
@@ -691,6 +710,8 @@ int launch_x6_variant(int v, GemmArgs& a, hipStream_t s) {
     case 11: if (m256) return launch_x6<EPI, X256x128>(a, s); break;
     case 12: if (m256 && n256) return launch_x6<EPI, X256w8pf2>(a, s); break;
     case 13: if (m256 && n256) return launch_x6<EPI, X256w8k32>(a, s); break;
+    case 14: if (m256 && n256) return launch_x6<EPI, X256w8late>(a, s); break;
+    case 15: return launch_x6<EPI, X128late>(a, s);
     case 7: if (g_x6_a3) { a.A3 = g_x6_a3; a.strideA3 = g_x6_a3_stride; return launch_x6<EPI, X128a>(a, s); } break;
     case 8: if (g_x6_a3 && n256) { a.A3 = g_x6_a3; a.strideA3 = g_x6_a3_stride; return launch_x6<EPI, X128x256w8a>(a, s); } break;
     case 0: return launch_x6<EPI, X128>(a, s);
