@@ -689,3 +689,127 @@ def lanes_to_paths(done: np.ndarray, rewards: np.ndarray, obs: np.ndarray, steps
                 rows.append((ts, b))
                 start = t + 1
     return paths, rows
+
+
+# --------------------------------------------------------------------------------------
+# NPG policy update — mjrl/mjrl/algos/npg_cg.py:60-199 (CPI_surrogate, HVP, train_from_paths),
+# mjrl/mjrl/algos/batch_reinforce.py:58-62 (flat_vpg), mjrl/mjrl/policies/gaussian_mlp.py
+# (mean_LL :110-126, likelihood_ratio :138-142, mean_kl :144-155, set_param_values :71-94),
+# mjrl/mjrl/utils/cg_solve.py:3-23.  torch-CPU float32 autograd, as the reference.
+# --------------------------------------------------------------------------------------
+
+
+def policy_param_shapes(S: int, A: int, hidden=(32, 32)):
+    """Shapes of MLP.trainable_params in order: fc weights/biases then log_std."""
+    sizes = (S,) + tuple(hidden) + (A,)
+    shapes = []
+    for i in range(len(sizes) - 1):
+        shapes += [(sizes[i + 1], sizes[i]), (sizes[i + 1],)]
+    return shapes + [(A,)]
+
+
+def _unflatten(flat, shapes, grad=False):
+    out, i = [], 0
+    for sh in shapes:
+        n = int(np.prod(sh))
+        t = torch.from_numpy(np.asarray(flat[i:i + n], dtype=np.float32).reshape(sh).copy())
+        out.append(t.requires_grad_(grad))
+        i += n
+    return out
+
+
+def _policy_mean_ll(params, obs_t, act_t, A):
+    """MLP.mean_LL (gaussian_mlp.py:110-126) through FCNetwork.forward (fc_network.py:45-55,
+    default in_shift/in_scale: (x - 0) / (1 + 1e-8) == x in float32)."""
+    out = obs_t
+    layers = params[:-1]
+    n_lin = len(layers) // 2
+    for j in range(n_lin):
+        out = F.linear(out, layers[2 * j], layers[2 * j + 1])
+        if j < n_lin - 1:
+            out = torch.tanh(out)
+    log_std = params[-1]
+    zs = (act_t - out) / torch.exp(log_std)
+    LL = -0.5 * torch.sum(zs ** 2, dim=1) + -torch.sum(log_std) + -0.5 * A * np.log(2 * np.pi)
+    return out, LL
+
+
+def _mean_kl(new_mean, new_ls, old_mean, old_ls):
+    old_std, new_std = torch.exp(old_ls), torch.exp(new_ls)
+    Nr = (old_mean - new_mean) ** 2 + old_std ** 2 - new_std ** 2
+    Dr = 2 * new_std ** 2 + 1e-8
+    return torch.mean(torch.sum(Nr / Dr + new_ls - old_ls, dim=1))
+
+
+def npg_hvp(flat, shapes, obs, act, v, damping=1e-4):
+    """NPG.HVP (npg_cg.py:87-106): d/dtheta <grad mean_kl(new || old), v> + damping * v at
+    new == old, hvp_sample_frac = 1."""
+    A = shapes[-1][0]
+    obs_t, act_t = torch.from_numpy(np.asarray(obs)).float(), torch.from_numpy(np.asarray(act)).float()
+    new = _unflatten(flat, shapes, grad=True)
+    old = _unflatten(flat, shapes)
+    old_mean, _ = _policy_mean_ll(old, obs_t, act_t, A)
+    new_mean, _ = _policy_mean_ll(new, obs_t, act_t, A)
+    kl = _mean_kl(new_mean, new[-1], old_mean, old[-1])
+    g = torch.autograd.grad(kl, new, create_graph=True)
+    flat_g = torch.cat([x.contiguous().view(-1) for x in g])
+    h = torch.sum(flat_g * torch.from_numpy(np.asarray(v, dtype=np.float32)))
+    hv = torch.autograd.grad(h, new)
+    return np.concatenate([x.contiguous().view(-1).data.numpy() for x in hv]) + damping * np.asarray(v, np.float32)
+
+
+def _cpi_surrogate(new_flat, old_flat, shapes, obs, act, adv):
+    A = shapes[-1][0]
+    obs_t, act_t = torch.from_numpy(np.asarray(obs)).float(), torch.from_numpy(np.asarray(act)).float()
+    new = _unflatten(new_flat, shapes, grad=True)
+    old = _unflatten(old_flat, shapes)
+    _, LL_old = _policy_mean_ll(old, obs_t, act_t, A)
+    _, LL_new = _policy_mean_ll(new, obs_t, act_t, A)
+    LR = torch.exp(LL_new - LL_old)
+    return torch.mean(LR * torch.from_numpy(np.asarray(adv)).float()), new
+
+
+def npg_vpg(flat, shapes, obs, act, adv_w):
+    """BatchREINFORCE.flat_vpg (batch_reinforce.py:58-62) at new == old."""
+    surr, new = _cpi_surrogate(flat, flat, shapes, obs, act, adv_w)
+    g = torch.autograd.grad(surr, new)
+    return np.concatenate([x.contiguous().view(-1).data.numpy() for x in g]), float(surr.data.numpy())
+
+
+def cg_solve(f_Ax, b, cg_iters=10, residual_tol=1e-10):
+    """mjrl/mjrl/utils/cg_solve.py:3-23 (x_0 ignored: starts from zeros)."""
+    x = np.zeros_like(b)
+    r = b.copy()
+    p = r.copy()
+    rdotr = r.dot(r)
+    for _ in range(cg_iters):
+        z = f_Ax(p)
+        v = rdotr / p.dot(z)
+        x += v * p
+        r -= v * z
+        newrdotr = r.dot(r)
+        mu = newrdotr / rdotr
+        p = r + mu * p
+        rdotr = newrdotr
+        if rdotr < residual_tol:
+            break
+    return x
+
+
+def npg_update(flat, shapes, obs, act, adv, step=0.1, damping=1e-4, cg_iters=10, min_log_std=-2.0):
+    """NPG.train_from_paths (npg_cg.py:113-199) without logging: whitening
+    (batch_reinforce.py:284-285), VPG, CG on the HVP, alpha = sqrt(|step / (g.npg + 1e-20)|),
+    params += alpha * npg with the log_std clamp, surr_after."""
+    adv = np.asarray(adv, dtype=np.float64)
+    adv_w = (adv - np.mean(adv)) / (np.std(adv) + 1e-6)
+    flat = np.asarray(flat, dtype=np.float32)
+    vpg, surr_before = npg_vpg(flat, shapes, obs, act, adv_w)
+    npg = cg_solve(lambda v: npg_hvp(flat, shapes, obs, act, v, damping), vpg, cg_iters=cg_iters)
+    alpha = np.sqrt(np.abs(step / (np.dot(vpg.T, npg) + 1e-20)))
+    new = flat + alpha * npg
+    new32 = np.asarray(new).astype(np.float32)
+    A = shapes[-1][0]
+    new32[-A:] = np.maximum(new32[-A:], np.float32(min_log_std))  # torch.clamp(log_std, min_log_std)
+    surr_after, _ = _cpi_surrogate(new32, flat, shapes, obs, act, adv_w)
+    return dict(adv_whitened=adv_w, vpg=vpg, npg=npg, alpha=float(alpha), params1=new32,
+                surr_before=surr_before, surr_after=float(surr_after.data.numpy()))

@@ -286,6 +286,7 @@ def main():
                         pol_w0=pol_w[0][0][:4, :8])
     make_g9()
     make_g10()
+    make_g11()
     print("[make_golden] wrote fixtures to", OUT)
     return 0
 
@@ -350,10 +351,6 @@ def make_g9():
     ps.discount_sum = orig_discount_sum
 
 
-if __name__ == "__main__":
-    sys.exit(main())
-
-
 def g10_dbs(seed=10):
     """Synthetic trajectory databases in the reference's on-disk layout (collect_data.py /
     collect_expert.py): offline [{'episode': (states, actions, rewards), 'dtw_cost', 'ep_rew'}],
@@ -406,3 +403,52 @@ def make_g10():
         x = U.convert_to_veltopos(fe, Core(), False, True)
         out["v2p_expert"] = np.concatenate([t["episode"] for t in x])
     np.savez_compressed(os.path.join(OUT, "g10_db.npz"), seed=10, **out)
+
+
+def g11_paths(pol, seed=11):
+    """Synthetic rollout for G11: float32-representable observations (the policy reads
+    float32), actions = policy mean + exp(log_std) noise, raw advantages and rewards."""
+    rs = np.random.RandomState(seed)
+    paths = []
+    for T in (7, 1, 30, 12, 50, 3, 25, 64):
+        obs = (0.5 * rs.randn(T, S)).astype(np.float32).astype(np.float64)
+        obs[:, 0] = rs.uniform(0.8, 0.95, T).astype(np.float32)
+        mean = pol.model(torch.from_numpy(obs).float()).detach().numpy()
+        act = mean.astype(np.float64) + np.exp(-0.25) * rs.randn(T, A)
+        paths.append(dict(observations=obs, actions=act, advantages=rs.randn(T) * 2.0 + 0.3,
+                          rewards=rs.randn(T)))
+    return paths
+
+
+def make_g11():
+    """G11: one NPG policy update (mjrl/mjrl/algos/npg_cg.py:113-199: VPG gradient, Fisher
+    HVP by double backward of mean_kl, 10-iteration CG, normalized step, set_param_values
+    with the log_std clamp) on MILO's policy config (MLP(32,32), init_log_std -0.25,
+    min_log_std -2, kl_dist 0.05 -> normalized_step_size 0.1, damping 1e-4), plus one HVP of
+    a fixed vector."""
+    from mjrl.algos.npg_cg import NPG
+    from mjrl.policies.gaussian_mlp import MLP
+
+    torch.set_num_threads(1)
+    pol = MLP(S, A, hidden_sizes=(32, 32), seed=100, init_log_std=-0.25, min_log_std=-2.0)
+    p0 = pol.get_param_values()
+    paths = g11_paths(pol)
+    agent = NPG(None, pol, None, normalized_step_size=0.1, FIM_invert_args={"iters": 10, "damping": 1e-4},
+                hvp_sample_frac=1.0, seed=100, save_logs=False)
+    obs, act, adv_w, _, _ = agent.process_paths(paths)
+    v = np.random.RandomState(111).randn(p0.size).astype(np.float32)
+    hvp = agent.HVP(obs, act, v)
+    infos = {}
+    agent.train_from_paths(paths, infos)
+    p1 = pol.get_param_values()
+    np.savez_compressed(os.path.join(OUT, "g11_npg.npz"), seed=11, step=0.1, damping=1e-4, cg_iters=10,
+                        min_log_std=-2.0, lengths=np.array([len(p["advantages"]) for p in paths]),
+                        observations=obs.astype(np.float32), actions=act,
+                        advantages=np.concatenate([p["advantages"] for p in paths]), adv_whitened=adv_w,
+                        params0=p0, hvp_v=v, hvp=hvp, vpg=infos["vpg_grad"], npg=infos["npg_grad"],
+                        surr_before=np.float64(infos["surr_before"]), surr_after=np.float64(infos["surr_after"]),
+                        params1=p1)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -214,3 +214,19 @@ def test_g9_returns_advantages(golden, mode, lam):
         adv_w, stats = R.whiten_advantages(paths)
         np.testing.assert_array_equal(adv_w, g["adv_whitened"])
         np.testing.assert_array_equal(np.array(stats), g["base_stats"])
+
+
+def test_g11_npg_update(golden):
+    """Oracle NPG update (VPG, HVP, CG, step, clamp, surr_after) vs the reference's NPG."""
+    g = golden("g11_npg.npz")
+    shapes = R.policy_param_shapes(226, 28, (32, 32))
+    obs, act = g["observations"].astype(np.float64), g["actions"]
+    hv = R.npg_hvp(g["params0"], shapes, obs, act, g["hvp_v"], float(g["damping"]))
+    np.testing.assert_array_equal(hv, g["hvp"])
+    out = R.npg_update(g["params0"], shapes, obs, act, g["advantages"], step=float(g["step"]),
+                       damping=float(g["damping"]), cg_iters=int(g["cg_iters"]), min_log_std=float(g["min_log_std"]))
+    np.testing.assert_array_equal(out["adv_whitened"], g["adv_whitened"])
+    np.testing.assert_array_equal(out["vpg"], g["vpg"])
+    np.testing.assert_array_equal(out["npg"], g["npg"])
+    np.testing.assert_array_equal(out["params1"], g["params1"])
+    assert out["surr_after"] == float(g["surr_after"])
