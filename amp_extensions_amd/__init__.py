@@ -5,7 +5,8 @@ cost with the ensemble-disagreement bonus, the AMP/GAIL least-squares discrimina
 reward and the humanoid3d fall/horizon termination, as hand-written HIP kernels for
 gfx950 behind a C ABI (include/amx_hip.h, libamx_hip.so) and the reference's Python
 surfaces (SimEnv, sample_points, RBFLinearCost, GAILCost, DynamicsEnsemble), plus the
-sampler's consumer: returns, MLP value baseline and GAE (mjrl process_samples).
+sampler's consumers: returns, MLP value baseline and GAE (mjrl process_samples) and the
+NPG policy update (mjrl npg_cg).
 
 The native library is loaded on first use; there is no CPU fallback.
 """
@@ -14,6 +15,7 @@ from .humanoid import TerminationConfig  # noqa: F401
 __all__ = [
     "AmxContext", "DeviceEnsemble", "RffMap", "RolloutEngine", "RBFLinearCost", "GAILCost", "DevicePolicy",
     "TerminationConfig", "SimEnv", "BatchedSimEnv", "sample_points", "DeviceMLPBaseline", "process_samples",
+    "DeviceNPG",
 ]
 
 
@@ -36,6 +38,9 @@ def __getattr__(name):
     if name in ("DeviceMLPBaseline", "process_samples"):
         from . import gae
         return getattr(gae, name)
+    if name == "DeviceNPG":
+        from .npg import DeviceNPG
+        return DeviceNPG
     if name == "sample_points":
         from .sampler import sample_points
         return sample_points

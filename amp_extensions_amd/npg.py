@@ -1,0 +1,232 @@
+"""Device NPG policy update: the learner step that consumes the rollout
+(mjrl NPG.train_from_paths, mjrl/mjrl/algos/npg_cg.py:113-199), next to the rollout engine.
+
+The per-sample work (policy forward, Jacobian-vector products, back-propagation and the
+reduction of per-sample gradients) is the HIP kernel `amx_npg_pass` (csrc/amx_npg.hip); the
+10-iteration conjugate gradient (mjrl/mjrl/utils/cg_solve.py) is fp64 vector algebra on the
+device between passes.  Parameters live in the reference's flat order (MLP.trainable_params:
+W1, b1, W2, b2, W3, b3, log_std — gaussian_mlp.py:44-62), so `get_param_values` /
+`set_param_values` exchange the same vectors as the reference policy.
+
+Same semantics as the reference with hvp_sample_frac = 1 (MILO's default,
+milo/milo/arguments.py:122) and no input normalization (FCNetwork's default in_shift/in_scale:
+(x - 0) / (1 + 1e-8) == x in float32); a subsampled FIM or input normalization raise.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .engine import AmxContext
+
+NPG_VPG, NPG_FVP, NPG_EVAL = 0, 1, 2
+
+
+def pack_policy(layers, log_std) -> np.ndarray:
+    """[(W1, b1), (W2, b2), (W3, b3)], log_std -> the reference's flat fp32 parameter vector."""
+    parts = []
+    for W, b in layers:
+        parts += [np.asarray(torch.as_tensor(W).detach().cpu().float()).ravel(),
+                  np.asarray(torch.as_tensor(b).detach().cpu().float()).ravel()]
+    parts.append(np.asarray(torch.as_tensor(log_std).detach().cpu().float()).ravel())
+    return np.concatenate(parts).astype(np.float32)
+
+
+def unpack_policy(flat, S: int, A: int, hidden=(32, 32)):
+    """Inverse of pack_policy: ([(W, b)] * 3, log_std) as CPU float32 tensors."""
+    flat = np.asarray(flat, dtype=np.float32)
+    sizes = (S,) + tuple(hidden) + (A,)
+    layers, i = [], 0
+    for k in range(len(sizes) - 1):
+        o, n = sizes[k + 1], sizes[k]
+        W = torch.from_numpy(flat[i:i + o * n].reshape(o, n).copy())
+        i += o * n
+        b = torch.from_numpy(flat[i:i + o].copy())
+        i += o
+        layers.append((W, b))
+    return layers, torch.from_numpy(flat[i:i + A].copy())
+
+
+class DeviceNPG:
+    """NPG (npg_cg.py:26-199) for the mjrl Gaussian MLP policy, on the device.
+
+    `policy_layers`/`log_std`: the current policy (nn.Linear layout).  `policy` (optional): a
+    DevicePolicy to refresh after every update (the rollout's sampler)."""
+
+    def __init__(self, ctx: AmxContext, policy_layers, log_std, normalized_step_size=0.01, const_learn_rate=None,
+                 FIM_invert_args=None, hvp_sample_frac=1.0, kl_dist=None, min_log_std=-3.0,
+                 input_normalization=None, policy=None, residual_tol=1e-10):
+        if hvp_sample_frac is not None and hvp_sample_frac < 0.99:
+            raise NotImplementedError("subsampled Fisher (hvp_sample_frac < 1) is not implemented")
+        if input_normalization:
+            raise NotImplementedError("running input normalization is not implemented")
+        if len(policy_layers) != 3 or any(W.shape[0] != 32 for W, _ in policy_layers[:2]):
+            raise NotImplementedError("the device NPG kernel supports the (32, 32) tanh MLP (MILO's actor)")
+        self.ctx = ctx
+        self.S, self.A = ctx.S, ctx.A
+        if policy_layers[0][0].shape[1] != self.S or policy_layers[2][0].shape[0] != self.A:
+            raise ValueError("policy shapes do not match the context's S, A")
+        FIM_invert_args = FIM_invert_args or {"iters": 10, "damping": 1e-4}
+        self.cg_iters = int(FIM_invert_args["iters"])
+        self.damping = float(FIM_invert_args["damping"])
+        self.alpha = const_learn_rate
+        self.n_step_size = normalized_step_size if kl_dist is None else 2.0 * kl_dist
+        self.min_log_std = float(min_log_std)
+        self.residual_tol = residual_tol
+        self.policy = policy
+        self.P = int(ctx.lib.amx_npg_param_count(self.S, self.A))
+        self.theta = torch.from_numpy(pack_policy(policy_layers, log_std)).to(ctx.device)
+        assert self.theta.numel() == self.P
+        self._bufs = {}
+
+    # ---- parameters (reference flat order) ----------------------------------------------
+    def get_param_values(self) -> np.ndarray:
+        return self.theta.cpu().numpy().copy()
+
+    def set_param_values(self, new_params) -> None:
+        """MLP.set_param_values (gaussian_mlp.py:71-94): float32, log_std clamped at min_log_std."""
+        t = torch.as_tensor(np.asarray(new_params), dtype=torch.float32).to(self.ctx.device).clone()
+        t[-self.A:] = torch.clamp(t[-self.A:], min=self.min_log_std)
+        self.theta = t.contiguous()
+        if self.policy is not None:
+            layers, ls = unpack_policy(self.theta.cpu().numpy(), self.S, self.A)
+            self.policy.sync_from(layers, ls)
+
+    # ---- passes --------------------------------------------------------------------------
+    def _rows_per_block(self, n: int) -> int:
+        return max(32, int(math.ceil(n / 512 / 32)) * 32)
+
+    def _pass(self, mode, obs, act, adv, vec):
+        c = self.ctx
+        n = obs.shape[0]
+        rpb = self._rows_per_block(n)
+        nb = (n + rpb - 1) // rpb
+        width = 2 if mode == NPG_EVAL else self.P
+        key = (nb, width)
+        part = self._bufs.get(key)
+        if part is None:
+            part = self._bufs[key] = torch.empty(nb, width, dtype=torch.float64, device=c.device)
+        od = N.AMX_IN_F64 if obs.dtype == torch.float64 else N.AMX_IN_F32
+        ad = N.AMX_IN_F64 if act.dtype == torch.float64 else N.AMX_IN_F32
+        N.check(c.lib.amx_npg_pass(c.h, mode, n, obs.data_ptr(), od, obs.stride(0), act.data_ptr(), ad, act.stride(0),
+                                   None if adv is None else adv.data_ptr(), self.theta.data_ptr(),
+                                   None if vec is None else vec.data_ptr(), rpb, part.data_ptr(), c.stream),
+                "amx_npg_pass")
+        out = torch.empty(width, dtype=torch.float64, device=c.device)
+        N.check(c.lib.amx_npg_reduce(c.h, part.data_ptr(), nb, width, out.data_ptr(), c.stream), "amx_npg_reduce")
+        return out
+
+    def _inputs(self, observations, actions, advantages=None):
+        dev = self.ctx.device
+        obs = torch.as_tensor(observations).to(dev)
+        act = torch.as_tensor(actions).to(dev)
+        if obs.dtype not in (torch.float32, torch.float64):
+            obs = obs.double()
+        if act.dtype not in (torch.float32, torch.float64):
+            act = act.double()
+        obs, act = obs.contiguous(), act.contiguous()
+        if obs.dim() != 2 or obs.shape[1] != self.S or act.shape != (obs.shape[0], self.A):
+            raise ValueError(f"observations {tuple(obs.shape)} / actions {tuple(act.shape)} do not match S, A")
+        adv = None
+        if advantages is not None:
+            adv = torch.as_tensor(advantages).to(dev, torch.float64).contiguous()
+            if adv.numel() != obs.shape[0]:
+                raise ValueError("advantages must have one entry per observation")
+        return obs, act, adv
+
+    def flat_vpg(self, observations, actions, advantages) -> torch.Tensor:
+        """BatchREINFORCE.flat_vpg (batch_reinforce.py:58-62) at new == old: fp64 [P]."""
+        obs, act, adv = self._inputs(observations, actions, advantages)
+        return self._pass(NPG_VPG, obs, act, adv, None)
+
+    def _ls_curvature(self) -> torch.Tensor:
+        """d^2 mean_kl / d log_std^2 at new == old (gaussian_mlp.py:144-155 with Dr's 1e-8):
+        (8 s^2 - 4 s eps) / (2 s + eps)^2, s = exp(log_std)^2."""
+        ls = self.theta[-self.A:].double()
+        s = torch.exp(ls) ** 2
+        eps = 1e-8
+        return (8 * s * s - 4 * s * eps) / (2 * s + eps) ** 2
+
+    def HVP(self, observations, actions, vector, regu_coef=None) -> torch.Tensor:
+        """NPG.HVP (npg_cg.py:87-106): Fisher (mean_kl Hessian) times `vector` + damping."""
+        obs, act, _ = self._inputs(observations, actions)
+        return self._hvp(obs, act, torch.as_tensor(vector).to(self.ctx.device), regu_coef)
+
+    def _hvp(self, obs, act, v, regu_coef=None):
+        regu = self.damping if regu_coef is None else regu_coef
+        v32 = v.to(torch.float32).contiguous()   # the reference casts the vector to float32
+        h = self._pass(NPG_FVP, obs, act, None, v32)
+        h[-self.A:] += self._ls_curvature() * v32[-self.A:].double()
+        return h + regu * v32.double()
+
+    def cg_solve(self, obs, act, b: torch.Tensor) -> torch.Tensor:
+        """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol)."""
+        x = torch.zeros_like(b)
+        r = b.clone()
+        p = r.clone()
+        rdotr = torch.dot(r, r)
+        for _ in range(self.cg_iters):
+            z = self._hvp(obs, act, p)
+            v = rdotr / torch.dot(p, z)
+            x += v * p
+            r -= v * z
+            newrdotr = torch.dot(r, r)
+            mu = newrdotr / rdotr
+            p = r + mu * p
+            rdotr = newrdotr
+            if float(rdotr) < self.residual_tol:
+                break
+        return x
+
+    def surrogate_kl(self, obs, act, adv_w, new_theta) -> tuple[float, float]:
+        """(CPI_surrogate, kl_old_new) of new_theta against the current parameters."""
+        tot = self._pass(NPG_EVAL, obs, act, adv_w, new_theta.to(torch.float32).contiguous())
+        n = obs.shape[0]
+        return float(tot[0]) / n, float(tot[1]) / n
+
+    # ---- the update ------------------------------------------------------------------------
+    def train_from_arrays(self, observations, actions, advantages, whiten: bool = True) -> dict:
+        """NPG.train_from_paths on concatenated arrays (npg_cg.py:113-199): whitening
+        (batch_reinforce.py:284-285), VPG, CG, step size, update with the log_std clamp,
+        surr_after and kl_dist.  Returns the reference's infos entries."""
+        obs, act, adv = self._inputs(observations, actions, advantages)
+        if whiten:
+            adv = (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-6)
+        vpg = self._pass(NPG_VPG, obs, act, adv, None)
+        npg = self.cg_solve(obs, act, vpg)
+        gdot = float(torch.dot(vpg, npg))
+        if self.alpha is not None:
+            alpha = self.alpha
+            n_step_size = alpha ** 2 * gdot
+        else:
+            n_step_size = self.n_step_size
+            alpha = math.sqrt(abs(self.n_step_size / (gdot + 1e-20)))
+        new = (self.theta.double() + alpha * npg).to(torch.float32)
+        new[-self.A:] = torch.clamp(new[-self.A:], min=self.min_log_std)
+        surr_after, kl = self.surrogate_kl(obs, act, adv, new)
+        self.set_param_values(new.cpu().numpy())
+        return {"vpg_grad": vpg, "npg_grad": npg, "alpha": alpha, "delta": n_step_size, "surr_before": 0.0,
+                "surr_after": surr_after, "kl_dist": kl, "advantages": adv}
+
+    def train_from_paths(self, paths, infos: dict | None = None):
+        """Reference surface: mjrl path dicts (observations, actions, advantages, rewards) ->
+        base_stats [mean, std, min, max] of path returns; infos updated as the reference's."""
+        obs = np.concatenate([p["observations"] for p in paths])
+        act = np.concatenate([p["actions"] for p in paths])
+        adv = np.concatenate([p["advantages"] for p in paths])
+        out = self.train_from_arrays(obs, act, adv)
+        if infos is not None:
+            infos.update({k: v for k, v in out.items()})
+        returns = [float(np.sum(p["rewards"])) for p in paths]
+        return [float(np.mean(returns)), float(np.std(returns)), float(np.min(returns)), float(np.max(returns))]
+
+    def train_from_engine(self, engine, advantages: torch.Tensor) -> dict:
+        """Update from the rollout engine's buffers without a host round trip: the recorded
+        transitions obs[:T], acts[:T] ([T, B] rows) and GAE advantages [T, B]."""
+        T, B = engine.t, engine.B
+        obs = engine.obs[:T].reshape(T * B, self.S)
+        act = engine.acts[:T].reshape(T * B, self.A)
+        return self.train_from_arrays(obs, act, advantages.reshape(T * B))

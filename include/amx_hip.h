@@ -145,6 +145,25 @@ int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const
                         const uint16_t* W3, const float* b, float scale, float* phi, int ldphi,
                         double* col_partials, const uint8_t* row_mask, void* stream);
 
+/* ---- NPG policy update (the rollout's learner; mjrl/mjrl/algos/npg_cg.py:113-199) ----
+ * Policy: mjrl MLP(S -> 32 -> 32 -> A, tanh) + log_std (mjrl/mjrl/policies/gaussian_mlp.py),
+ * parameters packed in the reference's flat order (W1, b1, W2, b2, W3, b3, log_std; fp32,
+ * amx_npg_param_count(S, A) floats).  obs [N][ldo] / act [N][lda] are fp64 or fp32
+ * (AMX_IN_*); the policy reads float32(obs) as the reference does (gaussian_mlp.py:112-117).
+ * amx_npg_pass writes one fp64 partial per block of rows_per_block rows (multiple of 32):
+ *   mode 0 (VPG):  grad of mean(exp(LL_new - LL_old) * adv) at new == old
+ *                  (BatchREINFORCE.flat_vpg, batch_reinforce.py:58-62)            -> [blocks][P]
+ *   mode 1 (FVP):  J^T diag(2/(2 sigma^2 + 1e-8)) J vec / N, the mean-network block of
+ *                  NPG.HVP (npg_cg.py:87-106; log_std block and damping: caller)  -> [blocks][P]
+ *   mode 2 (EVAL): sum of exp(LL_vec - LL_theta) * adv and of the per-sample mean_kl
+ *                  terms (surr_after / kl_old_new, npg_cg.py:181-183)             -> [blocks][2]
+ * amx_npg_reduce sums the partials over blocks in block order (deterministic). */
+long long amx_npg_param_count(int S, int A);
+int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
+                 const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
+                 const float* vec, int rows_per_block, double* partials, void* stream);
+int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, void* stream);
+
 /* ---- step + termination ------------------------------------------------------- */
 
 /* One batched SimEnv.step after the forward (gym-simenv/gym_simenv/envs/sim_env.py:140-173):

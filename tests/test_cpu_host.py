@@ -158,3 +158,18 @@ def test_db_loader_refuses_arbitrary_callables(tmp_path):
     torch.save([{"episode": Evil()}], str(f), pickle_module=pickle)
     with pytest.raises(Exception):
         D.load_db(str(f))
+
+
+def test_npg_pack_unpack_roundtrip():
+    """DeviceNPG's flat parameter order is the reference's (MLP.trainable_params)."""
+    from amp_extensions_amd.npg import pack_policy, unpack_policy
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from oracle import milo_ref as R
+    layers, ls = init_mlp_policy_params(226, 28, (32, 32), seed=100, init_log_std=-0.25)
+    flat = pack_policy(layers, ls)
+    shapes = R.policy_param_shapes(226, 28, (32, 32))
+    assert flat.size == sum(int(np.prod(s)) for s in shapes)
+    l2, ls2 = unpack_policy(flat, 226, 28)
+    for (W, b), (W2, b2) in zip(layers, l2):
+        assert torch.equal(W, W2) and torch.equal(b, b2)
+    assert torch.equal(ls, ls2)

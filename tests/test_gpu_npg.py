@@ -1,0 +1,101 @@
+"""Device NPG policy update (amx_npg_pass / DeviceNPG) vs the reference's NPG (G11 golden,
+mjrl/mjrl/algos/npg_cg.py) and vs the oracle's restatement at rollout sizes.
+
+Tolerances (fp32 per-sample math in a different order, fp64 block reductions, fp64 CG):
+  * VPG gradient and a single Fisher-vector product: |x - ref| <= 1e-4 * max|ref|
+  * the 10-iteration CG solution, the updated parameters: <= 2e-3 * max|ref| (CG on a
+    damping-1e-4 Fisher amplifies the last-bit differences of each HVP)
+  * surr_after: rel 1e-3
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import milo_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def close(x, ref, tol):
+    x, ref = np.asarray(x, np.float64), np.asarray(ref, np.float64)
+    return np.abs(x - ref).max() <= tol * np.abs(ref).max()
+
+
+def make(S, A, params):
+    import amp_extensions_amd as amx
+    from amp_extensions_amd.npg import unpack_policy
+    ctx = amx.AmxContext(S, A, n_models=1, hidden=128, n_hidden=1, device=DEV)
+    layers, ls = unpack_policy(params, S, A)
+    return amx.DeviceNPG(ctx, layers, ls, normalized_step_size=0.1, FIM_invert_args={"iters": 10, "damping": 1e-4},
+                         min_log_std=-2.0)
+
+
+def test_npg_vs_reference_golden(golden):
+    g = golden("g11_npg.npz")
+    S, A = 226, 28
+    npg = make(S, A, g["params0"])
+    obs, act = g["observations"].astype(np.float64), g["actions"]
+    vpg = npg.flat_vpg(obs, act, g["adv_whitened"]).cpu().numpy()
+    assert close(vpg, g["vpg"], 1e-4), np.abs(vpg - g["vpg"]).max()
+    hv = npg.HVP(obs, act, g["hvp_v"]).cpu().numpy()
+    assert close(hv, g["hvp"], 1e-4), np.abs(hv - g["hvp"]).max()
+    out = npg.train_from_arrays(obs, act, g["advantages"])
+    np.testing.assert_allclose(out["advantages"].cpu().numpy(), g["adv_whitened"], rtol=1e-12)
+    assert close(out["npg_grad"].cpu().numpy(), g["npg"], 2e-3)
+    assert close(npg.get_param_values() - g["params0"], g["params1"] - g["params0"], 2e-3)
+    np.testing.assert_allclose(out["surr_after"], float(g["surr_after"]), rtol=1e-3)
+    # the log_std clamp and the flat order: log_std is the last A entries
+    assert (npg.get_param_values()[-A:] >= -2.0).all()
+
+
+@pytest.mark.parametrize("S,A,N", [(197, 36, 4096), (226, 28, 1000)])
+def test_npg_vs_oracle_rollout_size(S, A, N):
+    """Rollout-sized batches (ragged last block), f64 inputs as the engine holds them."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    p0 = pack_policy(layers, ls)
+    rs = np.random.RandomState(7)
+    obs = (0.5 * rs.randn(N, S)).astype(np.float32).astype(np.float64)
+    h = torch.from_numpy(obs).float()
+    for i, (W, b) in enumerate(layers):
+        h = torch.nn.functional.linear(h, W, b)
+        h = torch.tanh(h) if i < len(layers) - 1 else h
+    act = h.numpy().astype(np.float64) + np.exp(-0.25) * rs.randn(N, A)
+    adv = rs.randn(N) * 1.5 + 0.2
+    shapes = R.policy_param_shapes(S, A, (32, 32))
+    ref = R.npg_update(p0, shapes, obs, act, adv, step=0.1, damping=1e-4, cg_iters=10, min_log_std=-2.0)
+    npg = make(S, A, p0)
+    vpg = npg.flat_vpg(obs, act, ref["adv_whitened"]).cpu().numpy()
+    assert close(vpg, ref["vpg"], 1e-4)
+    out = npg.train_from_arrays(obs, act, adv)
+    assert close(out["npg_grad"].cpu().numpy(), ref["npg"], 2e-3)
+    assert close(npg.get_param_values() - p0, ref["params1"] - p0, 2e-3)
+    np.testing.assert_allclose(out["surr_after"], ref["surr_after"], rtol=1e-3)
+
+
+def test_npg_engine_path_refreshes_policy():
+    """train_from_engine on the rollout buffers updates the device sampler's policy."""
+    import amp_extensions_amd as amx
+    from amp_extensions_amd import synthetic as syn
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.ensemble import init_ensemble_weights
+    S, A = 197, 36
+    s, a, s2 = syn.offline(2048, S, A, 0)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
+    ctx = amx.AmxContext(S, A, n_models=4, hidden=128, n_hidden=2, device=DEV)
+    ens = amx.DeviceEnsemble(ctx, init_ensemble_weights(S, A, [128] * 2, 4, 100), norms)
+    layers, ls = init_mlp_policy_params(S, A)
+    pol = amx.DevicePolicy(ctx, layers, ls, seed=3)
+    eng = amx.RolloutEngine(ens, syn.reset_table(512, S, 1), lanes=256, policy=pol, seed=5, max_steps=4)
+    eng.reset_all()
+    eng.rollout()
+    adv = torch.randn(4, 256, dtype=torch.float64, device=DEV)
+    npg = amx.DeviceNPG(ctx, layers, ls, normalized_step_size=0.1, min_log_std=-2.0, policy=pol)
+    blob0 = pol.blob.clone()
+    out = npg.train_from_engine(eng, adv)
+    assert np.isfinite(out["alpha"]) and out["kl_dist"] > 0
+    # the KL of the step is about half the normalized step size (2 * kl_dist = 0.1)
+    assert 0.01 < out["kl_dist"] < 0.2
+    assert not torch.equal(blob0, pol.blob)
