@@ -39,6 +39,10 @@ SIGNATURES = {
                                        vp, c_ll, vp, c_int, c_ll, vp]),
     "amx_rff_features_x6": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, c_flt, vp, c_int,
                                     vp, vp, vp]),
+    "amx_set_motion": (c_int, [vp, vp, c_ll]),
+    "amx_motion_duration": (c_dbl, [vp]),
+    "amx_motion_states": (c_int, [vp, vp, c_int, c_int, vp, c_ll, vp]),
+    "amx_reset_lanes_motion": (c_int, [vp, vp, vp, c_u64, c_int, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_npg_param_count": (c_ll, [c_int, c_int]),
     "amx_npg_pass": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp]),
     "amx_npg_reduce": (c_int, [vp, vp, c_int, c_int, vp, vp]),

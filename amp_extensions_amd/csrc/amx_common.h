@@ -36,6 +36,11 @@ struct amx_ctx {
   int have_norm;
   amx_termination term;
   int have_term;
+  // reference motion for the motion-reset path (amx_set_motion): device copy of the blob
+  double* d_motion;
+  long long motion_n;
+  int motion_J, motion_D, motion_F;
+  double motion_duration;
 };
 
 namespace amx {
@@ -103,5 +108,6 @@ __host__ __device__ inline double u53(uint32_t a, uint32_t b) {
 // Stream tags in the 4th counter word keep the RNG streams of different kernels apart.
 constexpr uint32_t kTagReset = 0x52534554u;   // 'RSET'
 constexpr uint32_t kTagPolicy = 0x504F4C49u;  // 'POLI'
+constexpr uint32_t kTagMotion = 0x4D4F5449u;  // 'MOTI'
 
 }  // namespace amx

@@ -57,6 +57,7 @@ extern "C" amx_ctx* amx_create(int device, int S, int A, int n_models, int hidde
 extern "C" int amx_destroy(amx_ctx* c) {
   if (!c) return AMX_OK;
   if (c->d_norm) (void)hipFree(c->d_norm);
+  if (c->d_motion) (void)hipFree(c->d_motion);
   free(c);
   return AMX_OK;
 }

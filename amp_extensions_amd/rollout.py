@@ -53,10 +53,14 @@ class RolloutEngine:
         self.auto_reset = auto_reset
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
-        table = torch.as_tensor(reset_table, dtype=torch.float64)
-        if table.dim() != 2 or table.shape[1] != c.S:
-            raise ValueError(f"reset table must be [R, {c.S}] float64")
-        self.table = table.to(dev).contiguous()
+        from .motion import ReferenceMotion
+        self.motion = reset_table if isinstance(reset_table, ReferenceMotion) else None
+        self.table = None
+        if self.motion is None:
+            table = torch.as_tensor(reset_table, dtype=torch.float64)
+            if table.dim() != 2 or table.shape[1] != c.S:
+                raise ValueError(f"reset table must be [R, {c.S}] float64 (or a ReferenceMotion)")
+            self.table = table.to(dev).contiguous()
         S, A, B, Bp, K = c.S, c.A, self.B, self.Bp, self.K
         z = lambda *shape, dt=torch.float32: torch.zeros(*shape, dtype=dt, device=dev)
         # trajectory buffers of one rollout (obs[K] carries the lane state into the next rollout)
@@ -74,6 +78,7 @@ class RolloutEngine:
         self.model_idx = z(B, dt=torch.int32)
         self.reset_count = z(B, dt=torch.int32)
         self.reset_rows = z(K, B, dt=torch.int32)
+        self.reset_times = z(K, B, dt=torch.float64) if self.motion is not None else None
         # [s, s'] cost-input rows of every recorded transition, scored in one batched pass
         self.cost_in = z(K, Bp, c.k_rff_pad)
         # rows t*Bp + b with b >= B are padding: excluded from the feature sums
@@ -100,12 +105,27 @@ class RolloutEngine:
         """SimEnv.reset on every lane (sim_env.py:270-285)."""
         self.reset_lanes(None, rows)
 
+    def _reset_motion(self, mask, times, src, dst, t_out) -> None:
+        c = self.ctx
+        N.check(c.lib.amx_reset_lanes_motion(c.h, None if mask is None else mask.data_ptr(),
+                                             None if times is None else times.data_ptr(), self.seed,
+                                             self.motion.flags, src.data_ptr(), dst.data_ptr(),
+                                             self.num_steps.data_ptr(), self.model_idx.data_ptr(),
+                                             self.reset_count.data_ptr(), None if t_out is None else t_out.data_ptr(),
+                                             self.B, c.stream), "amx_reset_lanes_motion")
+
     def reset_lanes(self, mask: torch.Tensor | None, rows: torch.Tensor | None = None) -> None:
         """SimEnv.reset on the lanes with mask != 0 (all lanes when mask is None); the lane
-        states are taken from (and written back to) slot 0 of a fresh rollout."""
+        states are taken from (and written back to) slot 0 of a fresh rollout.  With a
+        ReferenceMotion reset source, `rows` are motion times [B] float64 (None: drawn
+        uniform(0, duration) per lane from Philox)."""
         c = self.ctx
         self.begin_rollout()
         dst = self.obs[0]
+        if self.motion is not None:
+            self._reset_motion(mask, rows, dst, dst, None)
+            self.t = 0
+            return
         N.check(c.lib.amx_reset_lanes(c.h, None if mask is None else mask.data_ptr(), self.table.data_ptr(),
                                       self.table.shape[0], None if rows is None else rows.data_ptr(), self.seed,
                                       dst.data_ptr(), dst.data_ptr(), self.num_steps.data_ptr(),
@@ -147,7 +167,9 @@ class RolloutEngine:
                                self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
                                self.cost_in[t].data_ptr(), c.k_rff_pad, self.nonfinite[t].data_ptr(), B, s),
                 "amx_step")
-        if self.auto_reset:
+        if self.auto_reset and self.motion is not None:
+            self._reset_motion(self.done[t], reset_rows, ob_next, self.obs[t + 1], self.reset_times[t])
+        elif self.auto_reset:
             N.check(c.lib.amx_reset_lanes(c.h, self.done[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
                                           None if reset_rows is None else reset_rows.data_ptr(), self.seed,
                                           ob_next.data_ptr(), self.obs[t + 1].data_ptr(), self.num_steps.data_ptr(),

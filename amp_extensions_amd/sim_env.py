@@ -6,11 +6,11 @@
 * `BatchedSimEnv` — B of them in lock-step on the GPU (vectorised-env semantics:
                     done lanes auto-reset; the returned observation is the pre-reset s').
 
-Deviation (documented in DESIGN.md): SimEnv.reset asks DeepMimicCore for the kinematic pose
-at a random motion time t ~ U(0, motion_length) (sim_env.py:276-280).  DeepMimicCore (C++
-Bullet/OpenGL) is out of scope, so the pose comes from a reset-state table: the facade
-draws t exactly as the reference does (np_random.uniform(0, time_max)) with time_max = the
-table length and uses row floor(t).
+Reset source: SimEnv.reset asks DeepMimicCore for the state at a random motion time
+t ~ U(0, motion_length) (sim_env.py:276-280).  With a `ReferenceMotion` the facade draws t
+exactly as the reference does (np_random.uniform(0, time_max), time_max = the clip length)
+and the state is computed on the device from the clip (csrc/amx_motion.hip); with a
+reset-state table (the synthetic benchmark) it uses row floor(t) of the table.
 """
 from __future__ import annotations
 
@@ -76,8 +76,11 @@ class SimEnv:
 
     def __init__(self, dynamic_ensemble, deepmimic_args=None, enable_velocity_check=False, horizon=HORIZON,
                  device=None, seed=None, reset_args=None, reset_table=None):
+        """`reset_table`: a [R, S] reset-state table (row floor(t)), or a `ReferenceMotion`
+        (amp_extensions_amd.motion): the state at motion time t computed on the device as
+        DeepMimicCore's reset_time(t) builds it."""
         if reset_table is None:
-            raise ValueError("SimEnv needs a reset_table (DeepMimicCore reset poses are out of scope)")
+            raise ValueError("SimEnv needs a reset source: a ReferenceMotion or a reset_table")
         self.dynamic_ensemble = dynamic_ensemble
         dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
         self.enable_velocity_check = enable_velocity_check
@@ -89,7 +92,10 @@ class SimEnv:
         self.state_size, self.action_size = c.S, c.A
         self.observation_space = Box([-np.inf] * c.S, [np.inf] * c.S)
         self.action_space = Box([-np.inf] * c.A, [np.inf] * c.A)
-        self.time_max = float(np.asarray(reset_table).shape[0])
+        self.motion = self._eng.motion
+        # sim_env.py:77: time_max = the motion length (a table's length in rows otherwise)
+        self.time_max = self.motion.get_motion_length() if self.motion is not None else \
+            float(np.asarray(reset_table).shape[0])
         self.ob = None
         self.num_steps = 0
         self.reset_counter = 0
@@ -143,8 +149,12 @@ class SimEnv:
     def reset(self):
         """sim_env.py:270-285: t ~ U(0, time_max) -> reset pose; next ensemble member."""
         t = self.np_random.uniform(low=0, high=self.time_max)
-        row = torch.tensor([int(np.floor(t))], dtype=torch.int32, device=self._eng.ctx.device)
-        self._eng.reset_all(rows=row)
+        if self.motion is not None:
+            self._eng.reset_all(rows=torch.tensor([t], dtype=torch.float64, device=self._eng.ctx.device))
+        else:
+            row = torch.tensor([int(np.floor(t))], dtype=torch.int32, device=self._eng.ctx.device)
+            self._eng.reset_all(rows=row)
+        self.last_reset_time = t
         self.num_steps = 0
         self.reset_counter = (self.reset_counter + 1) % self._eng.ctx.M
         self.ob = self._eng.obs[0, 0].cpu().numpy().copy()

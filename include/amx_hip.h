@@ -145,6 +145,27 @@ int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const
                         const uint16_t* W3, const float* b, float scale, float* phi, int ldphi,
                         double* col_partials, const uint8_t* row_mask, void* stream);
 
+/* ---- reference-motion resets (SimEnv.reset -> DeepMimicCore reset_time, §8f #2) ----------
+ * amx_set_motion: host blob (copied; amp_extensions_amd/motion.py build_blob): header[16]
+ *   {J, D, F, loop, duration, -, -, -, cycle_delta xyz, ground_pad, ...}, joints [J][8]
+ *   {type (0 revolute, 3 fixed, 4 spherical, 5 root), parent, param offset, param size,
+ *   attach xyz, -}, bodies [J][8] {shape (0 box, 1 capsule, 2 sphere), attach xyz, Param0-2,
+ *   valid}, frame times [F], post-processed frames [F][D], frame velocities [F][D]
+ *   (cMotion::Load, deepmimic/deepmimic/DeepMimicCore/anim/Motion.cpp:104-188, 415-442).
+ *   Requires S == 1 + 15 J (CtController pose + velocity layout, sim/CtController.cpp:305-319).
+ * amx_motion_states: ob[b] = the state recorded after reset_time(times[b]) (motion pose and
+ *   velocity at t, plane placement, ground resolve, CtController::BuildStatePose/Vel);
+ *   flags: 1 RecordWorldRootPos, 2 RecordWorldRootRot, 4 RecordAllWorld.
+ * amx_reset_lanes_motion: amx_reset_lanes with those states; t = times[b] or
+ *   uniform(0, duration) from Philox(seed, lane, reset#) (sim_env.py:276); t_out nullable. */
+int amx_set_motion(amx_ctx* ctx, const double* blob, long long n);
+double amx_motion_duration(const amx_ctx* ctx);
+int amx_motion_states(amx_ctx* ctx, const double* times, int B, int flags, double* ob, long long ldo,
+                      void* stream);
+int amx_reset_lanes_motion(amx_ctx* ctx, const uint8_t* mask, const double* times, uint64_t seed,
+                           int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
+                           int32_t* model_idx, int32_t* reset_count, double* t_out, int B, void* stream);
+
 /* ---- NPG policy update (the rollout's learner; mjrl/mjrl/algos/npg_cg.py:113-199) ----
  * Policy: mjrl MLP(S -> 32 -> 32 -> A, tanh) + log_std (mjrl/mjrl/policies/gaussian_mlp.py),
  * parameters packed in the reference's flat order (W1, b1, W2, b2, W3, b3, log_std; fp32,

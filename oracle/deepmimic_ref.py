@@ -1,0 +1,374 @@
+"""CPU restatement of SimEnv.reset's DeepMimicCore path (TEST INFRASTRUCTURE ONLY).
+
+SimEnv.reset (gym-simenv/gym_simenv/envs/sim_env.py:270-285) asks DeepMimicCore for the
+state of the simulated character reset to time t of the reference motion.  The C++ core is
+not buildable here (Bullet 2.88, Eigen 3.3.7, GL are absent), so this module restates, in
+float64 numpy, the code that path runs (paths relative to
+deepmimic/deepmimic/DeepMimicCore/):
+
+  Motion::Load / PostProcessFrames / BuildFrameVel / CalcFrame / CalcFrameVel /
+      CalcIndexBlend (anim/Motion.cpp:104-135, 167-305, 415-530)
+  KinTree::LerpPoses / CalcVel / PostProcessPose / JointWorldTrans / ChildParentTrans* /
+      BuildOriginTrans / CalcHeading (anim/KinTree.cpp:1082-1135, 1518-1720, 1806-1880)
+  KinCharacter::CalcPose (StandardizeQuat of the root, anim/KinCharacter.cpp:573-596)
+  SceneImitate::ResetKinCharTime + SyncCharacters (scenes/SceneImitate.cpp:469-533) with
+      SimEnv's default reset_args (no noise, radian 0: AddNoise is a no-op)
+  SceneSimChar::ResetSceneTime -> SetCharRandPlacement (plane ground: root x, z -> 0,
+      scenes/SceneSimChar.cpp:545-562, sim/Ground.cpp:154-159) -> ResolveCharGroundIntersect
+      (scenes/SceneSimChar.cpp:565-607, 0.001 pad) over the body shapes' AABBs
+  CtController::BuildStatePose / BuildStateVel (sim/CtController.cpp:378-495) with the
+      humanoid3d_rot_ctrl flags (RecordWorldRootPos false, RecordWorldRootRot true)
+  cMathUtil quaternion helpers (util/MathUtil.cpp:141-640)
+
+Third-party algorithms restated from their published sources (absent here):
+  * Eigen 3.3.7 QuaternionBase::slerp (Eigen/src/Geometry/Quaternion.h) and the
+    quaternion-vector product (v + w*uv + u x uv, uv = 2 u x v);
+  * Bullet 2.88 getAabb of btSphereShape (center +- radius), btCapsuleShape (Y-up half
+    extents (r, r + h/2, r) through |R|) and btBoxShape (half extents through |R|; the box's
+    margin is folded into its implicit dimensions, so the AABB is the geometric one).
+Body velocities are the kinematic world velocities of the body attach points
+(KinTree::CalcBodyPartVel / RBDUtil::CalcWorldVel, sim/RBDUtil.cpp:225-495): the simulated
+character is set to the kinematic pose and velocity at reset.  Parity is UNPINNED against
+the reference: no reference output of this path exists without the C++ core.
+"""
+from __future__ import annotations
+
+import json
+import math
+
+import numpy as np
+
+JOINT_TYPES = {"revolute": 0, "planar": 1, "prismatic": 2, "fixed": 3, "spherical": 4, "none": 5}
+PARAM_SIZE = {0: 1, 1: 3, 2: 1, 3: 0, 4: 4, 5: 7}
+SHAPES = {"box": 0, "capsule": 1, "sphere": 2, "cylinder": 3, "plane": 4}
+
+
+def load_character(src):
+    """src: a character file path, its JSON text, or the parsed dict."""
+    d = src if isinstance(src, dict) else (json.loads(src) if src.lstrip().startswith("{") else json.load(open(src)))
+    joints = []
+    off = 0
+    for j in d["Skeleton"]["Joints"]:
+        t = JOINT_TYPES[j["Type"]] if j["Parent"] != -1 else JOINT_TYPES["none"]
+        size = PARAM_SIZE[t]
+        attach = np.array([j["AttachX"], j["AttachY"], j["AttachZ"]], float)
+        if j["Parent"] == -1:
+            attach[:] = 0.0  # KinTree::PostProcessJointMat zeroes the root attach point
+        joints.append(dict(type=t, parent=int(j["Parent"]), offset=off, size=size, attach=attach,
+                           theta=np.array([j["AttachThetaX"], j["AttachThetaY"], j["AttachThetaZ"]], float)))
+        off += size
+    bodies = []
+    for b in d["BodyDefs"]:
+        bodies.append(dict(shape=SHAPES[b["Shape"]], attach=np.array([b["AttachX"], b["AttachY"], b["AttachZ"]], float),
+                           theta=np.array([b["AttachThetaX"], b["AttachThetaY"], b["AttachThetaZ"]], float),
+                           param=np.array([b["Param0"], b["Param1"], b["Param2"]], float)))
+    return joints, bodies, off
+
+
+# ---- quaternion helpers (w, x, y, z), cMathUtil / Eigen -----------------------------------
+def qmul(a, b):
+    aw, ax, ay, az = a
+    bw, bx, by, bz = b
+    return np.array([aw * bw - ax * bx - ay * by - az * bz, aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by + ay * bw + az * bx - ax * bz, aw * bz + az * bw + ax * by - ay * bx])
+
+
+def qconj(q):
+    return np.array([q[0], -q[1], -q[2], -q[3]])
+
+
+def qrot(q, v):
+    """Eigen Quaternion * Vector3: uv = 2 (u x v); v + w uv + u x uv."""
+    u = q[1:]
+    uv = np.cross(u, v)
+    uv = uv + uv
+    return v + q[0] * uv + np.cross(u, uv)
+
+
+def slerp(q0, q1, t):
+    """Eigen 3.3.7 QuaternionBase::slerp."""
+    one = 1.0 - np.finfo(float).eps
+    d = float(np.dot(q0, q1))
+    absd = abs(d)
+    if absd >= one:
+        s0, s1 = 1.0 - t, t
+    else:
+        th = math.acos(absd)
+        st = math.sin(th)
+        s0 = math.sin((1.0 - t) * th) / st
+        s1 = math.sin(t * th) / st
+    if d < 0:
+        s1 = -s1
+    return s0 * q0 + s1 * q1
+
+
+def rotmat(q):
+    """cMathUtil::RotateMat(quaternion), 3x3."""
+    w, x, y, z = q
+    sqw, sqx, sqy, sqz = w * w, x * x, y * y, z * z
+    invs = 1 / (sqx + sqy + sqz + sqw)
+    m = np.zeros((3, 3))
+    m[0, 0] = (sqx - sqy - sqz + sqw) * invs
+    m[1, 1] = (-sqx + sqy - sqz + sqw) * invs
+    m[2, 2] = (-sqx - sqy + sqz + sqw) * invs
+    t1, t2 = x * y, z * w
+    m[1, 0] = 2.0 * (t1 + t2) * invs
+    m[0, 1] = 2.0 * (t1 - t2) * invs
+    t1, t2 = x * z, y * w
+    m[2, 0] = 2.0 * (t1 - t2) * invs
+    m[0, 2] = 2.0 * (t1 + t2) * invs
+    t1, t2 = y * z, x * w
+    m[2, 1] = 2.0 * (t1 + t2) * invs
+    m[1, 2] = 2.0 * (t1 - t2) * invs
+    return m
+
+
+def rotmat_axis(axis, theta):
+    c, s = math.cos(theta), math.sin(theta)
+    x, y, z = axis
+    return np.array([[c + x * x * (1 - c), x * y * (1 - c) - z * s, x * z * (1 - c) + y * s],
+                     [y * x * (1 - c) + z * s, c + y * y * (1 - c), y * z * (1 - c) - x * s],
+                     [z * x * (1 - c) - y * s, z * y * (1 - c) + x * s, c + z * z * (1 - c)]])
+
+
+def mat_to_quat(m):
+    """cMathUtil::RotMatToQuaternion."""
+    tr = m[0, 0] + m[1, 1] + m[2, 2]
+    if tr > 0:
+        S = math.sqrt(tr + 1.0) * 2
+        return np.array([0.25 * S, (m[2, 1] - m[1, 2]) / S, (m[0, 2] - m[2, 0]) / S, (m[1, 0] - m[0, 1]) / S])
+    if m[0, 0] > m[1, 1] and m[0, 0] > m[2, 2]:
+        S = math.sqrt(1.0 + m[0, 0] - m[1, 1] - m[2, 2]) * 2
+        return np.array([(m[2, 1] - m[1, 2]) / S, 0.25 * S, (m[0, 1] + m[1, 0]) / S, (m[0, 2] + m[2, 0]) / S])
+    if m[1, 1] > m[2, 2]:
+        S = math.sqrt(1.0 + m[1, 1] - m[0, 0] - m[2, 2]) * 2
+        return np.array([(m[0, 2] - m[2, 0]) / S, (m[0, 1] + m[1, 0]) / S, 0.25 * S, (m[1, 2] + m[2, 1]) / S])
+    S = math.sqrt(1.0 + m[2, 2] - m[0, 0] - m[1, 1]) * 2
+    return np.array([(m[1, 0] - m[0, 1]) / S, (m[0, 2] + m[2, 0]) / S, (m[1, 2] + m[2, 1]) / S, 0.25 * S])
+
+
+def quat_to_axis_angle(q):
+    """cMathUtil::QuaternionToAxisAngle."""
+    q1 = q
+    if q1[0] > 1:
+        q1 = q1 / np.linalg.norm(q1)
+    sin_t = math.sqrt(1 - q1[0] * q1[0])
+    if sin_t > 0.000001:
+        th = 2 * math.acos(q1[0])
+        th = normalize_angle(th)
+        return q1[1:] / sin_t, th
+    return np.array([0.0, 0.0, 1.0]), 0.0
+
+
+def normalize_angle(th):
+    """cMathUtil::NormalizeAngle: wrap into (-pi, pi]."""
+    th = math.fmod(th, 2 * math.pi)
+    if th < -math.pi:
+        th += 2 * math.pi
+    elif th > math.pi:
+        th -= 2 * math.pi
+    return th
+
+
+def quat_vel(q0, q1, dt):
+    """CalcQuaternionVel: world-frame angular velocity of q0 -> q1 (q_diff = q1 q0*)."""
+    axis, th = quat_to_axis_angle(qmul(q1, qconj(q0)))
+    return (th / dt) * axis
+
+
+def quat_vel_rel(q0, q1, dt):
+    """CalcQuaternionVelRel: angular velocity in the frame of q0 (q_diff = q0* q1)."""
+    axis, th = quat_to_axis_angle(qmul(qconj(q0), q1))
+    return (th / dt) * axis
+
+
+# ---- motion ------------------------------------------------------------------------------
+class Motion:
+    def __init__(self, src, joints):
+        """src: a motion file path or the parsed {"Loop", "Frames"} dict."""
+        d = src if isinstance(src, dict) else json.load(open(src))
+        self.loop = d.get("Loop", "none") != "none"
+        raw = np.array(d["Frames"], float)
+        self.joints = joints
+        durs = raw[:, 0].copy()
+        frames = raw[:, 1:].copy()
+        t, times = 0.0, np.zeros(len(raw))
+        off = frames[0, 0:3].copy()
+        off[1] = 0.0
+        for f in range(len(raw)):   # PostProcessFrames (Motion.cpp:415-442)
+            times[f] = t
+            t += durs[f]
+            frames[f, 0:3] -= off
+            self._post_process(frames[f])
+        self.times, self.frames = times, frames
+        n = len(frames)
+        vels = np.zeros_like(frames)   # BuildFrameVel (Motion.cpp:167-188)
+        for f in range(n - 1):
+            vels[f] = self.calc_vel(frames[f], frames[f + 1], times[f + 1] - times[f])
+        if n > 1:
+            vels[n - 1] = vels[n - 2]
+        self.vels = vels
+        self.duration = times[-1]
+        self.cycle_delta = frames[-1, 0:3] - frames[0, 0:3]
+        self.cycle_delta[1] = 0.0
+
+    def _post_process(self, pose):
+        pose[3:7] /= np.linalg.norm(pose[3:7])
+        for j in self.joints[1:]:
+            if j["type"] == 4:
+                o = j["offset"]
+                pose[o:o + 4] /= np.linalg.norm(pose[o:o + 4])
+
+    def calc_vel(self, p0, p1, dt):
+        """KinTree::CalcVel (KinTree.cpp:1518-1556)."""
+        out = np.zeros_like(p0)
+        out[0:3] = (p1[0:3] - p0[0:3]) / dt
+        out[3:6] = quat_vel(p0[3:7], p1[3:7], dt)
+        out[6] = 0.0
+        for j in self.joints[1:]:
+            o, s = j["offset"], j["size"]
+            if j["type"] == 4:
+                out[o:o + 3] = quat_vel_rel(p0[o:o + 4], p1[o:o + 4], dt)
+                out[o + 3] = 0.0
+            elif s > 0:
+                out[o:o + s] = (p1[o:o + s] - p0[o:o + s]) / dt
+        return out
+
+    def index_blend(self, time):
+        """Motion::CalcIndexBlend (Motion.cpp:495-522)."""
+        if not self.loop:
+            if time <= 0:
+                return 0, 0.0
+            if time >= self.duration:
+                return len(self.frames) - 2, 1.0
+        count = int(math.floor(time / self.duration))
+        if not self.loop:
+            count = min(max(count, 0), 1)
+        time -= count * self.duration
+        idx = int(np.searchsorted(self.times, time, side="right")) - 1
+        t0, t1 = self.times[idx], self.times[idx + 1]
+        return idx, (time - t0) / (t1 - t0)
+
+    def pose(self, time):
+        """MotionController::CalcPose + KinCharacter::CalcPose (origin identity)."""
+        idx, blend = self.index_blend(time)
+        blend = min(max(blend, 0.0), 1.0)   # Motion::BlendFrames saturates
+        p0, p1 = self.frames[idx], self.frames[idx + 1]
+        out = np.zeros_like(p0)
+        out[0:3] = (1 - blend) * p0[0:3] + blend * p1[0:3]
+        q = slerp(p0[3:7], p1[3:7], blend)
+        out[3:7] = q / np.linalg.norm(q)
+        for j in self.joints[1:]:
+            o, s = j["offset"], j["size"]
+            if j["type"] == 4:
+                out[o:o + 4] = slerp(p0[o:o + 4], p1[o:o + 4], blend)
+            elif s > 0:
+                out[o:o + s] = (1 - blend) * p0[o:o + s] + blend * p1[o:o + s]
+        if self.loop:
+            out[0:3] += math.floor(time / self.duration) * self.cycle_delta
+        if out[3] < 0:   # StandardizeQuat
+            out[3:7] = -out[3:7]
+        return out
+
+    def vel(self, time):
+        if not self.loop and time >= self.duration:
+            return np.zeros(self.frames.shape[1])
+        idx, blend = self.index_blend(time)
+        return (1.0 - blend) * self.vels[idx] + blend * self.vels[idx + 1]
+
+
+# ---- kinematics, reset, state ------------------------------------------------------------
+def forward_kinematics(joints, pose, vel):
+    """Joint world rotations R_j, origins o_j, angular velocities w_j and origin velocities
+    v_j (JointWorldTrans / RBDUtil::CalcWorldVel)."""
+    J = len(joints)
+    R, o, w, v = [None] * J, [None] * J, [None] * J, [None] * J
+    for j, jt in enumerate(joints):
+        if jt["parent"] < 0:
+            R[j] = rotmat(pose[3:7])
+            o[j] = pose[0:3].copy()
+            w[j] = vel[3:6].copy()
+            v[j] = vel[0:3].copy()
+            continue
+        p = jt["parent"]
+        o[j] = o[p] + R[p] @ jt["attach"]
+        off = jt["offset"]
+        if jt["type"] == 4:
+            R[j] = R[p] @ rotmat(pose[off:off + 4])
+            w[j] = w[p] + R[j] @ vel[off:off + 3]
+        elif jt["type"] == 0:
+            R[j] = R[p] @ rotmat_axis((0.0, 0.0, 1.0), pose[off])
+            w[j] = w[p] + R[j] @ np.array([0.0, 0.0, vel[off]])
+        else:   # fixed
+            R[j] = R[p].copy()
+            w[j] = w[p].copy()
+        v[j] = v[p] + np.cross(w[p], o[j] - o[p])
+    return R, o, w, v
+
+
+def body_aabb_min_y(body, R, c):
+    """Bullet 2.88 getAabb (min y) of the body's collision shape at rotation R, center c."""
+    sh, prm = body["shape"], body["param"]
+    if sh == 2:   # sphere: diameter Param0
+        return c[1] - 0.5 * prm[0]
+    if sh == 1:   # capsule: diameter Param0, cylinder height Param1, Y-up
+        half = np.array([0.5 * prm[0], 0.5 * prm[0] + 0.5 * prm[1], 0.5 * prm[0]])
+    else:         # box
+        half = 0.5 * prm
+    return c[1] - np.abs(R[1]) @ half
+
+
+def reset_state(joints, bodies, motion, time, record_world_root_pos=False, record_world_root_rot=True,
+                record_all_world=False, ground_pad=0.001):
+    """The 226-d state SimEnv.reset records after reset_time(time)."""
+    pose = motion.pose(time)
+    vel = motion.vel(time)
+    pose[0] = 0.0   # SetCharRandPlacement on the plane: root x, z -> 0 (y kept)
+    pose[2] = 0.0
+    R, o, w, v = forward_kinematics(joints, pose, vel)
+    bpos = [o[j] + R[j] @ bodies[j]["attach"] for j in range(len(joints))]
+    # ResolveCharGroundIntersect
+    min_viol = 0.0
+    for j in range(len(joints)):
+        min_viol = min(min_viol, body_aabb_min_y(bodies[j], R[j], bpos[j]) - ground_pad)
+    if min_viol < 0:
+        pose[1] += -min_viol
+        for j in range(len(joints)):
+            o[j][1] += -min_viol
+            bpos[j][1] += -min_viol
+    # CtController::BuildStatePose
+    root_pos = pose[0:3]
+    rd = qrot(pose[3:7], np.array([1.0, 0.0, 0.0]))
+    heading = math.atan2(-rd[2], rd[0])
+    Rh = rotmat_axis((0.0, 1.0, 0.0), -heading)
+    origin = np.array([root_pos[0], 0.0, root_pos[2]])
+    qh = mat_to_quat(Rh)
+
+    def to_origin(x):
+        return Rh @ (x - origin)
+
+    root_rel = to_origin(root_pos)
+    n = len(joints)
+    S = 1 + n * 9 + n * 6
+    out = np.zeros(S)
+    out[0] = root_rel[1]
+    for i in range(n):
+        p = bpos[i].copy()
+        if not record_all_world and (not record_world_root_pos or i != 0):
+            p = to_origin(p) - root_rel
+        out[9 * i + 1:9 * i + 4] = p
+        q = mat_to_quat(R[i])
+        if not record_all_world and (not record_world_root_rot or i != 0):
+            q = qmul(qh, q)
+        out[9 * i + 4:9 * i + 7] = qrot(q, np.array([0.0, 1.0, 0.0]))
+        out[9 * i + 7:9 * i + 10] = qrot(q, np.array([1.0, 0.0, 0.0]))
+    # CtController::BuildStateVel
+    base = 1 + n * 9
+    for i in range(n):
+        lv = v[i] + np.cross(w[i], bpos[i] - o[i])
+        av = w[i]
+        if not record_all_world and (not record_world_root_rot or i != 0):
+            lv, av = Rh @ lv, Rh @ av
+        out[base + 6 * i:base + 6 * i + 3] = lv
+        out[base + 6 * i + 3:base + 6 * i + 6] = av
+    return out

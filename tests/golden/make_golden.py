@@ -287,6 +287,7 @@ def main():
     make_g9()
     make_g10()
     make_g11()
+    make_g12()
     print("[make_golden] wrote fixtures to", OUT)
     return 0
 
@@ -448,6 +449,28 @@ def make_g11():
                         params0=p0, hvp_v=v, hvp=hvp, vpg=infos["vpg_grad"], npg=infos["npg_grad"],
                         surr_before=np.float64(infos["surr_before"]), surr_after=np.float64(infos["surr_after"]),
                         params1=p1)
+
+
+
+def make_g12():
+    """G12: the data the reset-from-motion path reads — the humanoid3d character file and the
+    spinkick clip (deepmimic/deepmimic/data/characters/humanoid3d.txt, data/motions/
+    humanoid3d_spinkick.txt) as the reference holds them, so the GPU box (which has no
+    /root/reference) can run the motion-reset tests.  Data only: the JSON text of the
+    character and the clip's frame array.  No reference output exists for this path (the C++
+    core is unbuildable here): the tests compare the device kernel with oracle/deepmimic_ref.py
+    ("parity unpinned")."""
+    base = os.path.join(REF, "deepmimic", "deepmimic", "data")
+    with open(os.path.join(base, "characters", "humanoid3d.txt")) as f:
+        character = f.read()
+    import json
+    motion = json.load(open(os.path.join(base, "motions", "humanoid3d_spinkick.txt")))
+    ctrl = json.load(open(os.path.join(base, "controllers", "humanoid3d_rot_ctrl.txt")))
+    np.savez_compressed(os.path.join(OUT, "g12_motion.npz"), character_json=np.array(character),
+                        frames=np.array(motion["Frames"], dtype=np.float64), loop=np.array(motion["Loop"]),
+                        record_world_root_pos=bool(ctrl.get("RecordWorldRootPos", False)),
+                        record_world_root_rot=bool(ctrl.get("RecordWorldRootRot", False)),
+                        record_all_world=bool(ctrl.get("RecordAllWorld", False)))
 
 
 if __name__ == "__main__":
