@@ -41,6 +41,8 @@ struct amx_ctx {
   long long motion_n;
   int motion_J, motion_D, motion_F;
   double motion_duration;
+  double* d_npg_scratch;     // amx_npg_reduce's run sums
+  size_t npg_scratch_bytes;
 };
 
 namespace amx {

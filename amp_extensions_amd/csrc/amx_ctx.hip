@@ -58,6 +58,7 @@ extern "C" int amx_destroy(amx_ctx* c) {
   if (!c) return AMX_OK;
   if (c->d_norm) (void)hipFree(c->d_norm);
   if (c->d_motion) (void)hipFree(c->d_motion);
+  if (c->d_npg_scratch) (void)hipFree(c->d_npg_scratch);
   free(c);
   return AMX_OK;
 }

@@ -360,12 +360,22 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   else if (t >= 128 && t < 128 + A) out[L.ls + t - 128] = a.mode == NPG_VPG ? gb : 0.0;
 }
 
-// out[c] = sum_b partials[b][c] in block order (deterministic)
-__global__ void k_npg_reduce(const double* __restrict__ part, int nb, int P, double* __restrict__ out) {
+// out[c] = sum_b partials[b][c] in a fixed order (deterministic): stage 1 sums runs of RB
+// consecutive blocks per column (grid.y = run), stage 2 sums the runs in order.
+constexpr int RB = 16;
+__global__ void k_npg_reduce1(const double* __restrict__ part, int nb, int P, double* __restrict__ mid) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= P) return;
+  const int b0 = blockIdx.y * RB, b1 = min(nb, b0 + RB);
+  double s = 0.0;
+  for (int b = b0; b < b1; ++b) s += part[(long long)b * P + c];
+  mid[(long long)blockIdx.y * P + c] = s;
+}
+__global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, double* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= P) return;
   double s = 0.0;
-  for (int b = 0; b < nb; ++b) s += part[(long long)b * P + c];
+  for (int r = 0; r < nr; ++r) s += mid[(long long)r * P + c];
   out[c] = s;
 }
 
@@ -413,8 +423,30 @@ extern "C" int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int 
 
 extern "C" int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, void* stream) {
   AMX_CHECK_ARG(ctx && partials && out && blocks > 0 && P > 0, "amx_npg_reduce: bad arguments");
-  hipLaunchKernelGGL(k_npg_reduce, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, partials, blocks, P,
-                     out);
+  const int runs = (blocks + RB - 1) / RB;
+  if (runs == 1) {
+    hipLaunchKernelGGL(k_npg_reduce2, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, partials, blocks, P,
+                       out);
+    AMX_CHECK_LAUNCH();
+    return AMX_OK;
+  }
+  // the runs' sums go to a context-owned scratch (grown on demand, freed with the context)
+  const size_t need = sizeof(double) * (size_t)runs * P;
+  if (ctx->npg_scratch_bytes < need) {
+    if (ctx->d_npg_scratch) AMX_CHECK_HIP(hipFree(ctx->d_npg_scratch));
+    ctx->d_npg_scratch = nullptr;
+    ctx->npg_scratch_bytes = 0;
+    if (hipMalloc((void**)&ctx->d_npg_scratch, need) != hipSuccess) {
+      amx::set_error("amx_npg_reduce: hipMalloc of %zu B failed", need);
+      return AMX_E_NOMEM;
+    }
+    ctx->npg_scratch_bytes = need;
+  }
+  hipLaunchKernelGGL(k_npg_reduce1, dim3((P + 255) / 256, runs), dim3(256), 0, (hipStream_t)stream, partials, blocks,
+                     P, ctx->d_npg_scratch);
+  AMX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_npg_reduce2, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, ctx->d_npg_scratch,
+                     runs, P, out);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

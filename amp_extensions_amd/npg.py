@@ -97,7 +97,8 @@ class DeviceNPG:
 
     # ---- passes --------------------------------------------------------------------------
     def _rows_per_block(self, n: int) -> int:
-        return max(32, int(math.ceil(n / 512 / 32)) * 32)
+        # one block per CU (the pass kernel holds ~140 KB of LDS): one wave of blocks
+        return max(32, int(math.ceil(n / 256 / 32)) * 32)
 
     def _pass(self, mode, obs, act, adv, vec):
         c = self.ctx
