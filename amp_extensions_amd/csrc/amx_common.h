@@ -41,6 +41,7 @@ struct amx_ctx {
   long long motion_n;
   int motion_J, motion_D, motion_F;
   double motion_duration;
+  int amp_obs_size;          // AMP observation features per transition (0: no character)
   double* d_npg_scratch;     // amx_npg_reduce's run sums
   size_t npg_scratch_bytes;
 };

@@ -293,6 +293,254 @@ __device__ void motion_state(const MView& m, double time, int flags, double* __r
   }
 }
 
+// ---- AMP observation features (scenes/SceneImitateAMP.cpp:287-475) ---------------------------
+// BuildAMPObs(prev_pose, prev_vel, pose, vel): [pose part(pose), pose part(prev), vel part(vel),
+// vel part(prev)], every part in the CURRENT pose's heading frame (ref_origin_rot):
+//   pose part = root_h, root rotation tangent-normal (world, or heading frame with
+//               enable_amp_obs_local_root), per joint: spherical -> tangent-normal of its local
+//               rotation (6), revolute -> angle (1), fixed -> nothing; end-effector body
+//               positions relative to the root joint (3 each)
+//   vel part  = root linear / angular velocity (world, or heading frame), then the raw joint
+//               velocity parameters (spherical: local angular velocity x, y, z, 0; revolute 1)
+// Kinematic quantities per joint: rotation in the heading frame Rh_j, angular velocity w_j in
+// the heading frame, root joint world velocity, end-effector offsets in the heading frame.
+struct AmpKin {
+  double R[MAXJ][9];   // joint rotations in this pose's heading frame
+  double Rw0[9];       // root rotation, world
+  V3 v0, w0;           // root joint linear / angular velocity, world
+  double jv[MAXD];     // joint velocity parameters (vel[7:] of the KinTree layout)
+  int njv;
+  V3 ee[8];            // end-effector body offsets from the root joint, this heading frame
+  double root_y;
+  double Rh[9];        // world -> this pose's heading frame
+};
+
+__device__ inline void tn_mat(const double* nt, double* R) {  // columns tan, nrm, tan x nrm
+  const V3 n = {nt[0], nt[1], nt[2]}, t = {nt[3], nt[4], nt[5]};
+  const V3 z = cross(t, n);
+  R[0] = t.x; R[1] = n.x; R[2] = z.x;
+  R[3] = t.y; R[4] = n.y; R[5] = z.y;
+  R[6] = t.z; R[7] = n.z; R[8] = z.z;
+}
+__device__ inline void heading_of(const double* Rw0, double* Rh) {  // KinTree::CalcHeadingRot
+  const double heading = atan2(-Rw0[6], Rw0[0]);                    // R e_x = column 0
+  axis_mat({0.0, 1.0, 0.0}, -heading, Rh);
+}
+__device__ inline V3 mtv(const double* m, V3 v) {  // m^T v
+  return {m[0] * v.x + m[3] * v.y + m[6] * v.z, m[1] * v.x + m[4] * v.y + m[7] * v.z,
+          m[2] * v.x + m[5] * v.y + m[8] * v.z};
+}
+__device__ inline void mtm(const double* a, const double* b, double* o) {  // a^T b
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) o[3 * i + j] = a[i] * b[j] + a[3 + i] * b[3 + j] + a[6 + i] * b[6 + j];
+}
+
+// kinematics of a recorded SimEnv state (CtController layout with the root rotation and the
+// root velocities in the world frame, RecordWorldRootRot): rotations from the tangent-normal
+// pairs (R = [tan, nrm, tan x nrm]), joint velocity parameters from the body angular
+// velocities (spherical: R_j^T (w_j - w_parent), revolute: its z component)
+__device__ void kin_from_state(const MView& m, const double* s, AmpKin& k) {
+  const int n = m.J, base = 1 + 9 * n;
+  k.root_y = s[0];
+  tn_mat(s + 4, k.Rw0);
+  heading_of(k.Rw0, k.Rh);
+  mm(k.Rh, k.Rw0, k.R[0]);
+  for (int i = 1; i < n; ++i) tn_mat(s + 9 * i + 4, k.R[i]);
+  V3 w[MAXJ];
+  k.w0 = {s[base + 3], s[base + 4], s[base + 5]};
+  w[0] = mv(k.Rh, k.w0);
+  for (int i = 1; i < n; ++i) w[i] = {s[base + 6 * i + 3], s[base + 6 * i + 4], s[base + 6 * i + 5]};
+  // root joint velocity: body-0 velocity minus w0 x (body-0 offset, back in the world frame)
+  const V3 off = mtv(k.Rh, {s[1], s[2], s[3]});
+  k.v0 = sub({s[base], s[base + 1], s[base + 2]}, cross(k.w0, off));
+  int c = 0;
+  for (int j = 1; j < n; ++j) {
+    const double* jt = m.joints + 8 * j;
+    const int type = (int)jt[0], par = (int)jt[1];
+    if (type == JT_SPHERICAL || type == JT_REVOLUTE) {
+      const V3 wl = mtv(k.R[j], sub(w[j], w[par]));
+      if (type == JT_SPHERICAL) {
+        k.jv[c++] = wl.x; k.jv[c++] = wl.y; k.jv[c++] = wl.z; k.jv[c++] = 0.0;
+      } else {
+        k.jv[c++] = wl.z;
+      }
+    }
+  }
+  k.njv = c;
+  int e = 0;
+  for (int j = 0; j < n && e < 8; ++j)
+    if (m.joints[8 * j + 7] != 0.0) k.ee[e++] = {s[9 * j + 1], s[9 * j + 2], s[9 * j + 3]};
+}
+
+// kinematics of a clip pose / velocity (Motion::CalcFrame / CalcFrameVel)
+__device__ void kin_from_pose(const MView& m, const double* pose, const double* vel, AmpKin& k) {
+  double R[MAXJ][9];
+  V3 o[MAXJ];
+  k.root_y = pose[1];
+  qmat(ldq(pose + 3), k.Rw0);
+  heading_of(k.Rw0, k.Rh);
+  k.w0 = {vel[3], vel[4], vel[5]};
+  k.v0 = {vel[0], vel[1], vel[2]};
+  for (int q = 0; q < 9; ++q) R[0][q] = k.Rw0[q];
+  o[0] = {pose[0], pose[1], pose[2]};
+  for (int j = 1; j < m.J; ++j) {
+    const double* jt = m.joints + 8 * j;
+    const int type = (int)jt[0], par = (int)jt[1], off = (int)jt[2];
+    o[j] = add(o[par], mv(R[par], {jt[4], jt[5], jt[6]}));
+    double L[9];
+    if (type == JT_SPHERICAL) {
+      qmat(ldq(pose + off), L);
+      mm(R[par], L, R[j]);
+    } else if (type == JT_REVOLUTE) {
+      axis_mat({0.0, 0.0, 1.0}, pose[off], L);
+      mm(R[par], L, R[j]);
+    } else {
+      for (int q = 0; q < 9; ++q) R[j][q] = R[par][q];
+    }
+  }
+  for (int j = 0; j < m.J; ++j) mm(k.Rh, R[j], k.R[j]);
+  k.njv = m.D - 7;
+  for (int i = 0; i < k.njv; ++i) k.jv[i] = vel[7 + i];
+  int e = 0;
+  for (int j = 0; j < m.J && e < 8; ++j)
+    if (m.joints[8 * j + 7] != 0.0) {
+      const double* bd = m.bodies + 8 * j;
+      k.ee[e++] = mv(k.Rh, sub(add(o[j], mv(R[j], {bd[1], bd[2], bd[3]})), o[0]));
+    }
+}
+
+// one pose part / one vel part; Rc = the current pose's heading rotation (ref_origin_rot)
+__device__ int amp_pose_part(const MView& m, const AmpKin& k, const double* Rc, bool local_root, double* out) {
+  int c = 0;
+  out[c++] = k.root_y;
+  double R0[9];
+  if (local_root) {
+    mm(Rc, k.Rw0, R0);
+  } else {
+    for (int q = 0; q < 9; ++q) R0[q] = k.Rw0[q];
+  }
+  out[c++] = R0[1]; out[c++] = R0[4]; out[c++] = R0[7];   // norm = R e_y
+  out[c++] = R0[0]; out[c++] = R0[3]; out[c++] = R0[6];   // tan  = R e_x
+  for (int j = 1; j < m.J; ++j) {
+    const double* jt = m.joints + 8 * j;
+    const int type = (int)jt[0], par = (int)jt[1];
+    if (type == JT_SPHERICAL || type == JT_REVOLUTE) {
+      double L[9];
+      mtm(k.R[par], k.R[j], L);
+      if (type == JT_SPHERICAL) {
+        out[c++] = L[1]; out[c++] = L[4]; out[c++] = L[7];
+        out[c++] = L[0]; out[c++] = L[3]; out[c++] = L[6];
+      } else {
+        out[c++] = atan2(L[3], L[0]);
+      }
+    }
+  }
+  // end effectors: this pose's heading-frame offsets re-expressed in the current heading
+  // frame (Rc Rh^T)
+  double Rx[9];
+  for (int i = 0; i < 3; ++i)
+    for (int jj = 0; jj < 3; ++jj)
+      Rx[3 * i + jj] = Rc[3 * i] * k.Rh[3 * jj] + Rc[3 * i + 1] * k.Rh[3 * jj + 1] + Rc[3 * i + 2] * k.Rh[3 * jj + 2];
+  int e = 0;
+  for (int j = 0; j < m.J && e < 8; ++j)
+    if (m.joints[8 * j + 7] != 0.0) {
+      const V3 p = mv(Rx, k.ee[e++]);
+      out[c++] = p.x; out[c++] = p.y; out[c++] = p.z;
+    }
+  return c;
+}
+
+__device__ int amp_vel_part(const AmpKin& k, const double* Rc, bool local_root, double* out) {
+  int c = 0;
+  V3 v = k.v0, w = k.w0;
+  if (local_root) {
+    v = mv(Rc, v);
+    w = mv(Rc, w);
+  }
+  out[c++] = v.x; out[c++] = v.y; out[c++] = v.z;
+  out[c++] = w.x; out[c++] = w.y; out[c++] = w.z;
+  for (int i = 0; i < k.njv; ++i) out[c++] = k.jv[i];
+  return c;
+}
+
+__device__ void amp_obs(const MView& m, const AmpKin& prev, const AmpKin& cur, bool local_root, double* out) {
+  int c = 0;
+  c += amp_pose_part(m, cur, cur.Rh, local_root, out + c);
+  c += amp_pose_part(m, prev, cur.Rh, local_root, out + c);
+  c += amp_vel_part(cur, cur.Rh, local_root, out + c);
+  c += amp_vel_part(prev, cur.Rh, local_root, out + c);
+}
+
+// raw clip frame and velocity at `time` (Motion::CalcFrame / CalcFrameVel)
+__device__ void clip_frame(const MView& m, double time, double* pose, double* vel) {
+  const double dur = m.h[4];
+  const bool loop = m.h[3] != 0.0;
+  int idx;
+  double blend;
+  if (!loop && time <= 0.0) {
+    idx = 0; blend = 0.0;
+  } else if (!loop && time >= dur) {
+    idx = m.F - 2; blend = 1.0;
+  } else {
+    double cnt = floor(time / dur);
+    if (!loop) cnt = fmin(fmax(cnt, 0.0), 1.0);
+    const double tt = time - cnt * dur;
+    int lo = 0, hi = m.F;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (m.times[mid] <= tt) lo = mid + 1; else hi = mid;
+    }
+    idx = min(max(lo - 1, 0), m.F - 2);
+    blend = (tt - m.times[idx]) / (m.times[idx + 1] - m.times[idx]);
+  }
+  const double lerp = fmin(fmax(blend, 0.0), 1.0);
+  const double* f0 = m.frames + (long long)idx * m.D;
+  const double* f1 = f0 + m.D;
+  const double* v0 = m.vels + (long long)idx * m.D;
+  const double* v1 = v0 + m.D;
+  for (int i = 0; i < m.D; ++i) {
+    pose[i] = (1 - lerp) * f0[i] + lerp * f1[i];
+    vel[i] = (!loop && time >= dur) ? 0.0 : (1.0 - blend) * v0[i] + blend * v1[i];
+  }
+  const Q q = qnorm(slerp(ldq(f0 + 3), ldq(f1 + 3), lerp));
+  pose[3] = q.w; pose[4] = q.x; pose[5] = q.y; pose[6] = q.z;
+  for (int j = 1; j < m.J; ++j) {
+    const double* jt = m.joints + 8 * j;
+    if ((int)jt[0] == JT_SPHERICAL) {
+      const int o = (int)jt[2];
+      const Q r = slerp(ldq(f0 + o), ldq(f1 + o), lerp);
+      pose[o] = r.w; pose[o + 1] = r.x; pose[o + 2] = r.y; pose[o + 3] = r.z;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_state_amp_obs(const double* __restrict__ blob, const double* __restrict__ sp,
+                                                      const double* __restrict__ sc, long long lds, int B,
+                                                      int local_root, double* __restrict__ out, long long ldo) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const MView m(blob);
+  AmpKin kp, kc;
+  kin_from_state(m, sp + (long long)b * lds, kp);
+  kin_from_state(m, sc + (long long)b * lds, kc);
+  amp_obs(m, kp, kc, local_root != 0, out + (long long)b * ldo);
+}
+
+__global__ __launch_bounds__(64) void k_motion_amp_obs(const double* __restrict__ blob, const double* __restrict__ times,
+                                                       double dt, int B, int local_root, double* __restrict__ out,
+                                                       long long ldo) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const MView m(blob);
+  double pose[MAXD], vel[MAXD];
+  AmpKin kp, kc;
+  clip_frame(m, times[b] - dt, pose, vel);
+  kin_from_pose(m, pose, vel, kp);
+  clip_frame(m, times[b], pose, vel);
+  kin_from_pose(m, pose, vel, kc);
+  amp_obs(m, kp, kc, local_root != 0, out + (long long)b * ldo);
+}
+
 __global__ __launch_bounds__(64) void k_motion_states(const double* __restrict__ blob, const double* __restrict__ times,
                                                       int B, int flags, double* __restrict__ ob, long long ldo) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
@@ -371,6 +619,17 @@ extern "C" int amx_set_motion(amx_ctx* c, const double* blob, long long n) {
   c->motion_D = D;
   c->motion_F = F;
   c->motion_duration = blob[4];
+  // SceneImitateAMP::GetAMPObsSize (scenes/SceneImitateAMP.cpp:101-110, 287-330)
+  int pose = 1 + 6, vel = 6, ee = 0;
+  for (int j = 1; j < J; ++j) {
+    const double* jt = blob + HDR + 8 * j;
+    const int type = (int)jt[0];
+    pose += type == JT_SPHERICAL ? 6 : (int)jt[3];
+    vel += (int)jt[3];
+  }
+  for (int j = 0; j < J; ++j) ee += blob[HDR + 8 * j + 7] != 0.0;
+  AMX_CHECK_ARG(ee <= 8, "amx_set_motion: %d end effectors (max 8)", ee);
+  c->amp_obs_size = 2 * (pose + 3 * ee) + 2 * vel;
   return AMX_OK;
 }
 
@@ -397,6 +656,35 @@ extern "C" int amx_reset_lanes_motion(amx_ctx* c, const uint8_t* mask, const dou
   hipLaunchKernelGGL(k_reset_motion, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->d_motion, mask, times,
                      (uint32_t)seed, (uint32_t)(seed >> 32), flags, ob_src, ob_out, num_steps, model_idx,
                      reset_count, t_out, c->S, c->M, B);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+// ---- AMP observation features ----------------------------------------------------------------
+extern "C" int amx_amp_obs_size(const amx_ctx* c) {
+  if (!c || !c->d_motion) return -1;
+  return c->amp_obs_size;
+}
+
+extern "C" int amx_state_amp_obs(amx_ctx* c, const double* s_prev, const double* s_cur, long long lds, int B,
+                                 int local_root, double* out, long long ldo, void* stream) {
+  AMX_CHECK_ARG(c && c->d_motion, "amx_state_amp_obs: no character set (amx_set_motion)");
+  AMX_CHECK_ARG(s_prev && s_cur && out && B >= 0 && lds >= c->S && ldo >= c->amp_obs_size,
+                "amx_state_amp_obs: bad arguments (lds=%lld ldo=%lld)", lds, ldo);
+  if (B == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_state_amp_obs, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->d_motion, s_prev,
+                     s_cur, lds, B, local_root, out, ldo);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_motion_amp_obs(amx_ctx* c, const double* times, double dt, int B, int local_root, double* out,
+                                  long long ldo, void* stream) {
+  AMX_CHECK_ARG(c && c->d_motion, "amx_motion_amp_obs: no motion set (amx_set_motion)");
+  AMX_CHECK_ARG(times && out && B >= 0 && ldo >= c->amp_obs_size, "amx_motion_amp_obs: bad arguments");
+  if (B == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_motion_amp_obs, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->d_motion, times,
+                     dt, B, local_root, out, ldo);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

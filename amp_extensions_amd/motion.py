@@ -57,7 +57,7 @@ def _conj(q):
 
 
 def skeleton_tables(character: dict):
-    """Joint table [J][8] (type, parent, offset, size, attach xyz, 0) and body table [J][8]
+    """Joint table [J][8] (type, parent, offset, size, attach xyz, is-end-effector) and body table [J][8]
     (shape, attach xyz, Param0-2, valid) of a parsed character file."""
     joints = character["Skeleton"]["Joints"]
     bodies = {b["ID"]: b for b in character["BodyDefs"]}
@@ -74,7 +74,7 @@ def skeleton_tables(character: dict):
         if any(d.get(k, 0.0) != 0.0 for k in ("AttachThetaX", "AttachThetaY", "AttachThetaZ")):
             raise NotImplementedError("non-zero joint AttachTheta")
         attach = [0.0, 0.0, 0.0] if d["Parent"] == -1 else [d["AttachX"], d["AttachY"], d["AttachZ"]]
-        jt[j] = [t, d["Parent"], off, _PARAM_SIZE[t], *attach, 0.0]
+        jt[j] = [t, d["Parent"], off, _PARAM_SIZE[t], *attach, float(d.get("IsEndEffector", 0))]
         off += _PARAM_SIZE[t]
         b = bodies.get(j)
         if b is not None:
@@ -158,6 +158,39 @@ class ReferenceMotion:
         N.check(ctx.lib.amx_set_motion(ctx.h, self.blob.ctypes.data, self.blob.size), "amx_set_motion")
         self.duration = float(times[-1])
         self.S = ctx.S
+
+    @property
+    def amp_obs_size(self) -> int:
+        """SceneImitateAMP::GetAMPObsSize (2 x (pose part + vel part); humanoid3d: 226)."""
+        return int(self.ctx.lib.amx_amp_obs_size(self.ctx.h))
+
+    def expert_amp_obs(self, times, dt: float = 1.0 / 30, local_root: bool = False) -> torch.Tensor:
+        """RecordAMPObsExpert (scenes/SceneImitateAMP.cpp:167-193) at the given clip times:
+        BuildAMPObs of the clip frame at t - dt (prev) and t, dt = 1 / UpdateRate."""
+        c = self.ctx
+        t = torch.as_tensor(times, dtype=torch.float64).reshape(-1).to(c.device).contiguous()
+        D = self.amp_obs_size
+        out = torch.empty(t.numel(), D, dtype=torch.float64, device=c.device)
+        N.check(c.lib.amx_motion_amp_obs(c.h, t.data_ptr(), float(dt), t.numel(), int(local_root), out.data_ptr(), D,
+                                         c.stream), "amx_motion_amp_obs")
+        return out
+
+    def amp_obs_from_states(self, s_prev: torch.Tensor, s_cur: torch.Tensor, local_root: bool = False,
+                            out: torch.Tensor | None = None) -> torch.Tensor:
+        """RecordAMPObsAgent (BuildAMPObs of the previous and the current simulated pose) from
+        two recorded SimEnv states per row ([B, S] float64, CtController layout with
+        RecordWorldRootRot): the joint rotations, joint velocities and root velocity are
+        recovered from the tangent-normal rotations and body velocities of the states."""
+        if self.flags != 2:
+            raise NotImplementedError("AMP features from states need RecordWorldRootRot only (humanoid3d_rot_ctrl)")
+        c = self.ctx
+        B = s_cur.shape[0]
+        D = self.amp_obs_size
+        if out is None:
+            out = torch.empty(B, D, dtype=torch.float64, device=c.device)
+        N.check(c.lib.amx_state_amp_obs(c.h, s_prev.data_ptr(), s_cur.data_ptr(), s_cur.stride(0), B, int(local_root),
+                                        out.data_ptr(), out.stride(0), c.stream), "amx_state_amp_obs")
+        return out
 
     def get_motion_length(self) -> float:
         """DeepMimicEnv.get_motion_length (SimEnv's time_max, sim_env.py:77)."""

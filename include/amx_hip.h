@@ -166,6 +166,21 @@ int amx_reset_lanes_motion(amx_ctx* ctx, const uint8_t* mask, const double* time
                            int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
                            int32_t* model_idx, int32_t* reset_count, double* t_out, int B, void* stream);
 
+/* AMP observation features (SceneImitateAMP::BuildAMPObs, deepmimic/deepmimic/DeepMimicCore/
+ * scenes/SceneImitateAMP.cpp:352-475; the discriminator input of the original AMP agent):
+ * [pose(cur), pose(prev), vel(cur), vel(prev)] in the current heading frame, amx_amp_obs_size
+ * doubles per row (humanoid3d: 226).  Needs amx_set_motion's character tables.
+ *   amx_state_amp_obs:  from recorded SimEnv states (s_prev, s_cur) [B][lds] — the agent's
+ *                       features of a transition (RecordAMPObsAgent, :154-165);
+ *   amx_motion_amp_obs: from the clip at times[b] - dt and times[b] (RecordAMPObsExpert,
+ *                       :167-193; dt = 1 / UpdateRate).
+ * local_root = enable_amp_obs_local_root (default false, :29). */
+int amx_amp_obs_size(const amx_ctx* ctx);
+int amx_state_amp_obs(amx_ctx* ctx, const double* s_prev, const double* s_cur, long long lds, int B,
+                      int local_root, double* out, long long ldo, void* stream);
+int amx_motion_amp_obs(amx_ctx* ctx, const double* times, double dt, int B, int local_root, double* out,
+                       long long ldo, void* stream);
+
 /* ---- NPG policy update (the rollout's learner; mjrl/mjrl/algos/npg_cg.py:113-199) ----
  * Policy: mjrl MLP(S -> 32 -> 32 -> A, tanh) + log_std (mjrl/mjrl/policies/gaussian_mlp.py),
  * parameters packed in the reference's flat order (W1, b1, W2, b2, W3, b3, log_std; fp32,

@@ -372,3 +372,88 @@ def reset_state(joints, bodies, motion, time, record_world_root_pos=False, recor
         out[base + 6 * i:base + 6 * i + 3] = lv
         out[base + 6 * i + 3:base + 6 * i + 6] = av
     return out
+
+
+# ---- AMP observation features (scenes/SceneImitateAMP.cpp:287-475) -----------------------
+def end_effectors(char_src):
+    d = char_src if isinstance(char_src, dict) else json.loads(char_src)
+    return [j["ID"] for j in d["Skeleton"]["Joints"] if j.get("IsEndEffector", 0)]
+
+
+def motion_frame(M, time):
+    """Motion::CalcFrame (raw clip blend: no cycle offset, no root StandardizeQuat)."""
+    idx, blend = M.index_blend(time)
+    blend = min(max(blend, 0.0), 1.0)
+    p0, p1 = M.frames[idx], M.frames[idx + 1]
+    out = (1 - blend) * p0 + blend * p1
+    q = slerp(p0[3:7], p1[3:7], blend)
+    out[3:7] = q / np.linalg.norm(q)
+    for j in M.joints[1:]:
+        if j["type"] == 4:
+            o = j["offset"]
+            out[o:o + 4] = slerp(p0[o:o + 4], p1[o:o + 4], blend)
+    return out
+
+
+def heading_rot(q):
+    """KinTree::CalcHeadingRot: rotation about y by -heading (3x3)."""
+    rd = qrot(q, np.array([1.0, 0.0, 0.0]))
+    return rotmat_axis((0.0, 1.0, 0.0), -math.atan2(-rd[2], rd[0]))
+
+
+def amp_obs_pose(joints, bodies, ee, pose, Rh, local_root=False, ground_h=0.0):
+    """RecordAMPObsPose (SceneImitateAMP.cpp:370-439)."""
+    out = [pose[1] - ground_h]
+    R0 = rotmat(pose[3:7])
+    if local_root:
+        R0 = Rh @ R0
+    out += list(R0[:, 1]) + list(R0[:, 0])   # tan-norm: R e_y (norm), R e_x (tan)
+    for j in joints[1:]:
+        o = j["offset"]
+        if j["type"] == 4:
+            L = rotmat(pose[o:o + 4])
+            out += list(L[:, 1]) + list(L[:, 0])
+        elif j["size"] > 0:
+            out += list(pose[o:o + j["size"]])
+    R, org, _, _ = forward_kinematics(joints, pose, np.zeros(len(pose)))
+    for e in ee:
+        p = org[e] + R[e] @ bodies[e]["attach"] - pose[0:3]
+        out += list(Rh @ p)
+    return np.array(out)
+
+
+def amp_obs_vel(joints, vel, Rh, local_root=False):
+    """RecordAMPObsVel (SceneImitateAMP.cpp:441-475)."""
+    v, w = vel[0:3], vel[3:6]
+    if local_root:
+        v, w = Rh @ v, Rh @ w
+    return np.concatenate([v, w, vel[7:]])
+
+
+def amp_obs(joints, bodies, ee, prev_pose, prev_vel, pose, vel, local_root=False, ground_h=0.0):
+    """BuildAMPObs (SceneImitateAMP.cpp:352-368): [pose, prev pose, vel, prev vel] in the
+    current pose's heading frame."""
+    Rh = heading_rot(pose[3:7])
+    return np.concatenate([amp_obs_pose(joints, bodies, ee, pose, Rh, local_root, ground_h),
+                           amp_obs_pose(joints, bodies, ee, prev_pose, Rh, local_root, ground_h),
+                           amp_obs_vel(joints, vel, Rh, local_root), amp_obs_vel(joints, prev_vel, Rh, local_root)])
+
+
+def expert_amp_obs(joints, bodies, ee, M, time, dt=1.0 / 30, local_root=False):
+    """RecordAMPObsExpert (SceneImitateAMP.cpp:167-193) at a given clip time."""
+    return amp_obs(joints, bodies, ee, motion_frame(M, time - dt), M.vel(time - dt), motion_frame(M, time),
+                   M.vel(time), local_root)
+
+
+def reset_pose_vel(joints, bodies, M, time, ground_pad=0.001):
+    """(pose, vel) of the simulated character after reset_time(time): the pose reset_state
+    records (placement on the plane and the ground lift applied)."""
+    pose = M.pose(time)
+    vel = M.vel(time)
+    pose[0] = pose[2] = 0.0
+    R, o, w, v = forward_kinematics(joints, pose, vel)
+    lows = [body_aabb_min_y(bodies[j], R[j], o[j] + R[j] @ bodies[j]["attach"]) - ground_pad
+            for j in range(len(joints))]
+    lift = -min(0.0, min(lows))
+    pose[1] += lift
+    return pose, vel

@@ -112,3 +112,43 @@ def test_simenv_facade_motion_reset(setup):
         assert env.last_reset_time == t
         ref = D.reset_state(J, B, M, t)
         assert np.abs(ob - ref).max() <= 1e-10 * max(1.0, np.abs(ref).max())
+
+
+def test_expert_amp_obs_match_oracle(setup):
+    """RecordAMPObsExpert features from the clip (prev frame at t - 1/30) vs the oracle's
+    BuildAMPObs restatement; both local_root settings."""
+    amx, ctx, rm, J, B, M = setup
+    import json
+    ee = [5, 8, 11, 14]
+    assert rm.amp_obs_size == 226
+    rs = np.random.RandomState(3)
+    times = np.concatenate([[0.0, 0.01, M.duration * 0.999], rs.uniform(0, M.duration, 200)])
+    for local in (False, True):
+        got = rm.expert_amp_obs(times, local_root=local).cpu().numpy()
+        ref = np.stack([D.expert_amp_obs(J, B, ee, M, t, local_root=local) for t in times])
+        err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= 1e-10, (local, err.max(), np.unravel_index(err.argmax(), err.shape))
+
+
+def test_state_amp_obs_recovers_the_pose_features(setup):
+    """AMP features of a SimEnv transition computed from the two recorded states equal
+    BuildAMPObs of the simulated character's (pose, vel) pair the states were recorded from
+    (joint rotations / velocities recovered from the tangent-normal rotations and body
+    velocities of the states)."""
+    amx, ctx, rm, J, B, M = setup
+    ee = [5, 8, 11, 14]
+    dt = 1.0 / 30
+    rs = np.random.RandomState(4)
+    times = rs.uniform(dt, M.duration, 100)
+    sp = rm.states(times - dt)
+    sc = rm.states(times)
+    for local in (False, True):
+        got = rm.amp_obs_from_states(sp, sc, local_root=local).cpu().numpy()
+        ref = []
+        for t in times:
+            pp, vp = D.reset_pose_vel(J, B, M, t - dt)
+            pc, vc = D.reset_pose_vel(J, B, M, t)
+            ref.append(D.amp_obs(J, B, ee, pp, vp, pc, vc, local_root=local))
+        ref = np.stack(ref)
+        err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+        assert err.max() <= 1e-9, (local, err.max(), np.unravel_index(err.argmax(), err.shape))
