@@ -61,8 +61,11 @@ SIGNATURES = {
     "amx_sum_partials": (c_int, [vp, vp, c_int, c_int, vp, vp]),
     "amx_mmd_fit": (c_int, [vp, vp, c_dbl, vp, c_int, vp, vp, vp]),
     "amx_mmd_reward": (c_int, [vp, vp, c_int, vp, c_int, vp, c_flt, c_dbl, c_flt, c_flt, vp, vp, vp, c_int, vp]),
+    "amx_mmd_reward_raw": (c_int, [vp, vp, c_int, vp, c_int, vp, c_dbl, vp, vp, vp, c_int, vp]),
     "amx_expert_cost": (c_int, [vp, vp, c_int, vp, c_int, c_int, c_flt, c_flt, vp, vp]),
     "amx_amp_reward": (c_int, [vp, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
+    "amx_disc_reward": (c_int, [vp, c_int, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
+    "amx_cost_rows": (c_int, [vp, vp, c_ll, c_int, vp, c_ll, c_int, vp, c_ll, c_int, c_int, vp, c_int, vp]),
     "amx_value_features": (c_int, [vp, c_int, c_int, vp, vp, vp, c_ll, vp, vp, c_int, vp, c_int, vp]),
     "amx_value_head": (c_int, [vp, c_int, vp, c_int, c_int, vp, vp, vp, vp]),
     "amx_gae": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, vp, c_ll, vp, c_dbl, c_dbl, vp, vp, vp]),
@@ -75,6 +78,7 @@ AMX_K_TILE = 32
 AMX_SHAPE_SPHERE, AMX_SHAPE_CAPSULE, AMX_SHAPE_BOX = 0, 1, 2
 AMX_ACT_NONE, AMX_ACT_RELU = 0, 1
 AMX_IN_F64, AMX_IN_F32 = 0, 1
+AMX_DISC_LEAST_SQUARES, AMX_DISC_LOG_LIKELIHOOD = 0, 1
 
 
 class AmxNativeError(RuntimeError):

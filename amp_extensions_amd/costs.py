@@ -18,6 +18,43 @@ import torch.nn as nn
 from . import _native as N
 from .engine import AmxContext, RffMap, round_up, split_bf16x3
 
+# cost-input row of a transition (linear_cost.py:115-127, gail_cost.py:258-268); "amp" is
+# the AMP observation of (s, s') (SceneImitateAMP::BuildAMPObs, via a ReferenceMotion)
+INPUT_TYPES = ("ss", "sa", "sas", "s", "amp")
+
+
+def input_width(input_type: str, S: int, A: int, motion=None) -> int:
+    """Width of the cost-input row of `input_type` for state size S and action size A."""
+    if input_type == "amp":
+        if motion is None:
+            raise ValueError("input_type 'amp' needs the ReferenceMotion (motion=...)")
+        return motion.amp_obs_size
+    return {"ss": 2 * S, "sa": S + A, "sas": 2 * S + A, "s": S}[input_type]
+
+
+def cost_input(input_type: str, states, actions, next_states, motion=None) -> torch.Tensor:
+    """float32 cost-input rows [n, width] of `input_type` (the reference's torch.cat branches)."""
+    if input_type == "sa":
+        return torch.cat([states.float(), actions.float()], dim=1)
+    if input_type == "ss":
+        assert next_states is not None
+        return torch.cat([states.float(), next_states.float()], dim=1)
+    if input_type == "sas":
+        return torch.cat([states.float(), actions.float(), next_states.float()], dim=1)
+    if input_type == "s":
+        return states.float()
+    if input_type == "amp":
+        assert next_states is not None and motion is not None
+        return motion.amp_obs_from_states(states.double().contiguous(), next_states.double().contiguous()).float()
+    raise NotImplementedError("Input type not implemented")
+
+
+def _check_input_type(input_type: str, motion) -> None:
+    if input_type not in INPUT_TYPES:
+        raise NotImplementedError("Input type not implemented")
+    if input_type == "amp" and motion is None:
+        raise ValueError("input_type 'amp' needs the ReferenceMotion (motion=...)")
+
 
 class RBFLinearCost:
     """MMD cost with random-Fourier-feature representations (linear_cost.py:6-152).
@@ -28,20 +65,22 @@ class RBFLinearCost:
 
     def __init__(self, expert_data: torch.Tensor, feature_dim=1024, input_type="ss", cost_range=(-1.0, 0.0),
                  bw_quantile=0.1, bw_samples=100000, lambda_b=1.0, lr=0.0, seed=100, ctx: AmxContext | None = None,
-                 device="cuda", gemm: str = "bf16x6"):
+                 device="cuda", gemm: str = "bf16x6", motion=None):
         """`gemm` selects the feature GEMM: "bf16x6" (3-limb bf16 split, fp32-level error) or
-        "f32" (f32 MFMA); everything else follows the reference constructor."""
+        "f32" (f32 MFMA); `motion` (a ReferenceMotion) is needed for input_type "amp" (expert
+        rows = AMP observations); everything else follows the reference constructor."""
+        _check_input_type(input_type, motion)
         torch.manual_seed(seed)          # linear_cost.py:34-35
         np.random.seed(seed)
         expert_cpu = expert_data.detach().float().cpu()
         input_dim = expert_cpu.size(1)
         self.input_type = input_type
+        self.input_dim = input_dim
+        self.motion = motion
         self.feature_dim = feature_dim
         self.cost_range = cost_range
         if cost_range is not None:
             self.c_min, self.c_max = float(cost_range[0]), float(cost_range[1])
-        else:
-            raise NotImplementedError("cost_range=None (unclamped cost) is not on the MILO path")
         self.lambda_b = float(lambda_b)
         self.lr = lr
         self.quantile = bw_quantile
@@ -102,13 +141,25 @@ class RBFLinearCost:
         reward = torch.empty(n, dtype=torch.float32, device=c.device)
         ipm = torch.empty(n, dtype=torch.float32, device=c.device)
         wb = torch.empty(n, dtype=torch.float32, device=c.device)
-        N.check(c.lib.amx_mmd_reward(c.h, phi.data_ptr(), phi.stride(0), self.w.data_ptr(), self.feature_dim,
-                                     disc.data_ptr(), float(thr), self.lambda_b, self.c_min, self.c_max,
-                                     reward.data_ptr(), ipm.data_ptr(), wb.data_ptr(), n, c.stream), "amx_mmd_reward")
+        self.reward_launch(phi.data_ptr(), phi.stride(0), disc.data_ptr(), float(thr), reward.data_ptr(),
+                           ipm.data_ptr(), wb.data_ptr(), n)
         return reward, ipm, wb
 
+    def reward_launch(self, phi, ldphi: int, disc, thr: float, reward, ipm, wb, n: int) -> None:
+        """amx_mmd_reward (cost_range given) or amx_mmd_reward_raw (cost_range None) on raw
+        device pointers."""
+        c = self.ctx
+        if self.cost_range is not None:
+            N.check(c.lib.amx_mmd_reward(c.h, phi, ldphi, self.w.data_ptr(), self.feature_dim, disc, thr,
+                                         self.lambda_b, self.c_min, self.c_max, reward, ipm, wb, n, c.stream),
+                    "amx_mmd_reward")
+        else:
+            N.check(c.lib.amx_mmd_reward_raw(c.h, phi, ldphi, self.w.data_ptr(), self.feature_dim, disc,
+                                             self.lambda_b, reward, ipm, wb, n, c.stream), "amx_mmd_reward_raw")
+
     def get_costs(self, x: torch.Tensor) -> torch.Tensor:
-        """linear_cost.py:96-103: clamp(phi(x).w, c_min, c_max) [n, 1]."""
+        """linear_cost.py:96-103: clamp(phi(x).w, c_min, c_max) [n, 1] (unclamped when
+        cost_range is None)."""
         phi = self.get_rep(x)
         n = phi.shape[0]
         zeros = torch.zeros(n, dtype=torch.float32, device=self.ctx.device)
@@ -122,6 +173,8 @@ class RBFLinearCost:
 
     def get_expert_cost(self) -> torch.Tensor:
         """linear_cost.py:105-109 over the resident expert features."""
+        if self.cost_range is None:   # the reference clamps with c_min/c_max, unset without a range
+            raise AttributeError("'RBFLinearCost' object has no attribute 'c_min'")
         c = self.ctx
         N.check(c.lib.amx_expert_cost(c.h, self.expert_rep.data_ptr(), self.expert_rep.stride(0), self.w.data_ptr(),
                                       self.feature_dim, self.n_expert, self.c_min, self.c_max,
@@ -130,11 +183,8 @@ class RBFLinearCost:
         return np.float32(1 - self.lambda_b) * mean
 
     def get_bonus_costs(self, states, actions, ensemble, next_states=None):
-        """linear_cost.py:111-152 (input_type 'ss'): cost [T, 1] and the info dict."""
-        if self.input_type != "ss":
-            raise NotImplementedError("only the 'ss' cost input of the MILO humanoid path is implemented")
-        assert next_states is not None
-        x = torch.cat([states.float(), next_states.float()], dim=1)
+        """linear_cost.py:111-152: cost [T, 1] and the info dict."""
+        x = cost_input(self.input_type, states, actions, next_states, self.motion)
         phi = self.get_rep(x)
         disc = ensemble.get_action_discrepancy(states, actions)
         reward, ipm, wb = self._values(phi, disc, ensemble.threshold)
@@ -150,9 +200,11 @@ class GAILCost:
     def __init__(self, expert_data: torch.Tensor, agent_rb=None, feature_dim: int = 1, hidden_dims=(1024, 512),
                  input_type: str = "ss", scaling_coef: float = 0.5, reg_coef: float = 0.05, lambda_b: float = 0.5,
                  seed=100, grad_lambda=10.0, disc_loss_type="least_squares", disc_opt="sgd", disc_opt_args=None,
-                 ctx: AmxContext | None = None, device="cuda", gemm: str = "bf16x6"):
-        if disc_loss_type != "least_squares":
-            raise NotImplementedError("only the least-squares (AMP) discriminator reward is on the hot path")
+                 ctx: AmxContext | None = None, device="cuda", gemm: str = "bf16x6", motion=None):
+        """`motion` (a ReferenceMotion) is needed for input_type "amp" (discriminator on AMP
+        observations); any disc_loss_type other than "least_squares" selects the
+        log-likelihood cost, as in the reference's get_costs (gail_cost.py:246-251)."""
+        _check_input_type(input_type, motion)
         if feature_dim != 1:
             raise ValueError("Discriminator output must be 1-D")
         torch.manual_seed(seed)          # gail_cost.py:62-63
@@ -160,8 +212,10 @@ class GAILCost:
         self.expert_data = expert_data
         self.input_dim = expert_data.size(1)
         self.input_type = input_type
+        self.motion = motion
         self.lambda_b = float(lambda_b)
         self.disc_loss_type = disc_loss_type
+        self.loss_code = N.AMX_DISC_LEAST_SQUARES if disc_loss_type == "least_squares" else N.AMX_DISC_LOG_LIKELIHOOD
         sizes = [self.input_dim] + list(hidden_dims) + [1]
         layers = [nn.Linear(sizes[i], sizes[i + 1]) for i in range(len(sizes) - 1)]   # Discriminator :28-37
         for lin in layers:                                                             # disc_weight_init :11-16
@@ -171,7 +225,7 @@ class GAILCost:
                 nn.init.xavier_uniform_(lin.weight.data)
         self.weights = [(l.weight.data.clone(), l.bias.data.clone()) for l in layers]
         if ctx is None:
-            S = self.input_dim // 2
+            S = self.input_dim // 2 if input_type == "ss" else self.input_dim
             ctx = AmxContext(S, 1, n_models=1, hidden=128, n_hidden=0, feat_dim=128, device=device)
         self.ctx = ctx
         if gemm not in ("bf16x6", "f32"):
@@ -224,14 +278,16 @@ class GAILCost:
         return h
 
     def rewards_from_input(self, x_pad: torch.Tensor, rows: int, n: int, disc: torch.Tensor | None,
-                           out: torch.Tensor | None = None, logits: torch.Tensor | None = None) -> torch.Tensor:
+                           out: torch.Tensor | None = None, logits: torch.Tensor | None = None,
+                           loss_code: int | None = None) -> torch.Tensor:
         """Fused discriminator + reward on already padded input rows [rows, Kin]."""
         c = self.ctx
         h = self._hidden(x_pad, rows)
         out = torch.empty(n, dtype=torch.float32, device=c.device) if out is None else out
-        N.check(c.lib.amx_amp_reward(c.h, h.data_ptr(), h.stride(0), self.h_last, self.w3.data_ptr(), self.b3,
-                                     None if disc is None else disc.data_ptr(), self.lambda_b, out.data_ptr(),
-                                     None if logits is None else logits.data_ptr(), n, c.stream), "amx_amp_reward")
+        N.check(c.lib.amx_disc_reward(c.h, self.loss_code if loss_code is None else loss_code, h.data_ptr(),
+                                      h.stride(0), self.h_last, self.w3.data_ptr(), self.b3,
+                                      None if disc is None else disc.data_ptr(), self.lambda_b, out.data_ptr(),
+                                      None if logits is None else logits.data_ptr(), n, c.stream), "amx_disc_reward")
         return out
 
     def _pad(self, x: torch.Tensor):
@@ -250,20 +306,24 @@ class GAILCost:
     def get_ls_costs(self, ss: torch.Tensor) -> torch.Tensor:
         """gail_cost.py:231-236: -max(0, 1 - 0.25 (1 - D)^2)  [n, 1]."""
         xp, rows, n = self._pad(ss)
-        return (-self.rewards_from_input(xp, rows, n, None)).view(-1, 1)
+        return (-self.rewards_from_input(xp, rows, n, None, loss_code=N.AMX_DISC_LEAST_SQUARES)).view(-1, 1)
+
+    def get_ll_costs(self, ss: torch.Tensor) -> torch.Tensor:
+        """gail_cost.py:238-244: logsigmoid(D)  [n, 1]."""
+        xp, rows, n = self._pad(ss)
+        return (-self.rewards_from_input(xp, rows, n, None, loss_code=N.AMX_DISC_LOG_LIKELIHOOD)).view(-1, 1)
 
     def get_costs(self, ss: torch.Tensor) -> torch.Tensor:
-        return self.get_ls_costs(ss)
+        """gail_cost.py:246-251."""
+        return self.get_ls_costs(ss) if self.loss_code == N.AMX_DISC_LEAST_SQUARES else self.get_ll_costs(ss)
 
     def get_bonus_costs(self, states, actions, ensemble, next_states=None):
-        """gail_cost.py:254-279 ('ss'): cost = (1-lambda) * ls_cost - lambda * disagreement."""
-        if self.input_type != "ss":
-            raise NotImplementedError("only the 'ss' input of the humanoid path is implemented")
-        x = torch.cat([states.float(), next_states.float()], dim=1)
+        """gail_cost.py:254-279: cost = (1-lambda) * input cost - lambda * disagreement."""
+        x = cost_input(self.input_type, states, actions, next_states, self.motion)
         xp, rows, n = self._pad(x)
         disc = ensemble.get_action_discrepancy(states, actions)
         reward = self.rewards_from_input(xp, rows, n, disc)
-        input_cost = self.get_ls_costs(x)
+        input_cost = self.get_costs(x)
         lam = np.float32(self.lambda_b)
         ipm = np.float32(1 - self.lambda_b) * input_cost
         bonus = lam * disc.view(-1, 1)

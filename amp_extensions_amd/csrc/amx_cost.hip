@@ -75,6 +75,9 @@ __device__ inline float clampf_ref(float v, float lo, float hi) {
   return v > hi ? hi : v;
 }
 
+// CLAMP: cost_range given (clamped cost, bonus = min(disc/thr, 1) * c_min);
+// !CLAMP: cost_range None (raw cost, bonus = raw disagreement, linear_cost.py:103, 138-139).
+template <bool CLAMP>
 __global__ __launch_bounds__(256) void k_mmd_reward(const float* __restrict__ phi, int ldphi,
                                                     const float* __restrict__ w, int F,
                                                     const float* __restrict__ disc, float thr, float one_m_lambda,
@@ -86,10 +89,16 @@ __global__ __launch_bounds__(256) void k_mmd_reward(const float* __restrict__ ph
   if (r >= n) return;
   const double dot = row_dot(phi + (long long)r * ldphi, w, F, lane);
   if (lane != 0) return;
-  const float v = clampf_ref((float)dot, c_min, c_max);       // linear_cost.py:102
-  float dh = disc[r] / thr;                                    // :132
-  if (dh > 1.0f) dh = 1.0f;                                    // :134
-  const float bonus = dh * c_min;                              // :136
+  float v, bonus;
+  if constexpr (CLAMP) {
+    v = clampf_ref((float)dot, c_min, c_max);                  // linear_cost.py:102
+    float dh = disc[r] / thr;                                  // :132
+    if (dh > 1.0f) dh = 1.0f;                                  // :134
+    bonus = dh * c_min;                                        // :136
+  } else {
+    v = (float)dot;                                            // :103
+    bonus = disc[r];                                           // :139
+  }
   const float ipm = one_m_lambda * v;                          // :141  (1-lambda)*rff_cost
   const float wb = lambda_b * bonus;                           // :144
   const float cost = ipm - wb;                                 // :147
@@ -130,6 +139,9 @@ __global__ __launch_bounds__(256) void k_sum_small(const double* __restrict__ pa
   if (threadIdx.x == 0) out[0] = red[0];
 }
 
+// LOSS 0: least squares (get_ls_costs, gail_cost.py:231-236); LOSS 1: log-likelihood
+// (get_ll_costs, :238-244: cost = logsigmoid(D)).
+template <int LOSS>
 __global__ __launch_bounds__(256) void k_amp_reward(const float* __restrict__ h, int ldh, int Hd,
                                                     const float* __restrict__ w3, float b3,
                                                     const float* __restrict__ disc, float one_m_lambda,
@@ -144,17 +156,23 @@ __global__ __launch_bounds__(256) void k_amp_reward(const float* __restrict__ h,
   s = wave_sum(s);
   if (lane != 0) return;
   const float D = (float)s + b3;                     // Discriminator last nn.Linear
-  const float om = 1.0f - D;                         // gail_cost.py:234  1.0 - disc_outs
-  const float sq = om * om;                          //                   (.)**2
-  const float q = 0.25f * sq;                        //                   0.25 * (.)
-  float rew = 1.0f - q;                              //                   1.0 - (.)
-  if (rew < 0.0f) rew = 0.0f;                        // :235
+  float rew;
+  if constexpr (LOSS == 0) {
+    const float om = 1.0f - D;                       // gail_cost.py:234  1.0 - disc_outs
+    const float sq = om * om;                        //                   (.)**2
+    const float q = 0.25f * sq;                      //                   0.25 * (.)
+    rew = 1.0f - q;                                  //                   1.0 - (.)
+    if (rew < 0.0f) rew = 0.0f;                      // :235
+  } else {
+    // F.logsigmoid = min(D, 0) - log1p(exp(-|D|)); reward = -cost
+    rew = -(fminf(D, 0.0f) - log1pf(expf(-fabsf(D))));
+  }
   if (logits) logits[r] = D;
   if (disc == nullptr) {                             // get_costs path: reward = -cost = r
     reward[r] = rew;
     return;
   }
-  const float input_cost = -rew;                     // :236
+  const float input_cost = -rew;                     // :236 (ll: logsigmoid(D), :243)
   const float ipm = one_m_lambda * input_cost;       // :269
   const float bonus = lambda_b * disc[r];            // :273 (raw disagreement)
   const float cost = ipm - bonus;                    // :275
@@ -181,9 +199,9 @@ extern "C" int amx_mmd_fit(amx_ctx* ctx, const double* phi_sum, double count, co
   return AMX_OK;
 }
 
-extern "C" int amx_mmd_reward(amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
-                              float thr, double lambda_b, float c_min, float c_max, float* reward, float* ipm,
-                              float* wbonus, int n, void* stream) {
+static int mmd_reward(bool clamp, amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
+                      float thr, double lambda_b, float c_min, float c_max, float* reward, float* ipm, float* wbonus,
+                      int n, void* stream) {
   AMX_CHECK_ARG(ctx && phi && w && disc && reward, "amx_mmd_reward: null pointer");
   AMX_CHECK_ARG(F > 0 && F % 256 == 0 && ldphi >= F && ldphi % 4 == 0, "amx_mmd_reward: F=%d ldphi=%d", F, ldphi);
   AMX_CHECK_ARG(amx::aligned16(phi) && amx::aligned16(w), "amx_mmd_reward: phi/w must be 16-byte aligned");
@@ -192,10 +210,25 @@ extern "C" int amx_mmd_reward(amx_ctx* ctx, const float* phi, int ldphi, const f
   // lambda is a Python double in the reference: (1 - lambda) is formed in double, then
   // torch rounds each scalar to float32 for the fp32 kernel (linear_cost.py:141,144).
   const float one_m_lambda = (float)(1.0 - lambda_b);
-  hipLaunchKernelGGL(k_mmd_reward, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, phi, ldphi, w, F, disc,
-                     thr, one_m_lambda, (float)lambda_b, c_min, c_max, reward, ipm, wbonus, n);
+  if (clamp)
+    hipLaunchKernelGGL(k_mmd_reward<true>, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, phi, ldphi, w, F,
+                       disc, thr, one_m_lambda, (float)lambda_b, c_min, c_max, reward, ipm, wbonus, n);
+  else
+    hipLaunchKernelGGL(k_mmd_reward<false>, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, phi, ldphi, w, F,
+                       disc, thr, one_m_lambda, (float)lambda_b, c_min, c_max, reward, ipm, wbonus, n);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
+}
+
+extern "C" int amx_mmd_reward(amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
+                              float thr, double lambda_b, float c_min, float c_max, float* reward, float* ipm,
+                              float* wbonus, int n, void* stream) {
+  return mmd_reward(true, ctx, phi, ldphi, w, F, disc, thr, lambda_b, c_min, c_max, reward, ipm, wbonus, n, stream);
+}
+
+extern "C" int amx_mmd_reward_raw(amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
+                                  double lambda_b, float* reward, float* ipm, float* wbonus, int n, void* stream) {
+  return mmd_reward(false, ctx, phi, ldphi, w, F, disc, 1.0f, lambda_b, 0.f, 0.f, reward, ipm, wbonus, n, stream);
 }
 
 extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
@@ -213,15 +246,61 @@ extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi,
   return AMX_OK;
 }
 
+extern "C" int amx_disc_reward(amx_ctx* ctx, int loss_type, const float* h, int ldh, int Hd, const float* w3,
+                               float b3, const float* disc, double lambda_b, float* reward, float* logits, int n,
+                               void* stream) {
+  AMX_CHECK_ARG(ctx && h && w3 && reward, "amx_disc_reward: null pointer");
+  AMX_CHECK_ARG(Hd > 0 && ldh >= Hd && n >= 0, "amx_disc_reward: Hd=%d ldh=%d n=%d", Hd, ldh, n);
+  AMX_CHECK_ARG(loss_type == AMX_DISC_LEAST_SQUARES || loss_type == AMX_DISC_LOG_LIKELIHOOD,
+                "amx_disc_reward: loss_type=%d", loss_type);
+  if (n == 0) return AMX_OK;
+  const float one_m_lambda = (float)(1.0 - lambda_b);
+  if (loss_type == AMX_DISC_LEAST_SQUARES)
+    hipLaunchKernelGGL(k_amp_reward<0>, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, Hd, w3, b3,
+                       disc, one_m_lambda, (float)lambda_b, reward, logits, n);
+  else
+    hipLaunchKernelGGL(k_amp_reward<1>, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, Hd, w3, b3,
+                       disc, one_m_lambda, (float)lambda_b, reward, logits, n);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
 extern "C" int amx_amp_reward(amx_ctx* ctx, const float* h, int ldh, int Hd, const float* w3, float b3,
                               const float* disc, double lambda_b, float* reward, float* logits, int n,
                               void* stream) {
-  AMX_CHECK_ARG(ctx && h && w3 && reward, "amx_amp_reward: null pointer");
-  AMX_CHECK_ARG(Hd > 0 && ldh >= Hd && n >= 0, "amx_amp_reward: Hd=%d ldh=%d n=%d", Hd, ldh, n);
-  if (n == 0) return AMX_OK;
-  const float one_m_lambda = (float)(1.0 - lambda_b);
-  hipLaunchKernelGGL(k_amp_reward, dim3((n + 3) / 4), dim3(256), 0, (hipStream_t)stream, h, ldh, Hd, w3, b3, disc,
-                     one_m_lambda, (float)lambda_b, reward, logits, n);
+  return amx_disc_reward(ctx, AMX_DISC_LEAST_SQUARES, h, ldh, Hd, w3, b3, disc, lambda_b, reward, logits, n, stream);
+}
+
+// out[b] = float32 [x0[b, :w0], x1[b, :w1], x2[b, :w2], 0 ...] up to ldc: the cost-input row
+// of every input type (linear_cost.py:115-127, gail_cost.py:258-268).  One wave per row.
+__global__ __launch_bounds__(256) void k_cost_rows(const double* __restrict__ x0, long long ld0, int w0,
+                                                   const double* __restrict__ x1, long long ld1, int w1,
+                                                   const double* __restrict__ x2, long long ld2, int w2, int B,
+                                                   float* __restrict__ out, int ldc) {
+  const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (r >= B) return;
+  float* o = out + (long long)r * ldc;
+  for (int j = lane; j < ldc; j += 64) {
+    float v = 0.f;
+    if (j < w0) v = (float)x0[(long long)r * ld0 + j];
+    else if (j < w0 + w1) v = (float)x1[(long long)r * ld1 + (j - w0)];
+    else if (j < w0 + w1 + w2) v = (float)x2[(long long)r * ld2 + (j - w0 - w1)];
+    o[j] = v;
+  }
+}
+
+extern "C" int amx_cost_rows(amx_ctx* ctx, const double* x0, long long ld0, int w0, const double* x1, long long ld1,
+                             int w1, const double* x2, long long ld2, int w2, int B, float* out, int ldc,
+                             void* stream) {
+  AMX_CHECK_ARG(ctx && out && B >= 0, "amx_cost_rows: bad arguments");
+  AMX_CHECK_ARG(w0 >= 0 && w1 >= 0 && w2 >= 0 && w0 + w1 + w2 <= ldc, "amx_cost_rows: widths %d+%d+%d > ldc=%d", w0,
+                w1, w2, ldc);
+  AMX_CHECK_ARG((w0 == 0 || (x0 && ld0 >= w0)) && (w1 == 0 || (x1 && ld1 >= w1)) && (w2 == 0 || (x2 && ld2 >= w2)),
+                "amx_cost_rows: missing segment or short row stride");
+  if (B == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_cost_rows, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, x0, ld0, w0, x1, ld1, w1, x2,
+                     ld2, w2, B, out, ldc);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

@@ -11,45 +11,66 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .costs import GAILCost, RBFLinearCost
+from .costs import GAILCost, RBFLinearCost, cost_input
 from .dist import feature_mean
 
 
 def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", allreduce=None) -> dict:
+    """`cost_input_type` builds the fit_cost input ('ss' or 'sa', batch_reinforce.py:107-110);
+    the per-sample rewards use reward_func's own input_type (get_bonus_costs).  With
+    `ensemble` None the GAIL path replaces the rewards with -get_costs([s, s'])
+    (batch_reinforce.py:146-158)."""
     infos = {"int": [], "ext": [], "reward": [], "ep_len": []}
-    if cost_input_type != "ss":
-        raise NotImplementedError("the humanoid MILO path uses the 'ss' cost input")
+    if cost_input_type not in ("ss", "sa"):
+        # the reference leaves cost_input unbound for any other value
+        raise NotImplementedError(f"cost_input_type {cost_input_type!r}: batch_reinforce builds only 'ss' / 'sa'")
     dev = reward_func.ctx.device
     lens = [len(p["observations"]) for p in paths]
     obs = torch.from_numpy(np.concatenate([p["observations"] for p in paths])).float().to(dev)
     nxt = torch.from_numpy(np.concatenate([p["next_observations"] for p in paths])).float().to(dev)
     act = torch.from_numpy(np.concatenate([p["actions"] for p in paths])).float().to(dev)
+    bonus_v = ipm_v = None
     if isinstance(reward_func, RBFLinearCost):
-        x = torch.cat([obs, nxt], dim=1)
-        phi, tot = reward_func.map.embed(x)
-        mean = feature_mean(tot, float(x.shape[0]), allreduce if allreduce is not None else (lambda t: t))
+        if ensemble is None:
+            raise ValueError("the MMD relabel needs the ensemble (batch_reinforce.py:147 asserts a GAIL cost)")
+        x_fit = cost_input(cost_input_type, obs, act, nxt)
+        phi_fit, tot = reward_func.map.embed(x_fit)
+        mean = feature_mean(tot, float(x_fit.shape[0]), allreduce if allreduce is not None else (lambda t: t))
         infos["mb_mmd"] = reward_func.fit_w(mean.contiguous(), 1.0)           # batch_reinforce.py:113
+        if reward_func.input_type == cost_input_type:
+            phi = phi_fit
+        else:
+            phi = reward_func.get_rep(cost_input(reward_func.input_type, obs, act, nxt, reward_func.motion))
         disc = ensemble.get_action_discrepancy(obs, act)
         reward, ipm, wb = reward_func._values(phi, disc, ensemble.threshold)
         bonus_v, ipm_v = wb.cpu().numpy(), ipm.cpu().numpy()
     elif isinstance(reward_func, GAILCost):
-        cost, ci = reward_func.get_bonus_costs(obs, act, ensemble, next_states=nxt)
-        reward = -cost.view(-1)
-        bonus_v, ipm_v = ci["bonus"].view(-1).cpu().numpy(), ci["ipm"].view(-1).cpu().numpy()
+        # the reference scores [s, s'] here (:152-165); an AMP-feature discriminator scores AMP(s, s')
+        x_ss = (cost_input("amp", obs, act, nxt, reward_func.motion) if reward_func.input_type == "amp"
+                else torch.cat([obs, nxt], dim=-1))
+        if ensemble is not None:
+            cost, ci = reward_func.get_bonus_costs(obs, act, ensemble, next_states=nxt)
+            reward = -cost.view(-1)
+            bonus_v, ipm_v = ci["bonus"].view(-1).cpu().numpy(), ci["ipm"].view(-1).cpu().numpy()
+        else:
+            reward = -reward_func.get_costs(x_ss).view(-1)                             # :152-158
     else:
         raise TypeError("reward_func must be an RBFLinearCost or GAILCost")
     rew = reward.cpu().numpy()
     o = 0
     for p, T in zip(paths, lens):
-        isum = -np.sum(bonus_v[o:o + T])    # batch_reinforce.py:135
-        esum = -np.sum(ipm_v[o:o + T])      # :136
-        infos["int"].append(isum)
-        infos["ext"].append(esum)
-        infos["reward"].append(esum + isum)
-        infos["ep_len"].append(T)
+        if bonus_v is not None:
+            isum = -np.sum(bonus_v[o:o + T])    # batch_reinforce.py:135
+            esum = -np.sum(ipm_v[o:o + T])      # :136
+            infos["int"].append(isum)
+            infos["ext"].append(esum)
+            infos["reward"].append(esum + isum)
+            infos["ep_len"].append(T)
         p["rewards"] = rew[o:o + T].copy()  # :144 (reward = -cost)
         o += T
-    if isinstance(reward_func, RBFLinearCost):
+    if isinstance(reward_func, GAILCost):
+        infos["on_policy_gail_cost"] = reward_func.get_costs(x_ss)                     # :160-165
+    else:
         infos["bonus_mmd"] = np.concatenate([-1.0 * p["rewards"] for p in paths]).mean() - \
             float(reward_func.get_expert_cost())                                 # :169
     return infos

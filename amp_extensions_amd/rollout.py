@@ -5,6 +5,7 @@ One synchronous step (all lanes) is, in launch order on one HIP stream:
   2. assemble    amx_assemble_input    x0 = [(s-mu)/sd, (a-mu)/sd]               (dynamics.py:225-230)
   3. ensemble    L x amx_gemm_bias_act + amx_gemm_out_unnorm (all M members)     (dynamics.py:422-433)
   4. step        amx_step              s' = s + Δ_k (fp64), done, disagreement, [s, s'] f32 (sim_env.py:140-268)
+                 (amx_cost_rows for the 'sa' / 'sas' / 's' / AMP cost inputs)
   5. auto-reset  amx_reset_lanes       done lanes <- reset-table row, model k+1  (sim_env.py:270-285)
 The step kernel records the float32 [s, s'] cost-input row of every transition; the
 reward pass runs once over all recorded transitions (`score`, at the end of `rollout` or
@@ -29,7 +30,7 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .costs import GAILCost, RBFLinearCost
+from .costs import GAILCost, RBFLinearCost, input_width
 from .dist import feature_mean
 from .engine import DeviceEnsemble, round_up
 from .humanoid import TerminationConfig
@@ -79,8 +80,27 @@ class RolloutEngine:
         self.reset_count = z(B, dt=torch.int32)
         self.reset_rows = z(K, B, dt=torch.int32)
         self.reset_times = z(K, B, dt=torch.float64) if self.motion is not None else None
-        # [s, s'] cost-input rows of every recorded transition, scored in one batched pass
-        self.cost_in = z(K, Bp, c.k_rff_pad)
+        # cost-input rows of every recorded transition, scored in one batched pass: [s, s']
+        # ('ss', written by the step kernel) or [s, a], [s, a, s'], [s], AMP(s, s')
+        # (amx_cost_rows after the step)
+        self.cost_type = getattr(cost, "input_type", "ss") if cost is not None else "ss"
+        if isinstance(cost, RBFLinearCost):
+            self.kc = cost.map.Kp
+        elif isinstance(cost, GAILCost):
+            self.kc = cost.Kin
+        else:
+            self.kc = c.k_rff_pad
+        if cost is not None:
+            width = input_width(self.cost_type, S, A, getattr(cost, "motion", None))
+            if cost.input_dim != width:
+                raise ValueError(f"cost input width {cost.input_dim} does not match input_type "
+                                 f"{self.cost_type!r} (S={S}, A={A}: {width})")
+        self.cost_in = z(K, Bp, self.kc)
+        self.amp_rows = None
+        if self.cost_type == "amp":
+            if cost.motion.ctx is not c:
+                raise ValueError("the cost's ReferenceMotion must live on the engine's context")
+            self.amp_rows = z(B, self.kc, dt=torch.float64)
         # rows t*Bp + b with b >= B are padding: excluded from the feature sums
         self.row_mask = None
         if B != Bp:
@@ -91,11 +111,6 @@ class RolloutEngine:
             self.phi = z(K, Bp, cost.feature_dim)
             self.partials = z(K, Bp // 128, cost.feature_dim, dt=torch.float64)
             self.phi_sum = z(cost.feature_dim, dt=torch.float64)
-            if cost.map.Kp != c.k_rff_pad:
-                raise ValueError("cost input width does not match the state size")
-        elif isinstance(cost, GAILCost):
-            if cost.Kin != c.k_rff_pad:
-                raise ValueError("discriminator input width does not match the state size")
         self.t = 0              # steps taken in the current rollout
         self.step_counter = 0   # global step counter (policy RNG stream)
         self.mb_mmd = None
@@ -165,8 +180,10 @@ class RolloutEngine:
         N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
                                self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
-                               self.cost_in[t].data_ptr(), c.k_rff_pad, self.nonfinite[t].data_ptr(), B, s),
-                "amx_step")
+                               self.cost_in[t].data_ptr() if self.cost_type == "ss" else None, self.kc,
+                               self.nonfinite[t].data_ptr(), B, s), "amx_step")
+        if self.cost is not None and self.cost_type != "ss":
+            self._record_cost_input(t)
         if self.auto_reset and self.motion is not None:
             self._reset_motion(self.done[t], reset_rows, ob_next, self.obs[t + 1], self.reset_times[t])
         elif self.auto_reset:
@@ -180,6 +197,27 @@ class RolloutEngine:
         self.t += 1
         self.step_counter += 1
         return t
+
+    def _record_cost_input(self, t: int) -> None:
+        """Cost-input rows of step t for the non-'ss' input types (linear_cost.py:115-127)."""
+        c, B, S, A = self.ctx, self.B, self.ctx.S, self.ctx.A
+        ob, nx, act = self.obs[t], self.next_obs[t], self.acts[t]
+        typ = self.cost_type
+        if typ == "amp":
+            m = self.cost.motion
+            D = m.amp_obs_size
+            m.amp_obs_from_states(ob, nx, out=self.amp_rows[:, :D])
+            segs = ((self.amp_rows, self.kc, D), (None, 0, 0), (None, 0, 0))
+        elif typ == "sa":
+            segs = ((ob, S, S), (act, A, A), (None, 0, 0))
+        elif typ == "sas":
+            segs = ((ob, S, S), (act, A, A), (nx, S, S))
+        else:  # "s"
+            segs = ((ob, S, S), (None, 0, 0), (None, 0, 0))
+        args = []
+        for x, ld, w in segs:
+            args += [None if x is None else x.data_ptr(), ld, w]
+        N.check(c.lib.amx_cost_rows(c.h, *args, B, self.cost_in[t].data_ptr(), self.kc, c.stream), "amx_cost_rows")
 
     def rollout(self, K: int | None = None) -> int:
         """K synchronous steps (default: the buffer depth), then the batched reward pass.
@@ -199,7 +237,7 @@ class RolloutEngine:
             self._scored = t1
             return
         rows = (t1 - t0) * Bp
-        x = self.cost_in[t0:t1].view(rows, c.k_rff_pad)
+        x = self.cost_in[t0:t1].view(rows, self.kc)
         if isinstance(cost, RBFLinearCost):
             mask = None if self.row_mask is None else self.row_mask[t0 * Bp:t1 * Bp]
             cost.map.features(x, rows, rows, self.phi[t0:t1].view(rows, -1),
@@ -234,10 +272,8 @@ class RolloutEngine:
         mean = feature_mean(phi_sum, float(T * B), allreduce if allreduce is not None else (lambda t: t))
         self.mb_mmd = cost.fit_w_device(mean.contiguous(), 1.0)  # device tensor: no host sync
         n = T * self.Bp
-        N.check(c.lib.amx_mmd_reward(c.h, self.phi.data_ptr(), cost.feature_dim, cost.w.data_ptr(),
-                                     cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),
-                                     cost.lambda_b, cost.c_min, cost.c_max, self.rewards.data_ptr(),
-                                     self.ipm.data_ptr(), self.wbonus.data_ptr(), n, c.stream), "amx_mmd_reward")
+        cost.reward_launch(self.phi.data_ptr(), cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),
+                           self.rewards.data_ptr(), self.ipm.data_ptr(), self.wbonus.data_ptr(), n)
         return {"mb_mmd": self.mb_mmd}
 
     def advantages(self, baseline, gamma: float = 0.995, gae_lambda=0.97, whiten: bool = False,

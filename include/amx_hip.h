@@ -51,6 +51,7 @@ enum {
 enum { AMX_SHAPE_SPHERE = 0, AMX_SHAPE_CAPSULE = 1, AMX_SHAPE_BOX = 2 };
 enum { AMX_ACT_NONE = 0, AMX_ACT_RELU = 1 };
 enum { AMX_IN_F64 = 0, AMX_IN_F32 = 1 };
+enum { AMX_DISC_LEAST_SQUARES = 0, AMX_DISC_LOG_LIKELIHOOD = 1 };
 
 typedef struct amx_ctx amx_ctx;
 
@@ -291,6 +292,11 @@ int amx_mmd_reward(amx_ctx* ctx, const float* phi, int ldphi, const float* w, in
                    float thr, double lambda_b, float c_min, float c_max, float* reward, float* ipm,
                    float* wbonus, int n, void* stream);
 
+/* Same with cost_range=None (linear_cost.py:103, 138-139): v = phi[n].w unclamped,
+ * bonus = disc[n] (raw disagreement); ipm/wb/reward as above. */
+int amx_mmd_reward_raw(amx_ctx* ctx, const float* phi, int ldphi, const float* w, int F, const float* disc,
+                       double lambda_b, float* reward, float* ipm, float* wbonus, int n, void* stream);
+
 /* get_expert_cost (milo/milo/linear_cost.py:105-109): partial fp64 sums over row
  * blocks of clamp(phi_E[r].w, c_min, c_max); out[0] = sum (fp64), caller scales by
  * (1-lambda)/N_e.  Uses the resident expert features. */
@@ -307,6 +313,19 @@ int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const floa
 int amx_amp_reward(amx_ctx* ctx, const float* h, int ldh, int Hd, const float* w3, float b3,
                    const float* disc, double lambda_b, float* reward, float* logits, int n,
                    void* stream);
+
+/* amx_amp_reward for either discriminator loss type (GAILCost.get_costs,
+ * gail_cost.py:246-251): AMX_DISC_LEAST_SQUARES as above, AMX_DISC_LOG_LIKELIHOOD
+ * with input cost logsigmoid(D) (get_ll_costs, :238-244), r = -logsigmoid(D). */
+int amx_disc_reward(amx_ctx* ctx, int loss_type, const float* h, int ldh, int Hd, const float* w3, float b3,
+                    const float* disc, double lambda_b, float* reward, float* logits, int n, void* stream);
+
+/* Cost-input rows of the non-'ss' input types ('sa', 'sas', 's', or AMP features):
+ * out[b] = float32 [x0[b,:w0], x1[b,:w1], x2[b,:w2], 0...] up to ldc, fp64 sources
+ * (linear_cost.py:115-127, gail_cost.py:258-268, batch_reinforce.py:107-110).
+ * A segment with width 0 is absent (its pointer may be NULL). */
+int amx_cost_rows(amx_ctx* ctx, const double* x0, long long ld0, int w0, const double* x1, long long ld1, int w1,
+                  const double* x2, long long ld2, int w2, int B, float* out, int ldc, void* stream);
 
 /* ---- returns / value baseline / GAE (the sampler's consumer) ------------------ */
 

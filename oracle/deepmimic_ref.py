@@ -457,3 +457,61 @@ def reset_pose_vel(joints, bodies, M, time, ground_pad=0.001):
     lift = -min(0.0, min(lows))
     pose[1] += lift
     return pose, vel
+
+
+# ---- AMP features from two recorded SimEnv states ----------------------------------------
+# The learned-dynamics SimEnv records CtController states (no joint quaternions), so the
+# AMP observation of a transition (s, s') is built from what the state holds: rotations from
+# the tangent-normal pairs (R = [tan, nrm, tan x nrm]), joint velocity parameters from the
+# body angular velocities, end-effector offsets from the body positions.  On a state that
+# reset_state recorded these equal the quantities amp_obs reads from (pose, vel); this is the
+# restatement of amx_motion.hip's kin_from_state / amp_pose_part / amp_vel_part used to check
+# the device on arbitrary (dynamics-predicted) states.
+def _tn_mat(nt):
+    nrm, tan = np.asarray(nt[0:3], float), np.asarray(nt[3:6], float)
+    return np.column_stack([tan, nrm, np.cross(tan, nrm)])
+
+
+def state_kin(joints, ee, s):
+    n = len(joints)
+    base = 1 + 9 * n
+    Rw0 = _tn_mat(s[4:10])
+    Rh = rotmat_axis((0.0, 1.0, 0.0), -math.atan2(-Rw0[2, 0], Rw0[0, 0]))
+    R = [Rh @ Rw0] + [_tn_mat(s[9 * i + 4:9 * i + 10]) for i in range(1, n)]
+    w0 = np.asarray(s[base + 3:base + 6], float)
+    w = [Rh @ w0] + [np.asarray(s[base + 6 * i + 3:base + 6 * i + 6], float) for i in range(1, n)]
+    v0 = np.asarray(s[base:base + 3], float) - np.cross(w0, Rh.T @ np.asarray(s[1:4], float))
+    jv = []
+    for i in range(1, n):
+        j = joints[i]
+        if j["type"] in (0, 4):
+            wl = R[i].T @ (w[i] - w[j["parent"]])
+            jv += [wl[0], wl[1], wl[2], 0.0] if j["type"] == 4 else [wl[2]]
+    return dict(root_y=s[0], Rw0=Rw0, Rh=Rh, R=R, v0=v0, w0=w0, jv=np.array(jv),
+                ee=[np.asarray(s[9 * e + 1:9 * e + 4], float) for e in ee])
+
+
+def state_amp_obs(joints, ee, s_prev, s_cur, local_root=False):
+    kp, kc = state_kin(joints, ee, s_prev), state_kin(joints, ee, s_cur)
+    Rc = kc["Rh"]
+
+    def pose_part(k):
+        R0 = Rc @ k["Rw0"] if local_root else k["Rw0"]
+        out = [k["root_y"]] + list(R0[:, 1]) + list(R0[:, 0])
+        for i in range(1, len(joints)):
+            j = joints[i]
+            if j["type"] in (0, 4):
+                L = k["R"][j["parent"]].T @ k["R"][i]
+                out += list(L[:, 1]) + list(L[:, 0]) if j["type"] == 4 else [math.atan2(L[1, 0], L[0, 0])]
+        Rx = Rc @ k["Rh"].T
+        for e in k["ee"]:
+            out += list(Rx @ e)
+        return np.array(out)
+
+    def vel_part(k):
+        v, w = k["v0"], k["w0"]
+        if local_root:
+            v, w = Rc @ v, Rc @ w
+        return np.concatenate([v, w, k["jv"]])
+
+    return np.concatenate([pose_part(kc), pose_part(kp), vel_part(kc), vel_part(kp)])

@@ -245,6 +245,22 @@ def step_update_terminate(ob: np.ndarray, pred_k: np.ndarray, num_steps: np.ndar
 # --------------------------------------------------------------------------------------
 
 
+def cost_input(input_type: str, states, actions, next_states):
+    """The cost-input row of a transition by input type: linear_cost.py:115-127,
+    gail_cost.py:258-268 ('sa', 'ss', 'sas', 's'); batch_reinforce.py:107-110 builds the
+    fit_cost input the same way."""
+    if input_type == "sa":
+        return torch.cat([states, actions], dim=1)
+    if input_type == "ss":
+        assert next_states is not None
+        return torch.cat([states, next_states], dim=1)
+    if input_type == "sas":
+        return torch.cat([states, actions, next_states], dim=1)
+    if input_type == "s":
+        return states
+    raise NotImplementedError("Input type not implemented")
+
+
 class RBFLinearCostRef:
     """Restatement of RBFLinearCost (linear_cost.py:23-152), CPU torch."""
 
@@ -302,12 +318,15 @@ class RBFLinearCostRef:
 
     def get_bonus_costs(self, states, actions, disc_fn, thr, next_states=None):  # :111-152
         """`disc_fn(states, actions)` is the ensemble's get_action_discrepancy."""
-        rff_input = torch.cat([states, next_states], dim=1)
+        rff_input = cost_input(self.input_type, states, actions, next_states)   # :115-127
         rff_cost = self.get_costs(rff_input)
-        discrepancy = disc_fn(states, actions) / thr
-        discrepancy = discrepancy.view(-1, 1)
-        discrepancy[discrepancy > 1.0] = 1.0
-        bonus = discrepancy * self.c_min
+        if self.cost_range is not None:                                          # :131-137
+            discrepancy = disc_fn(states, actions) / thr
+            discrepancy = discrepancy.view(-1, 1)
+            discrepancy[discrepancy > 1.0] = 1.0
+            bonus = discrepancy * self.c_min
+        else:                                                                    # :138-139
+            bonus = disc_fn(states, actions).view(-1, 1)
         ipm = (1 - self.lambda_b) * rff_cost
         weighted_bonus = self.lambda_b * bonus.cpu()
         cost = ipm - weighted_bonus
@@ -355,11 +374,19 @@ def gail_ls_costs(weights, ss):
         return -rewards
 
 
-def gail_bonus_costs(weights, states, actions, next_states, disc_fn, lambda_b):
-    """get_bonus_costs (gail_cost.py:254-279), input_type 'ss'."""
+def gail_ll_costs(weights, ss):
+    """get_ll_costs (gail_cost.py:238-243): logsigmoid of the discriminator output."""
     with torch.no_grad():
-        inp = torch.cat([states, next_states], dim=1)
-        input_cost = gail_ls_costs(weights, inp)
+        return F.logsigmoid(disc_forward(weights, ss))
+
+
+def gail_bonus_costs(weights, states, actions, next_states, disc_fn, lambda_b, input_type="ss",
+                     disc_loss_type="least_squares"):
+    """get_bonus_costs (gail_cost.py:254-279); get_costs picks the loss type (:246-251)."""
+    with torch.no_grad():
+        inp = cost_input(input_type, states, actions, next_states)
+        costs = gail_ls_costs if disc_loss_type == "least_squares" else gail_ll_costs
+        input_cost = costs(weights, inp)
         ipm = (1 - lambda_b) * input_cost
         discrepancy = disc_fn(states, actions)
         bonus = lambda_b * discrepancy.view(-1, 1)

@@ -63,3 +63,18 @@ def test_reset_state_at_frame_time_uses_the_frame(g12):
         p = M.pose(M.times[f])
         np.testing.assert_allclose(p[7:], M.frames[f, 7:], atol=1e-15)
         assert p[3] >= 0
+
+
+def test_state_amp_obs_oracle_equals_pose_amp_obs(g12):
+    """The oracle's AMP features of two recorded states equal BuildAMPObs of the (pose, vel)
+    pairs those states were recorded from (the state -> pose recovery is consistent)."""
+    g, char, motion, J, B, M = g12
+    ee, dt = [5, 8, 11, 14], 1.0 / 30
+    for t in np.random.RandomState(2).uniform(dt, M.duration, 6):
+        sp, sc = D.reset_state(J, B, M, t - dt), D.reset_state(J, B, M, t)
+        pp, vp = D.reset_pose_vel(J, B, M, t - dt)
+        pc, vc = D.reset_pose_vel(J, B, M, t)
+        for local in (False, True):
+            a = D.state_amp_obs(J, ee, sp, sc, local)
+            b = D.amp_obs(J, B, ee, pp, vp, pc, vc, local_root=local)
+            assert a.shape == (226,) and np.abs(a - b).max() <= 1e-12
