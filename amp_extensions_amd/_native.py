@@ -46,6 +46,7 @@ SIGNATURES = {
     "amx_amp_obs_size": (c_int, [vp]),
     "amx_state_amp_obs": (c_int, [vp, vp, vp, c_ll, c_int, c_int, vp, c_ll, vp]),
     "amx_motion_amp_obs": (c_int, [vp, vp, c_dbl, c_int, c_int, vp, c_ll, vp]),
+    "amx_state_amp_rows": (c_int, [vp, vp, vp, c_ll, c_int, c_int, vp, c_ll, vp]),
     "amx_npg_param_count": (c_ll, [c_int, c_int]),
     "amx_npg_pass": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp]),
     "amx_npg_reduce": (c_int, [vp, vp, c_int, c_int, vp, vp]),

@@ -22,8 +22,9 @@
 //
 // The clip is preprocessed once on the host (amp_extensions_amd/motion.py: PostProcessFrames
 // and BuildFrameVel, Motion.cpp:167-188, 415-442) and uploaded as one fp64 blob
-// (amx_set_motion).  One thread per lane, fp64 throughout; the per-joint frames live in the
-// thread's private memory (resets are rare after the first: a few lanes per step).
+// (amx_set_motion).  One 64-thread workgroup per lane, one thread per joint / body, fp64
+// throughout, the lane's joint frames in LDS: a reset's latency is a few tree levels deep
+// instead of a serial walk over every joint (resets are a few lanes per step after the first).
 #include "amx_common.h"
 
 namespace {
@@ -147,11 +148,49 @@ __device__ inline Q qnorm(Q q) {
 }
 __device__ inline Q ldq(const double* p) { return {p[0], p[1], p[2], p[3]}; }
 
+// Per-wave scratch of motion_state (LDS): one 64-thread workgroup computes one lane's state,
+// thread j owning joint / body j.
+struct MotionLds {
+  double hdr[HDR], jt[8 * MAXJ], bt[8 * MAXJ];  // blob header and joint / body tables
+  double pose[MAXD], vel[MAXD];
+  double R[MAXJ][9];
+  V3 o[MAXJ], w[MAXJ], v[MAXJ], bp[MAXJ];
+};
+
+__device__ inline double wave_min(double x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = fmin(x, __shfl_xor(x, off));
+  return x;
+}
+
+// Copy the blob header and the joint / body tables into LDS (one pass of independent loads
+// instead of the dependent parent-chain walks reading them from HBM) and return a view whose
+// tables point there.
+__device__ inline MView stage_tables(const double* blob, double* hdr, double* jt, double* bt) {
+  const MView g(blob);
+  for (int i = threadIdx.x; i < HDR; i += blockDim.x) hdr[i] = g.h[i];
+  for (int i = threadIdx.x; i < 8 * g.J; i += blockDim.x) {
+    jt[i] = g.joints[i];
+    bt[i] = g.bodies[i];
+  }
+  __syncthreads();
+  MView m = g;
+  m.h = hdr;
+  m.joints = jt;
+  m.bodies = bt;
+  return m;
+}
+
 // The recorded state at motion time `time` (see the file comment).  out: [S] = 1 + 15 J.
-__device__ void motion_state(const MView& m, double time, int flags, double* __restrict__ out) {
+// Called by all 64 threads of a one-wave workgroup; thread j < J owns joint j.  The joint
+// transforms are composed level by level down the tree (the parent is always done first),
+// with the same per-joint arithmetic as a sequential walk, so the result does not depend on
+// the thread mapping.
+__device__ void motion_state(const MView& m, double time, int flags, double* __restrict__ out, MotionLds& L) {
+  const int tid = threadIdx.x;
   const double dur = m.h[4];
   const bool loop = m.h[3] != 0.0;
-  // ---- Motion::CalcIndexBlend ---------------------------------------------------------------
+  // ---- Motion::CalcIndexBlend (every thread) --------------------------------------------------
   int idx;
   double blend;
   double cycles = 0.0;
@@ -164,12 +203,13 @@ __device__ void motion_state(const MView& m, double time, int flags, double* __r
     if (!loop) cnt = fmin(fmax(cnt, 0.0), 1.0);
     cycles = cnt;
     const double tt = time - cnt * dur;
-    int lo = 0, hi = m.F;  // upper_bound
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (m.times[mid] <= tt) lo = mid + 1; else hi = mid;
-    }
-    idx = lo - 1;
+    // upper_bound over the sorted frame times = the number of times <= tt: counted by the
+    // whole wave with independent loads (no dependent binary-search chain)
+    int c = 0;
+    for (int f = tid; f < m.F; f += 64) c += m.times[f] <= tt;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    idx = c - 1;
     if (idx > m.F - 2) idx = m.F - 2;
     if (idx < 0) idx = 0;
     blend = (tt - m.times[idx]) / (m.times[idx + 1] - m.times[idx]);
@@ -179,116 +219,124 @@ __device__ void motion_state(const MView& m, double time, int flags, double* __r
   const double* f1 = f0 + m.D;
   const double* v0 = m.vels + (long long)idx * m.D;
   const double* v1 = v0 + m.D;
-  double pose[MAXD], vel[MAXD];
-  for (int i = 0; i < m.D; ++i) {
-    pose[i] = (1 - lerp) * f0[i] + lerp * f1[i];
-    vel[i] = (!loop && time >= dur) ? 0.0 : (1.0 - blend) * v0[i] + blend * v1[i];
+  for (int i = tid; i < m.D; i += 64) {
+    L.pose[i] = (1 - lerp) * f0[i] + lerp * f1[i];
+    L.vel[i] = (!loop && time >= dur) ? 0.0 : (1.0 - blend) * v0[i] + blend * v1[i];
   }
-  {
+  __syncthreads();
+  if (tid == 0) {
     Q q = qnorm(slerp(ldq(f0 + 3), ldq(f1 + 3), lerp));
     if (q.w < 0) q = {-q.w, -q.x, -q.y, -q.z};  // StandardizeQuat
-    pose[3] = q.w; pose[4] = q.x; pose[5] = q.y; pose[6] = q.z;
+    L.pose[3] = q.w; L.pose[4] = q.x; L.pose[5] = q.y; L.pose[6] = q.z;
+    if (loop) {
+      L.pose[0] += cycles * m.h[8];
+      L.pose[1] += cycles * m.h[9];
+      L.pose[2] += cycles * m.h[10];
+    }
+    L.pose[0] = 0.0;  // random placement on the plane: root x, z = 0
+    L.pose[2] = 0.0;
+  } else if (tid < m.J && (int)m.joints[8 * tid] == JT_SPHERICAL) {
+    const int o = (int)m.joints[8 * tid + 2];
+    const Q q = slerp(ldq(f0 + o), ldq(f1 + o), lerp);
+    L.pose[o] = q.w; L.pose[o + 1] = q.x; L.pose[o + 2] = q.y; L.pose[o + 3] = q.z;
   }
+  __syncthreads();
+  // ---- kinematics, one tree level per pass ----------------------------------------------------
+  int depth = 0, max_depth = 0;
   for (int j = 1; j < m.J; ++j) {
-    const double* jt = m.joints + 8 * j;
-    if ((int)jt[0] == JT_SPHERICAL) {
-      const int o = (int)jt[2];
-      const Q q = slerp(ldq(f0 + o), ldq(f1 + o), lerp);
-      pose[o] = q.w; pose[o + 1] = q.x; pose[o + 2] = q.y; pose[o + 3] = q.z;
-    }
+    int d = 0;
+    for (int p = j; p > 0; p = (int)m.joints[8 * p + 1]) ++d;
+    if (j == tid) depth = d;
+    max_depth = max(max_depth, d);
   }
-  if (loop) {
-    pose[0] += cycles * m.h[8];
-    pose[1] += cycles * m.h[9];
-    pose[2] += cycles * m.h[10];
-  }
-  pose[0] = 0.0;  // random placement on the plane: root x, z = 0
-  pose[2] = 0.0;
-  // ---- kinematics ---------------------------------------------------------------------------
-  double R[MAXJ][9];
-  V3 o[MAXJ], w[MAXJ], v[MAXJ], bp[MAXJ];
-  for (int j = 0; j < m.J; ++j) {
-    const double* jt = m.joints + 8 * j;
-    const int type = (int)jt[0], par = (int)jt[1], off = (int)jt[2];
-    if (par < 0) {
-      qmat(ldq(pose + 3), R[j]);
-      o[j] = {pose[0], pose[1], pose[2]};
-      w[j] = {vel[3], vel[4], vel[5]};
-      v[j] = {vel[0], vel[1], vel[2]};
-    } else {
-      o[j] = add(o[par], mv(R[par], {jt[4], jt[5], jt[6]}));
-      double L[9];
-      if (type == JT_SPHERICAL) {
-        qmat(ldq(pose + off), L);
-        mm(R[par], L, R[j]);
-        w[j] = add(w[par], mv(R[j], {vel[off], vel[off + 1], vel[off + 2]}));
-      } else if (type == JT_REVOLUTE) {
-        axis_mat({0.0, 0.0, 1.0}, pose[off], L);
-        mm(R[par], L, R[j]);
-        w[j] = add(w[par], mv(R[j], {0.0, 0.0, vel[off]}));
-      } else {  // fixed
-        for (int k = 0; k < 9; ++k) R[j][k] = R[par][k];
-        w[j] = w[par];
+  const int j = tid;
+  for (int lvl = 0; lvl <= max_depth; ++lvl) {
+    if (j < m.J && depth == lvl) {
+      const double* jt = m.joints + 8 * j;
+      const int type = (int)jt[0], par = (int)jt[1], off = (int)jt[2];
+      const double* pose = L.pose;
+      const double* vel = L.vel;
+      if (par < 0) {
+        qmat(ldq(pose + 3), L.R[j]);
+        L.o[j] = {pose[0], pose[1], pose[2]};
+        L.w[j] = {vel[3], vel[4], vel[5]};
+        L.v[j] = {vel[0], vel[1], vel[2]};
+      } else {
+        L.o[j] = add(L.o[par], mv(L.R[par], {jt[4], jt[5], jt[6]}));
+        double Lm[9];
+        if (type == JT_SPHERICAL) {
+          qmat(ldq(pose + off), Lm);
+          mm(L.R[par], Lm, L.R[j]);
+          L.w[j] = add(L.w[par], mv(L.R[j], {vel[off], vel[off + 1], vel[off + 2]}));
+        } else if (type == JT_REVOLUTE) {
+          axis_mat({0.0, 0.0, 1.0}, pose[off], Lm);
+          mm(L.R[par], Lm, L.R[j]);
+          L.w[j] = add(L.w[par], mv(L.R[j], {0.0, 0.0, vel[off]}));
+        } else {  // fixed
+          for (int k = 0; k < 9; ++k) L.R[j][k] = L.R[par][k];
+          L.w[j] = L.w[par];
+        }
+        L.v[j] = add(L.v[par], cross(L.w[par], sub(L.o[j], L.o[par])));
       }
-      v[j] = add(v[par], cross(w[par], sub(o[j], o[par])));
+      const double* bd = m.bodies + 8 * j;
+      L.bp[j] = add(L.o[j], mv(L.R[j], {bd[1], bd[2], bd[3]}));
     }
-    const double* bd = m.bodies + 8 * j;
-    bp[j] = add(o[j], mv(R[j], {bd[1], bd[2], bd[3]}));
+    __syncthreads();
   }
-  // ---- ResolveCharGroundIntersect -------------------------------------------------------------
-  double min_viol = 0.0;
+  // ---- ResolveCharGroundIntersect: deepest AABB violation over the bodies (fmin is exact) -----
+  double viol = 0.0;
   const double pad = m.h[11];
-  for (int j = 0; j < m.J; ++j) {
+  if (j < m.J) {
     const double* bd = m.bodies + 8 * j;
-    if (bd[7] == 0.0) continue;
-    const int sh = (int)bd[0];
-    double ext;
-    if (sh == SH_SPHERE) {
-      ext = 0.5 * bd[4];
-    } else {
-      const double hx = 0.5 * bd[4], hy = sh == SH_CAPSULE ? 0.5 * bd[4] + 0.5 * bd[5] : 0.5 * bd[5];
-      const double hz = sh == SH_CAPSULE ? 0.5 * bd[4] : 0.5 * bd[6];
-      ext = fabs(R[j][3]) * hx + fabs(R[j][4]) * hy + fabs(R[j][5]) * hz;
-    }
-    min_viol = fmin(min_viol, bp[j].y - ext - pad);
-  }
-  if (min_viol < 0) {
-    pose[1] += -min_viol;
-    for (int j = 0; j < m.J; ++j) {
-      o[j].y += -min_viol;
-      bp[j].y += -min_viol;
+    if (bd[7] != 0.0) {
+      const int sh = (int)bd[0];
+      double ext;
+      if (sh == SH_SPHERE) {
+        ext = 0.5 * bd[4];
+      } else {
+        const double hx = 0.5 * bd[4], hy = sh == SH_CAPSULE ? 0.5 * bd[4] + 0.5 * bd[5] : 0.5 * bd[5];
+        const double hz = sh == SH_CAPSULE ? 0.5 * bd[4] : 0.5 * bd[6];
+        ext = fabs(L.R[j][3]) * hx + fabs(L.R[j][4]) * hy + fabs(L.R[j][5]) * hz;
+      }
+      viol = fmin(0.0, L.bp[j].y - ext - pad);
     }
   }
+  const double min_viol = wave_min(viol);
   // ---- CtController::BuildStatePose / BuildStateVel ---------------------------------------------
+  double p[7];
+  for (int k = 0; k < 7; ++k) p[k] = L.pose[k];
+  if (min_viol < 0) p[1] += -min_viol;
   const bool world_root_pos = flags & 1, world_root_rot = flags & 2, all_world = flags & 4;
-  const V3 rd = qrot(ldq(pose + 3), {1.0, 0.0, 0.0});
+  const V3 rd = qrot(ldq(p + 3), {1.0, 0.0, 0.0});
   const double heading = atan2(-rd.z, rd.x);
   double Rh[9];
   axis_mat({0.0, 1.0, 0.0}, -heading, Rh);
-  const Q qh = mat_q(Rh);
-  const V3 origin = {pose[0], 0.0, pose[2]};
-  const V3 root_rel = mv(Rh, sub({pose[0], pose[1], pose[2]}, origin));
-  out[0] = root_rel.y;
-  const int n = m.J;
-  for (int i = 0; i < n; ++i) {
-    V3 p = bp[i];
-    if (!all_world && (!world_root_pos || i != 0)) p = sub(mv(Rh, sub(p, origin)), root_rel);
-    out[9 * i + 1] = p.x; out[9 * i + 2] = p.y; out[9 * i + 3] = p.z;
-    Q q = mat_q(R[i]);
+  const V3 origin = {p[0], 0.0, p[2]};
+  const V3 root_rel = mv(Rh, sub({p[0], p[1], p[2]}, origin));
+  if (tid == 0) out[0] = root_rel.y;
+  if (j < m.J) {
+    const int i = j;
+    V3 oi = L.o[i], bpi = L.bp[i];
+    if (min_viol < 0) {
+      oi.y += -min_viol;
+      bpi.y += -min_viol;
+    }
+    const Q qh = mat_q(Rh);
+    V3 pp = bpi;
+    if (!all_world && (!world_root_pos || i != 0)) pp = sub(mv(Rh, sub(pp, origin)), root_rel);
+    out[9 * i + 1] = pp.x; out[9 * i + 2] = pp.y; out[9 * i + 3] = pp.z;
+    Q q = mat_q(L.R[i]);
     if (!all_world && (!world_root_rot || i != 0)) q = qmul(qh, q);
     const V3 nrm = qrot(q, {0.0, 1.0, 0.0}), tan = qrot(q, {1.0, 0.0, 0.0});
     out[9 * i + 4] = nrm.x; out[9 * i + 5] = nrm.y; out[9 * i + 6] = nrm.z;
     out[9 * i + 7] = tan.x; out[9 * i + 8] = tan.y; out[9 * i + 9] = tan.z;
-  }
-  const int base = 1 + 9 * n;
-  for (int i = 0; i < n; ++i) {
-    V3 lv = add(v[i], cross(w[i], sub(bp[i], o[i])));
-    V3 av = w[i];
+    V3 lv = add(L.v[i], cross(L.w[i], sub(bpi, oi)));
+    V3 av = L.w[i];
     if (!all_world && (!world_root_rot || i != 0)) {
       lv = mv(Rh, lv);
       av = mv(Rh, av);
     }
-    double* d = out + base + 6 * i;
+    double* d = out + 1 + 9 * m.J + 6 * i;
     d[0] = lv.x; d[1] = lv.y; d[2] = lv.z; d[3] = av.x; d[4] = av.y; d[5] = av.z;
   }
 }
@@ -333,43 +381,6 @@ __device__ inline V3 mtv(const double* m, V3 v) {  // m^T v
 __device__ inline void mtm(const double* a, const double* b, double* o) {  // a^T b
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) o[3 * i + j] = a[i] * b[j] + a[3 + i] * b[3 + j] + a[6 + i] * b[6 + j];
-}
-
-// kinematics of a recorded SimEnv state (CtController layout with the root rotation and the
-// root velocities in the world frame, RecordWorldRootRot): rotations from the tangent-normal
-// pairs (R = [tan, nrm, tan x nrm]), joint velocity parameters from the body angular
-// velocities (spherical: R_j^T (w_j - w_parent), revolute: its z component)
-__device__ void kin_from_state(const MView& m, const double* s, AmpKin& k) {
-  const int n = m.J, base = 1 + 9 * n;
-  k.root_y = s[0];
-  tn_mat(s + 4, k.Rw0);
-  heading_of(k.Rw0, k.Rh);
-  mm(k.Rh, k.Rw0, k.R[0]);
-  for (int i = 1; i < n; ++i) tn_mat(s + 9 * i + 4, k.R[i]);
-  V3 w[MAXJ];
-  k.w0 = {s[base + 3], s[base + 4], s[base + 5]};
-  w[0] = mv(k.Rh, k.w0);
-  for (int i = 1; i < n; ++i) w[i] = {s[base + 6 * i + 3], s[base + 6 * i + 4], s[base + 6 * i + 5]};
-  // root joint velocity: body-0 velocity minus w0 x (body-0 offset, back in the world frame)
-  const V3 off = mtv(k.Rh, {s[1], s[2], s[3]});
-  k.v0 = sub({s[base], s[base + 1], s[base + 2]}, cross(k.w0, off));
-  int c = 0;
-  for (int j = 1; j < n; ++j) {
-    const double* jt = m.joints + 8 * j;
-    const int type = (int)jt[0], par = (int)jt[1];
-    if (type == JT_SPHERICAL || type == JT_REVOLUTE) {
-      const V3 wl = mtv(k.R[j], sub(w[j], w[par]));
-      if (type == JT_SPHERICAL) {
-        k.jv[c++] = wl.x; k.jv[c++] = wl.y; k.jv[c++] = wl.z; k.jv[c++] = 0.0;
-      } else {
-        k.jv[c++] = wl.z;
-      }
-    }
-  }
-  k.njv = c;
-  int e = 0;
-  for (int j = 0; j < n && e < 8; ++j)
-    if (m.joints[8 * j + 7] != 0.0) k.ee[e++] = {s[9 * j + 1], s[9 * j + 2], s[9 * j + 3]};
 }
 
 // kinematics of a clip pose / velocity (Motion::CalcFrame / CalcFrameVel)
@@ -514,16 +525,120 @@ __device__ void clip_frame(const MView& m, double time, double* pose, double* ve
   }
 }
 
+// AMP features of (s_prev, s_cur) rows from the recorded states (CtController layout with
+// the root rotation and root velocities in the world frame, RecordWorldRootRot): rotations
+// from the tangent-normal pairs (R = [tan, nrm, tan x nrm]), joint velocity parameters from
+// the body angular velocities (spherical: R_j^T (w_j - w_parent), revolute: its z component),
+// end effectors from the body positions; then the parts of amp_obs.  16 threads per row
+// (thread j: joint / body j), four rows per 64-thread workgroup.
+// T = double: out row = the features (ldo >= size); T = float: the fp32 cost-input row,
+// zero-padded up to ldo.
+struct AmpLds {
+  double R[2][MAXJ][9];  // [prev, cur] joint rotations (root: heading frame)
+  V3 w[2][MAXJ];         // body angular velocities (root: heading frame)
+};
+
+template <typename T>
 __global__ __launch_bounds__(64) void k_state_amp_obs(const double* __restrict__ blob, const double* __restrict__ sp,
                                                       const double* __restrict__ sc, long long lds, int B,
-                                                      int local_root, double* __restrict__ out, long long ldo) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const MView m(blob);
-  AmpKin kp, kc;
-  kin_from_state(m, sp + (long long)b * lds, kp);
-  kin_from_state(m, sc + (long long)b * lds, kc);
-  amp_obs(m, kp, kc, local_root != 0, out + (long long)b * ldo);
+                                                      int local_root, T* __restrict__ out, long long ldo) {
+  __shared__ AmpLds Ls[4];
+  __shared__ double hdr[HDR], jtab[8 * MAXJ], btab[8 * MAXJ];
+  const int g = threadIdx.x >> 4, j = threadIdx.x & 15;
+  const int b = blockIdx.x * 4 + g;
+  const bool valid = b < B;
+  AmpLds& L = Ls[g];
+  const MView m = stage_tables(blob, hdr, jtab, btab);
+  const int n = m.J;
+  const double* st[2] = {sp + (long long)(valid ? b : 0) * lds, sc + (long long)(valid ? b : 0) * lds};
+  const int base = 1 + 9 * n;
+  double Rw0[2][9], Rh[2][9];
+  for (int k = 0; k < 2; ++k) {
+    tn_mat(st[k] + 4, Rw0[k]);
+    heading_of(Rw0[k], Rh[k]);
+  }
+  if (valid && j < n) {
+    for (int k = 0; k < 2; ++k) {
+      const double* s = st[k];
+      if (j == 0) {
+        mm(Rh[k], Rw0[k], L.R[k][0]);
+        L.w[k][0] = mv(Rh[k], {s[base + 3], s[base + 4], s[base + 5]});
+      } else {
+        tn_mat(s + 9 * j + 4, L.R[k][j]);
+        L.w[k][j] = {s[base + 6 * j + 3], s[base + 6 * j + 4], s[base + 6 * j + 5]};
+      }
+    }
+  }
+  __syncthreads();
+  if (!valid) return;
+  // output offsets (SceneImitateAMP::GetAMPObsSize order)
+  int pw = 0, vw = 0, pj = 0, vj = 0, ne = 0, ej = -1;
+  for (int i = 1; i < n; ++i) {
+    const int type = (int)m.joints[8 * i];
+    if (i == j) { pj = pw; vj = vw; }
+    if (type == JT_SPHERICAL) { pw += 6; vw += 4; }
+    else if (type == JT_REVOLUTE) { pw += 1; vw += 1; }
+  }
+  for (int i = 0; i < n && ne < 8; ++i)
+    if (m.joints[8 * i + 7] != 0.0) {
+      if (i == j) ej = ne;
+      ++ne;
+    }
+  const int P = 7 + pw + 3 * ne, V = 6 + vw, D = 2 * P + 2 * V;
+  T* o = out + (long long)b * ldo;
+  const double* Rc = Rh[1];
+  for (int k = 0; k < 2; ++k) {   // k = 1: current (first part), k = 0: previous
+    const double* s = st[k];
+    T* po = o + (k == 1 ? 0 : P);
+    T* vo = o + 2 * P + (k == 1 ? 0 : V);
+    if (j == 0) {
+      double R0[9];
+      if (local_root) {
+        mm(Rc, Rw0[k], R0);
+      } else {
+        for (int q = 0; q < 9; ++q) R0[q] = Rw0[k][q];
+      }
+      po[0] = (T)s[0];
+      po[1] = (T)R0[1]; po[2] = (T)R0[4]; po[3] = (T)R0[7];
+      po[4] = (T)R0[0]; po[5] = (T)R0[3]; po[6] = (T)R0[6];
+      // root joint velocity: body-0 velocity minus w0 x (body-0 offset, back in the world frame)
+      const V3 w0 = {s[base + 3], s[base + 4], s[base + 5]};
+      const V3 off = mtv(Rh[k], {s[1], s[2], s[3]});
+      V3 v = sub({s[base], s[base + 1], s[base + 2]}, cross(w0, off)), w = w0;
+      if (local_root) {
+        v = mv(Rc, v);
+        w = mv(Rc, w);
+      }
+      vo[0] = (T)v.x; vo[1] = (T)v.y; vo[2] = (T)v.z; vo[3] = (T)w.x; vo[4] = (T)w.y; vo[5] = (T)w.z;
+    } else if (j < n) {
+      const int type = (int)m.joints[8 * j], par = (int)m.joints[8 * j + 1];
+      if (type == JT_SPHERICAL || type == JT_REVOLUTE) {
+        double Lm[9];
+        mtm(L.R[k][par], L.R[k][j], Lm);
+        const V3 wl = mtv(L.R[k][j], sub(L.w[k][j], L.w[k][par]));
+        T* q = po + 7 + pj;
+        T* u = vo + 6 + vj;
+        if (type == JT_SPHERICAL) {
+          q[0] = (T)Lm[1]; q[1] = (T)Lm[4]; q[2] = (T)Lm[7]; q[3] = (T)Lm[0]; q[4] = (T)Lm[3]; q[5] = (T)Lm[6];
+          u[0] = (T)wl.x; u[1] = (T)wl.y; u[2] = (T)wl.z; u[3] = (T)0.0;
+        } else {
+          q[0] = (T)atan2(Lm[3], Lm[0]);
+          u[0] = (T)wl.z;
+        }
+      }
+    }
+    if (ej >= 0) {  // end effector: this state's heading-frame offset in the current heading frame
+      double Rx[9];
+      for (int a = 0; a < 3; ++a)
+        for (int c = 0; c < 3; ++c)
+          Rx[3 * a + c] = Rc[3 * a] * Rh[k][3 * c] + Rc[3 * a + 1] * Rh[k][3 * c + 1] + Rc[3 * a + 2] * Rh[k][3 * c + 2];
+      const V3 e = mv(Rx, {s[9 * j + 1], s[9 * j + 2], s[9 * j + 3]});
+      T* q = po + 7 + pw + 3 * ej;
+      q[0] = (T)e.x; q[1] = (T)e.y; q[2] = (T)e.z;
+    }
+  }
+  if constexpr (sizeof(T) == 4)
+    for (long long c = D + j; c < ldo; c += 16) o[c] = (T)0;
 }
 
 __global__ __launch_bounds__(64) void k_motion_amp_obs(const double* __restrict__ blob, const double* __restrict__ times,
@@ -541,12 +656,14 @@ __global__ __launch_bounds__(64) void k_motion_amp_obs(const double* __restrict_
   amp_obs(m, kp, kc, local_root != 0, out + (long long)b * ldo);
 }
 
+// one 64-thread workgroup per lane (motion_state)
 __global__ __launch_bounds__(64) void k_motion_states(const double* __restrict__ blob, const double* __restrict__ times,
                                                       int B, int flags, double* __restrict__ ob, long long ldo) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ MotionLds L;
+  const int b = blockIdx.x;
   if (b >= B) return;
-  const MView m(blob);
-  motion_state(m, times[b], flags, ob + (long long)b * ldo);
+  const MView m = stage_tables(blob, L.hdr, L.jt, L.bt);
+  motion_state(m, times[b], flags, ob + (long long)b * ldo, L);
 }
 
 // SimEnv.reset on masked lanes with motion states: reset_count/model_idx/num_steps as in
@@ -557,16 +674,17 @@ __global__ __launch_bounds__(64) void k_reset_motion(const double* __restrict__ 
                                                      int flags, const double* ob_src, double* ob_out,
                                                      int32_t* num_steps, int32_t* model_idx, int32_t* reset_count,
                                                      double* t_out, int S, int M, int B) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ MotionLds L;
+  const int b = blockIdx.x, tid = threadIdx.x;
   if (b >= B) return;
   const bool do_reset = (mask == nullptr) || mask[b] != 0;
-  if (!do_reset) {
+  if (!do_reset) {  // carried lane: coalesced row copy
     if (ob_src != ob_out)
-      for (int j = 0; j < S; ++j) ob_out[(long long)b * S + j] = ob_src[(long long)b * S + j];
-    if (t_out) t_out[b] = -1.0;
+      for (int j = tid; j < S; j += 64) ob_out[(long long)b * S + j] = ob_src[(long long)b * S + j];
+    if (t_out && tid == 0) t_out[b] = -1.0;
     return;
   }
-  const MView m(blob);
+  const MView m = stage_tables(blob, L.hdr, L.jt, L.bt);
   const int rc = reset_count[b] + 1;
   double t;
   if (times) {
@@ -575,11 +693,13 @@ __global__ __launch_bounds__(64) void k_reset_motion(const double* __restrict__ 
     const amx::u32x4 r = amx::philox4x32_10({(uint32_t)b, (uint32_t)rc, 0u, amx::kTagMotion}, k0, k1);
     t = 0.0 + (m.h[4] - 0.0) * amx::u53(r.x, r.y);
   }
-  motion_state(m, t, flags, ob_out + (long long)b * S);
-  reset_count[b] = rc;
-  model_idx[b] = rc % M;
-  num_steps[b] = 0;
-  if (t_out) t_out[b] = t;
+  motion_state(m, t, flags, ob_out + (long long)b * S, L);
+  if (tid == 0) {
+    reset_count[b] = rc;
+    model_idx[b] = rc % M;
+    num_steps[b] = 0;
+    if (t_out) t_out[b] = t;
+  }
 }
 
 }  // namespace
@@ -640,7 +760,7 @@ extern "C" int amx_motion_states(amx_ctx* c, const double* times, int B, int fla
   AMX_CHECK_ARG(c && c->d_motion, "amx_motion_states: no motion set (amx_set_motion)");
   AMX_CHECK_ARG(times && ob && B >= 0 && ldo >= c->S, "amx_motion_states: bad arguments");
   if (B == 0) return AMX_OK;
-  hipLaunchKernelGGL(k_motion_states, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->d_motion, times, B,
+  hipLaunchKernelGGL(k_motion_states, dim3(B), dim3(64), 0, (hipStream_t)stream, c->d_motion, times, B,
                      flags, ob, ldo);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
@@ -653,7 +773,7 @@ extern "C" int amx_reset_lanes_motion(amx_ctx* c, const uint8_t* mask, const dou
   AMX_CHECK_ARG(ob_out && num_steps && model_idx && reset_count && B >= 0, "amx_reset_lanes_motion: null pointer");
   AMX_CHECK_ARG(mask == nullptr || ob_src != nullptr, "amx_reset_lanes_motion: masked reset needs ob_src");
   if (B == 0) return AMX_OK;
-  hipLaunchKernelGGL(k_reset_motion, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->d_motion, mask, times,
+  hipLaunchKernelGGL(k_reset_motion, dim3(B), dim3(64), 0, (hipStream_t)stream, c->d_motion, mask, times,
                      (uint32_t)seed, (uint32_t)(seed >> 32), flags, ob_src, ob_out, num_steps, model_idx,
                      reset_count, t_out, c->S, c->M, B);
   AMX_CHECK_LAUNCH();
@@ -672,8 +792,20 @@ extern "C" int amx_state_amp_obs(amx_ctx* c, const double* s_prev, const double*
   AMX_CHECK_ARG(s_prev && s_cur && out && B >= 0 && lds >= c->S && ldo >= c->amp_obs_size,
                 "amx_state_amp_obs: bad arguments (lds=%lld ldo=%lld)", lds, ldo);
   if (B == 0) return AMX_OK;
-  hipLaunchKernelGGL(k_state_amp_obs, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, c->d_motion, s_prev,
-                     s_cur, lds, B, local_root, out, ldo);
+  hipLaunchKernelGGL(k_state_amp_obs<double>, dim3((B + 3) / 4), dim3(64), 0, (hipStream_t)stream, c->d_motion,
+                     s_prev, s_cur, lds, B, local_root, out, ldo);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_state_amp_rows(amx_ctx* c, const double* s_prev, const double* s_cur, long long lds, int B,
+                                  int local_root, float* out, long long ldo, void* stream) {
+  AMX_CHECK_ARG(c && c->d_motion, "amx_state_amp_rows: no character set (amx_set_motion)");
+  AMX_CHECK_ARG(s_prev && s_cur && out && B >= 0 && lds >= c->S && ldo >= c->amp_obs_size,
+                "amx_state_amp_rows: bad arguments (lds=%lld ldo=%lld)", lds, ldo);
+  if (B == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_state_amp_obs<float>, dim3((B + 3) / 4), dim3(64), 0, (hipStream_t)stream, c->d_motion,
+                     s_prev, s_cur, lds, B, local_root, out, ldo);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

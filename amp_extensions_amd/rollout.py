@@ -5,7 +5,7 @@ One synchronous step (all lanes) is, in launch order on one HIP stream:
   2. assemble    amx_assemble_input    x0 = [(s-mu)/sd, (a-mu)/sd]               (dynamics.py:225-230)
   3. ensemble    L x amx_gemm_bias_act + amx_gemm_out_unnorm (all M members)     (dynamics.py:422-433)
   4. step        amx_step              s' = s + Δ_k (fp64), done, disagreement, [s, s'] f32 (sim_env.py:140-268)
-                 (amx_cost_rows for the 'sa' / 'sas' / 's' / AMP cost inputs)
+                 (amx_cost_rows for the 'sa' / 'sas' / 's' cost inputs, amx_state_amp_rows for AMP)
   5. auto-reset  amx_reset_lanes       done lanes <- reset-table row, model k+1  (sim_env.py:270-285)
 The step kernel records the float32 [s, s'] cost-input row of every transition; the
 reward pass runs once over all recorded transitions (`score`, at the end of `rollout` or
@@ -96,11 +96,8 @@ class RolloutEngine:
                 raise ValueError(f"cost input width {cost.input_dim} does not match input_type "
                                  f"{self.cost_type!r} (S={S}, A={A}: {width})")
         self.cost_in = z(K, Bp, self.kc)
-        self.amp_rows = None
-        if self.cost_type == "amp":
-            if cost.motion.ctx is not c:
-                raise ValueError("the cost's ReferenceMotion must live on the engine's context")
-            self.amp_rows = z(B, self.kc, dt=torch.float64)
+        if self.cost_type == "amp" and cost.motion.ctx is not c:
+            raise ValueError("the cost's ReferenceMotion must live on the engine's context")
         # rows t*Bp + b with b >= B are padding: excluded from the feature sums
         self.row_mask = None
         if B != Bp:
@@ -203,12 +200,11 @@ class RolloutEngine:
         c, B, S, A = self.ctx, self.B, self.ctx.S, self.ctx.A
         ob, nx, act = self.obs[t], self.next_obs[t], self.acts[t]
         typ = self.cost_type
-        if typ == "amp":
-            m = self.cost.motion
-            D = m.amp_obs_size
-            m.amp_obs_from_states(ob, nx, out=self.amp_rows[:, :D])
-            segs = ((self.amp_rows, self.kc, D), (None, 0, 0), (None, 0, 0))
-        elif typ == "sa":
+        if typ == "amp":   # fp32 AMP rows straight from the two recorded states
+            N.check(c.lib.amx_state_amp_rows(c.h, ob.data_ptr(), nx.data_ptr(), S, B, 0,
+                                             self.cost_in[t].data_ptr(), self.kc, c.stream), "amx_state_amp_rows")
+            return
+        if typ == "sa":
             segs = ((ob, S, S), (act, A, A), (None, 0, 0))
         elif typ == "sas":
             segs = ((ob, S, S), (act, A, A), (nx, S, S))

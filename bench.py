@@ -42,7 +42,9 @@ def parse():
     p.add_argument("--lanes", type=int, default=8192, help="persistent env lanes per GPU")
     p.add_argument("--samples", type=int, default=40000, help="samples per rollout per GPU (weak scaling)")
     p.add_argument("--faithful", action="store_true", help="use the 226/28 state/action layout")
-    p.add_argument("--cost", choices=["mmd", "gail"], default="mmd")
+    p.add_argument("--cost", choices=["mmd", "gail", "amp"], default="mmd",
+                   help="amp: LS discriminator on AMP pose features of (s, s') with reference-motion resets "
+                        "(BASELINE configs[4]; implies --faithful)")
     p.add_argument("--gemm", choices=["bf16x6", "f32"], default="bf16x6",
                    help="ensemble GEMM: 3-limb bf16 split on the bf16 MFMA pipe (fp32-level error) or f32 MFMA")
     p.add_argument("--expert-rows", type=int, default=50000)
@@ -85,6 +87,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cost == "amp":
+        args.faithful = True   # the AMP features are defined on the humanoid3d CtController state
     S, A = (226, 28) if args.faithful else (197, 36)
 
     cpu_base = None
@@ -123,17 +127,31 @@ def main():
     ctx = amx.AmxContext(S, A, n_models=M, hidden=512, n_hidden=4, feat_dim=512, device=dev)
     ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm)
     thr = ens.compute_threshold(st.to(dev), at.to(dev))
-    expert = torch.from_numpy(syn.expert(args.expert_rows, S, 3))
+    reset_source = syn.reset_table(65536, S, 1)
+    if args.cost == "amp":
+        # humanoid3d + spinkick clip (the reference's data files, held as a test fixture);
+        # expert rows = AMP features of the clip at uniform times (RecordAMPObsExpert)
+        from amp_extensions_amd.motion import ReferenceMotion
+        g = np.load(os.path.join(ROOT, "tests", "golden", "g12_motion.npz"), allow_pickle=False)
+        reset_source = ReferenceMotion(ctx, json.loads(str(g["character_json"])),
+                                       {"Loop": str(g["loop"]), "Frames": g["frames"].tolist()})
+        times = np.random.RandomState(3).uniform(1.0 / 30, reset_source.get_motion_length(), args.expert_rows)
+        expert = reset_source.expert_amp_obs(times).float().cpu()
+    else:
+        expert = torch.from_numpy(syn.expert(args.expert_rows, S, 3))
     if args.cost == "mmd":
         cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, bw_samples=100000, lambda_b=0.0025,
                                  seed=100, ctx=ctx)
-    else:
+    elif args.cost == "gail":
         cost = amx.GAILCost(expert, hidden_dims=(1024, 512), lambda_b=0.0025, seed=100, ctx=ctx)
+    else:
+        cost = amx.GAILCost(expert, hidden_dims=(1024, 512), input_type="amp", lambda_b=0.0025, seed=100, ctx=ctx,
+                            motion=reset_source)
     pw, log_std = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
     pol = amx.DevicePolicy(ctx, pw, log_std, seed=1000 + rank)
     B = args.lanes
     T = math.ceil(args.samples / B)
-    eng = amx.RolloutEngine(ens, syn.reset_table(65536, S, 1), lanes=B, policy=pol, cost=cost,
+    eng = amx.RolloutEngine(ens, reset_source, lanes=B, policy=pol, cost=cost,
                             seed=(7 << 32) + rank, max_steps=T)
     eng.reset_all()
 
@@ -178,7 +196,11 @@ def main():
     achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
     ens.gemm_events = None
 
-    step_flops = ens.mlp_flops_per_sample() + 2 * (2 * S) * 512  # + RFF features
+    # + the cost's share: RFF features, or the discriminator MLP on its input
+    if args.cost == "mmd":
+        step_flops = ens.mlp_flops_per_sample() + 2 * (2 * S) * 512
+    else:
+        step_flops = ens.mlp_flops_per_sample() + 2 * (cost.input_dim * 1024 + 1024 * 512 + 512)
     value = total_samples / elapsed
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "gemm_traffic.json")
@@ -208,8 +230,10 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (SURVEY §8d distributions; random-init reference architecture)",
             "config": {
-                "workload": "full MILO rollout: policy + 4-model ensemble step + termination + "
-                            f"{'RFF-MMD relabel' if args.cost == 'mmd' else 'AMP/GAIL LS-disc reward'}",
+                "workload": "full MILO rollout: policy + 4-model ensemble step + termination + " + {
+                    "mmd": "RFF-MMD relabel",
+                    "gail": "AMP/GAIL LS-disc reward on [s, s']",
+                    "amp": "AMP LS-disc reward on AMP pose features of (s, s'), reference-motion resets"}[args.cost],
                 "samples_per_rollout_per_gpu": T * B, "lanes_per_gpu": B, "sync_steps": T,
                 "state_dim": S, "action_dim": A, "ensemble": "4 x dense-connect [512]x4 ReLU",
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",

@@ -181,6 +181,10 @@ int amx_state_amp_obs(amx_ctx* ctx, const double* s_prev, const double* s_cur, l
                       int local_root, double* out, long long ldo, void* stream);
 int amx_motion_amp_obs(amx_ctx* ctx, const double* times, double dt, int B, int local_root, double* out,
                        long long ldo, void* stream);
+/* amx_state_amp_obs written as float32 cost-input rows (the AMP-feature discriminator's
+ * input), zero-padded from amx_amp_obs_size up to ldo. */
+int amx_state_amp_rows(amx_ctx* ctx, const double* s_prev, const double* s_cur, long long lds, int B,
+                       int local_root, float* out, long long ldo, void* stream);
 
 /* ---- NPG policy update (the rollout's learner; mjrl/mjrl/algos/npg_cg.py:113-199) ----
  * Policy: mjrl MLP(S -> 32 -> 32 -> A, tanh) + log_std (mjrl/mjrl/policies/gaussian_mlp.py),
