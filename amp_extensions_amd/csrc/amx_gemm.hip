@@ -71,6 +71,15 @@ struct GemmArgs {
   long long strideW3;      //   elements between groups; a row is 3*K elements
   const uint16_t* A3;      // bf16x6 path, pre-split activations: [g][rows][lda/16][3][16]
   long long strideA3;
+  // f16x3 path (see the section below)
+  const uint16_t* W2;      // 2-limb scaled weight image [g][N][K/16][2][16] (amx_split_f16x2)
+  long long strideW2;
+  const int* w_exp;        // [g][N] column exponents of W2 (strideWexp between groups)
+  long long strideWexp;
+  const int* row_exp;      // [g][slots][rows]: row exponents of A's column slices
+  long long strideRexp;    //   between groups
+  int rexp_slots;          //   slices of A read by this launch (exponent = max over them)
+  int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
 };
 
 long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
@@ -654,7 +663,391 @@ __global__ void k_split_bf16x3(const float* __restrict__ W, int ldw, long long s
   *reinterpret_cast<u32x2*>(dst + 32) = l2;
 }
 
-using X128 = TileX6<2, 2, 2, 2>;           // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
+// ==== f16x3: fp32 as two scaled fp16 limbs, three products ==================================
+// x = 2^-s (x0 + x1) with x0 = RN_f16(2^s x) and x1 = RN_f16(2^s x - x0): 11 + 11 significant
+// bits, |2^s x - x0 - x1| <= 2^-22 |2^s x| (or, below fp16's normal range, 2^-25 absolute
+// against a row maximum scaled to [2^13, 2^14)).  a*b is then a0b0 + a0b1 + a1b0 on the f16
+// matrix pipe with fp32 accumulation; the dropped a1b1 <= 2^-22 |ab|.  Over a K-long dot
+// product these per-term errors add up like sqrt(K) * 2^-23 while the fp32 accumulation of
+// the same sum rounds like K * 2^-24, so for K >= ~64 the result carries the same error as an
+// fp32 GEMM (measured against fp64: tools/x6_accuracy.py) -- at 3 MFMA per 32x32x16 block
+// instead of bf16x6's 6.
+//
+// The scales are powers of two, so they factor out of the contraction exactly:
+//   * weights: per output column c, exponent E_c with max_k |W[c][k]| < 2^E_c, stored
+//     scaled by 2^(14 - E_c) (amx_split_f16x2);
+//   * activations: per row r, exponent E_r with max_k |A[r][k]| < 2^E_r, scaled by
+//     2^(14 - E_r) while staged into LDS.  E_r = max over the row's column slices
+//     (row_exp[g][slot][r]); the dense-concat rows are built slice by slice (x0, h0, h1, ...),
+//     so the assembly writes slot 0 and each hidden layer's epilogue atomically max-es the
+//     exponents of the slice it writes into its own slot (no slot is read and written by the
+//     same launch: deterministic).
+//   * epilogue: acc * 2^(E_r + E_c - 28) (one exact v_ldexp), then the fp32 bias etc. exactly
+//     as the other paths.
+// Exponents are clamped to [-100, 100] (zero rows, inf/NaN rows keep propagating as in fp32).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr int HSC = 14;  // scaled operands stay below 2^14 (fp16 max 65504)
+
+__device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
+  // E with v < 2^E for v = |x| (bits of a non-negative float); clamped to [-100, 100]
+  int e = (int)(absbits >> 23) - 126;
+  e = e < -100 ? -100 : e;
+  return e > 100 ? 100 : e;
+}
+
+// NSUB 16-k granules per K-tile (BK = 16 NSUB); LDS row = NSUB x [limb0 16 | limb1 16] + 8 pad
+// (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
+// distinct 4-bank slots)
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1>
+struct TileH3 {
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
+  static constexpr int LD = NSUB * 32 + 8;                     // f16 per LDS row
+  static constexpr int NT = WM * WN * 64;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  static constexpr int STAGE = (BM + BN) * LD;                 // f16 of one stage (A + W)
+  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t) + BM * sizeof(int);
+  static constexpr int CPR = 4 * NSUB;                         // 16-B chunks per row and K-tile (A f32 and W)
+  static constexpr int NA = BM * CPR, NW = BN * CPR;
+  static constexpr int VA = (NA + NT - 1) / NT, VW = (NW + NT - 1) / NT;
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+// 4 consecutive k of one row, pre-scaled -> two f16 limbs packed as 4 f16 each
+__device__ __forceinline__ void split2(f32x4 x, u32x2& l0, u32x2& l1) {
+  const f16x4 h0 = __builtin_convertvector(x, f16x4);
+  const f32x4 r1 = x - __builtin_convertvector(h0, f32x4);  // exact
+  const f16x4 h1 = __builtin_convertvector(r1, f16x4);
+  l0 = __builtin_bit_cast(u32x2, h0);
+  l1 = __builtin_bit_cast(u32x2, h1);
+}
+
+// One reduce-scatter step of a max over the 32 lanes li: lanes with bit MASK set keep the upper
+// HALF values, their partners the lower; each receives the other half (ds_swizzle bitmask
+// mode: and 0x1f, xor MASK within 32-lane groups) and keeps the max.
+template <int MASK, int HALF>
+__device__ __forceinline__ void rs_step(uint32_t* v, int li) {
+  const bool up = (li & MASK) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const uint32_t keep = up ? v[HALF + i] : v[i];
+    const uint32_t send = up ? v[i] : v[HALF + i];
+    const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send, 0x1f | (MASK << 10));
+    v[i] = keep > recv ? keep : recv;
+  }
+}
+
+// bias / activation / un-normalisation epilogue of the scaled path; for a hidden layer it also
+// reduces the exponents of the rows it wrote (over its columns) into row_exp_out.
+template <int EPI, class TL>
+__device__ __forceinline__ void epilogue_h3(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], const int* sExp, int g,
+                                            int tm, int tn) {
+  constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN;
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int li = lane & 31, lh = lane >> 5;
+  const int lrow0 = wm * TM * 32;                 // tile-local
+  const int row0 = tm * BM + lrow0;
+  const int col0 = tn * BN + wn * TN * 32;
+  const float* bias = a.bias + (long long)g * a.strideBias;
+  const int* wexp = a.w_exp + (long long)g * a.strideWexp;
+  float* Cg = a.C + (long long)g * a.strideC;
+  // row exponents of this lane's 16 rows of block m (rows in groups of 4: ds_read_b128)
+  auto row_exps = [&](int m, int (&er)[16]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int4 v = *reinterpret_cast<const int4*>(sExp + lrow0 + m * 32 + 8 * j + 4 * lh);
+      er[4 * j] = v.x; er[4 * j + 1] = v.y; er[4 * j + 2] = v.z; er[4 * j + 3] = v.w;
+    }
+  };
+  if constexpr (EPI == EPI_BIAS_ACT) {
+    float bv[TN];
+    int ec[TN];
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int col = col0 + n * 32 + li;
+      bv[n] = bias[col];
+      ec[n] = wexp[col] - 2 * HSC;
+    }
+    int* out = a.row_exp_out ? a.row_exp_out + (long long)g * a.strideRexp : nullptr;
+#pragma unroll
+    for (int m = 0; m < TM; ++m) {
+      int er[16];
+      row_exps(m, er);
+      uint32_t mx[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mx[e] = 0u;
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int col = col0 + n * 32 + li;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+          float v = __builtin_amdgcn_ldexpf(acc[m][n][e], er[e] + ec[n]) + bv[n];
+          if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
+          Cg[(long long)row * a.ldc + a.col_off + col] = v;
+          const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
+          mx[e] = mx[e] > b ? mx[e] : b;
+        }
+      }
+      if (out) {
+        // max over the 32 columns (lanes li) of the block's 16 rows of this lane: a
+        // reduce-scatter butterfly over li bits 4..1 leaves lane li row index li>>1, then
+        // one exchange across bit 0
+        rs_step<16, 8>(mx, li);
+        rs_step<8, 4>(mx, li);
+        rs_step<4, 2>(mx, li);
+        rs_step<2, 1>(mx, li);
+        const uint32_t o = (uint32_t)__builtin_amdgcn_ds_swizzle((int)mx[0], 0x1f | (1 << 10));
+        const uint32_t r = mx[0] > o ? mx[0] : o;
+        if ((li & 1) == 0) {
+          const int e = li >> 1;
+          atomicMax(out + row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh, exp_of_bits(r));
+        }
+      }
+    }
+  } else {  // EPI_UNNORM
+#pragma unroll
+    for (int n = 0; n < TN; ++n) {
+      const int col = col0 + n * 32 + li;
+      if (col < a.n_valid) {
+        const float bv = bias[col];
+        const float sc = a.scale[col], sh = a.shift[col];
+        const int ec = wexp[col] - 2 * HSC;
+#pragma unroll
+        for (int m = 0; m < TM; ++m) {
+          int er[16];
+          row_exps(m, er);
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+            const float y = __builtin_amdgcn_ldexpf(acc[m][n][e], er[e] + ec) + bv;
+            const float prod = y * sc;    // two roundings, as torch's (y*scale)+mean
+            Cg[(long long)row * a.ldc + col] = prod + sh;
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int EPI, class TL>
+__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
+  constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
+  constexpr int NT = TL::NT, STAGE = TL::STAGE;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
+  int* const sExp = reinterpret_cast<int*>(sm + 2 * STAGE);
+  int g, tm, tn;
+  map_tile(a, blockIdx.x, g, tm, tn);
+  const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
+  const long long ldw2 = 2LL * a.K;
+  const uint16_t* __restrict__ Wg = a.W2 + (long long)g * a.strideW2 + (long long)tn * TL::BN * ldw2;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int li = lane & 31, lh = lane >> 5;
+
+  // row exponents of the tile's A rows: max over the slices this launch reads
+  {
+    const int* re = a.row_exp + (long long)g * a.strideRexp + (long long)tm * BM;
+    const long long slot = (long long)a.tiles_m * BM;  // slot stride = padded rows
+    for (int r = t; r < BM; r += NT) {
+      int e = -100;
+      for (int s = 0; s < a.rexp_slots; ++s) {
+        const int v = re[s * slot + r];
+        e = v > e ? v : e;
+      }
+      sExp[r] = e;
+    }
+  }
+  __syncthreads();
+
+  // staging maps: A chunk q = t + NT*j -> row q/CPR, k 4*(q%CPR); W chunk q -> row q/CPR,
+  // 16-B piece q%CPR (the image's [granule][limb][16] order is the LDS row's order)
+  constexpr int CPR = TL::CPR, NSUB = TL::NSUB, BK = TL::BK;
+  const float* a_src[VA];
+  int a_dst[VA], a_sh[VA];
+  bool a_ok[VA];
+#pragma unroll
+  for (int j = 0; j < VA; ++j) {
+    const int q = t + NT * j;
+    a_ok[j] = (TL::NA % NT == 0 || j + 1 < VA) ? true : q < TL::NA;
+    const int r = a_ok[j] ? q / CPR : 0, c = q % CPR;
+    a_src[j] = Ag + (long long)r * a.lda + 4 * c;
+    a_dst[j] = r * LD + (c >> 2) * 32 + (c & 3) * 4;
+    a_sh[j] = HSC - sExp[r];
+  }
+  const uint16_t* w_src[VW];
+  int w_dst[VW];
+  bool w_ok[VW];
+#pragma unroll
+  for (int j = 0; j < VW; ++j) {
+    const int q = t + NT * j;
+    w_ok[j] = (TL::NW % NT == 0 || j + 1 < VW) ? true : q < TL::NW;
+    const int r = w_ok[j] ? q / CPR : 0, p = q % CPR;
+    w_src[j] = Wg + (long long)r * ldw2 + p * 8;
+    w_dst[j] = BM * LD + r * LD + p * 8;
+  }
+
+  f32x4 ra[VA];
+  u32x4 rw[VW];
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = a.K / BK;
+  auto load = [&](int kt) {
+    kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
+#pragma unroll
+    for (int j = 0; j < VA; ++j)
+      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+      if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
+  };
+  auto publish = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < VA; ++j)
+      if (a_ok[j]) {
+        f32x4 x = ra[j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
+        u32x2 l0, l1;
+        split2(x, l0, l1);
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+      }
+#pragma unroll
+    for (int j = 0; j < VW; ++j)
+      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+  };
+  const int a_off = (wm * TM * 32 + li) * LD + lh * 8;
+  const int w_off = BM * LD + (wn * TN * 32 + li) * LD + lh * 8;
+  auto compute = [&](int base) {
+    const uint16_t* As = sm + base + a_off;
+    const uint16_t* Ws = sm + base + w_off;
+#pragma unroll
+    for (int sub = 0; sub < NSUB; ++sub) {
+      f16x8 fa[TM][2], fb[TN][2];
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+          fa[m][l] = *reinterpret_cast<const f16x8*>(As + m * 32 * LD + sub * 32 + l * 16);
+#pragma unroll
+      for (int n = 0; n < TN; ++n)
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+          fb[n][l] = *reinterpret_cast<const f16x8*>(Ws + n * 32 * LD + sub * 32 + l * 16);
+      // small terms first: (a1,b0) (a0,b1) (a0,b0)
+      constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
+    }
+  };
+
+  load(0);
+  publish(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    load(kt + 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMA block
+    compute(cur * STAGE);
+    publish((cur ^ 1) * STAGE);
+    __syncthreads();
+  }
+  epilogue_h3<EPI, TL>(a, acc, sExp, g, tm, tn);
+}
+
+// fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
+// [g][rows]: one wave per row (max |w| over K, then the split)
+__global__ __launch_bounds__(256) void k_split_f16x2(const float* __restrict__ W, int ldw, long long strideW,
+                                                     int rows, int K, uint16_t* __restrict__ W2, long long strideW2,
+                                                     int* __restrict__ w_exp, long long strideWexp) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.y;
+  if (r >= rows) return;
+  const float* src = W + g * strideW + (long long)r * ldw;
+  uint32_t mx = 0;
+  for (int c = 4 * lane; c < K; c += 256) {
+    const f32x4 x = *reinterpret_cast<const f32x4*>(src + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t b = __float_as_uint(x[i]) & 0x7fffffffu;
+      mx = mx > b ? mx : b;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
+    mx = mx > o ? mx : o;
+  }
+  const int e = exp_of_bits(mx);
+  if (lane == 0) w_exp[g * strideWexp + r] = e;
+  uint16_t* dst_row = W2 + g * strideW2 + (long long)r * 2 * K;
+  for (int c = 4 * lane; c < K; c += 256) {
+    f32x4 x = *reinterpret_cast<const f32x4*>(src + c);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], HSC - e);
+    u32x2 l0, l1;
+    split2(x, l0, l1);
+    uint16_t* dst = dst_row + (c / 16) * 32 + (c % 16);
+    *reinterpret_cast<u32x2*>(dst) = l0;
+    *reinterpret_cast<u32x2*>(dst + 16) = l1;
+  }
+}
+
+// row exponents of A's first K columns (the x0 slice) into slot 0 of row_exp, slots
+// 1..n_slots-1 reset to -100 (the hidden epilogues max into them): one wave per row
+__global__ __launch_bounds__(256) void k_row_exp(const float* __restrict__ A, int lda, long long strideA, int rows,
+                                                 int K, int* __restrict__ row_exp, long long strideRexp, int n_slots) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.y;
+  if (r >= rows) return;
+  const float* src = A + g * strideA + (long long)r * lda;
+  uint32_t mx = 0;
+  for (int c = lane; c < K; c += 64) {
+    const uint32_t b = __float_as_uint(src[c]) & 0x7fffffffu;
+    mx = mx > b ? mx : b;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
+    mx = mx > o ? mx : o;
+  }
+  int* re = row_exp + g * strideRexp + r;
+  if (lane < n_slots) re[(long long)lane * rows] = lane == 0 ? exp_of_bits(mx) : -100;
+}
+
+using H256w8 = TileH3<2, 4, 4, 2>;      // 256x256, 8 waves of 128x64 (83 KB): 1 WG / CU
+using H128 = TileH3<2, 2, 2, 2>;        // 128x128, 4 waves of 64x64 (41 KB): 2+ WGs / CU
+using H128x224w14 = TileH3<2, 7, 2, 1, 4>;  // 128x224 output layer, 14 waves of 64x32
+using H256w8k32 = TileH3<2, 4, 4, 2, 2, 2>;  // 256x256, BK 32 (148 KB)
+using H256w16 = TileH3<4, 4, 2, 2, 4>;       // 256x256, 16 waves of 64x64
+using H256x128 = TileH3<2, 2, 4, 2, 2>;      // 256x128, 4 waves of 128x64 (62 KB): 2 WGs / CU
+using H128x256 = TileH3<2, 2, 2, 4, 2>;      // 128x256, 4 waves of 64x128
+using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;    // 128x128, BK 32 (74 KB): 2 WGs / CU
+using H256x128k32 = TileH3<2, 2, 4, 2, 1, 2>;  // 256x128, BK 32 (111 KB): 1 WG / CU
+using H128x224k32 = TileH3<2, 7, 2, 1, 4, 2>;  // output layer, BK 32
+
+using X128 = TileX6<2, 2, 2, 2>;          // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
 using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
 using X128x224o4 = TileX6<1, 7, 4, 1, 1, 2, 1, 4>;  // same, <= 128 VGPRs: two WGs (14 waves) per CU
 using X128x224w14 = TileX6<2, 7, 2, 1, 1, 2, 1, 4>; // 128x224, 14 waves of 64x32
@@ -1027,4 +1420,154 @@ extern "C" int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
   return launch_x6<EPI_RFF, X128>(a, (hipStream_t)stream);
+}
+
+// ---- f16x3 entry points -------------------------------------------------------------------
+namespace {
+int g_h3_variant = -1;      // amx__set_h3_variant: hidden-layer tile (-1 automatic; see the switch)
+int g_h3_out_variant = -1;  // amx__set_h3_out_variant: output-layer tile (-1 automatic, 1 BK 32)
+
+template <int EPI, class TL>
+int launch_h3(GemmArgs& a, hipStream_t stream) {
+  a.tiles_m = a.rows / TL::BM;
+  a.tiles_n = a.N / TL::BN;
+  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+  if (nwg == 0) return AMX_OK;
+  hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+int check_h3(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W2,
+             long long strideW2, const int* w_exp, const int* row_exp, int rexp_slots) {
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
+  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
+                AMX_ROW_TILE);
+  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, XBK);
+  AMX_CHECK_ARG(A && W2 && amx::aligned16(A) && amx::aligned16(W2), "%s: null/unaligned operand", fn);
+  AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
+  AMX_CHECK_ARG(strideW2 % 8 == 0, "%s: strideW2=%lld must be a multiple of 8", fn, strideW2);
+  AMX_CHECK_ARG(w_exp && row_exp && rexp_slots >= 1, "%s: null exponents or rexp_slots=%d", fn, rexp_slots);
+  return AMX_OK;
+}
+}  // namespace
+
+extern "C" int amx__set_h3_variant(int v) {
+  g_h3_variant = v;
+  return AMX_OK;
+}
+extern "C" int amx__set_h3_out_variant(int v) {
+  g_h3_out_variant = v;
+  return AMX_OK;
+}
+
+extern "C" int amx_split_f16x2(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw, long long strideW,
+                               uint16_t* W2, long long strideW2, int* w_exp, long long strideWexp, void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_split_f16x2: null ctx");
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS && rows > 0, "amx_split_f16x2: groups=%d rows=%d", groups,
+                rows);
+  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "amx_split_f16x2: K=%d must be a positive multiple of %d", K, XBK);
+  AMX_CHECK_ARG(W && W2 && w_exp && amx::aligned16(W) && amx::aligned16(W2), "amx_split_f16x2: null/unaligned operand");
+  AMX_CHECK_ARG(ldw >= K && ldw % 4 == 0 && strideW2 >= 2LL * K * rows && strideW2 % 8 == 0 && strideWexp >= rows,
+                "amx_split_f16x2: ldw=%d strideW2=%lld strideWexp=%lld (K=%d rows=%d)", ldw, strideW2, strideWexp, K,
+                rows);
+  hipLaunchKernelGGL(k_split_f16x2, dim3((unsigned)((rows + 3) / 4), groups), dim3(256), 0, (hipStream_t)stream, W,
+                     ldw, strideW, rows, K, W2, strideW2, w_exp, strideWexp);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_row_exponents(amx_ctx* ctx, int groups, int rows, int K, const float* A, int lda, long long strideA,
+                                 int* row_exp, long long strideRexp, int n_slots, void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_row_exponents: null ctx");
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS && rows >= 0, "amx_row_exponents: groups=%d rows=%d", groups,
+                rows);
+  AMX_CHECK_ARG(A && row_exp && K > 0 && lda >= K, "amx_row_exponents: null operand or K=%d lda=%d", K, lda);
+  AMX_CHECK_ARG(n_slots >= 1 && n_slots <= 64 && strideRexp >= (long long)n_slots * rows,
+                "amx_row_exponents: n_slots=%d strideRexp=%lld rows=%d", n_slots, strideRexp, rows);
+  if (rows == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_row_exp, dim3((unsigned)((rows + 3) / 4), groups), dim3(256), 0, (hipStream_t)stream, A, lda,
+                     strideA, rows, K, row_exp, strideRexp, n_slots);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
+                                    long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
+                                    long long strideWexp, const float* bias, long long strideBias, float* C, int ldc,
+                                    long long strideC, int col_off, int act, const int* row_exp,
+                                    long long strideRexp, int rexp_slots, int* row_exp_out, void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_gemm_bias_act_h3: null ctx");
+  int rc = check_h3("amx_gemm_bias_act_h3", groups, rows, K, A, lda, W2, strideW2, w_exp, row_exp, rexp_slots);
+  if (rc) return rc;
+  AMX_CHECK_ARG(N > 0 && N % 128 == 0, "amx_gemm_bias_act_h3: N=%d must be a multiple of 128", N);
+  AMX_CHECK_ARG(strideW2 >= 2LL * K * N || groups == 1, "amx_gemm_bias_act_h3: strideW2=%lld < 2*K*N", strideW2);
+  AMX_CHECK_ARG(bias && C, "amx_gemm_bias_act_h3: null bias/C");
+  AMX_CHECK_ARG(col_off >= 0 && col_off + N <= ldc, "amx_gemm_bias_act_h3: col_off=%d N=%d ldc=%d", col_off, N, ldc);
+  AMX_CHECK_ARG(act == AMX_ACT_NONE || act == AMX_ACT_RELU, "amx_gemm_bias_act_h3: act=%d", act);
+  AMX_CHECK_ARG(strideRexp >= (long long)rexp_slots * rows || groups == 1, "amx_gemm_bias_act_h3: strideRexp=%lld",
+                strideRexp);
+  GemmArgs a = {};
+  a.A = A; a.strideA = strideA; a.lda = lda;
+  a.W2 = W2; a.strideW2 = strideW2; a.w_exp = w_exp; a.strideWexp = strideWexp;
+  a.bias = bias; a.strideBias = strideBias;
+  a.C = C; a.strideC = strideC; a.ldc = ldc; a.col_off = col_off;
+  a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
+  a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots; a.row_exp_out = row_exp_out;
+  const hipStream_t s = (hipStream_t)stream;
+  const bool fit256 = rows % 256 == 0 && N % 256 == 0;
+  const bool m256 = rows % 256 == 0, n256 = N % 256 == 0;
+  switch (g_h3_variant) {
+    case 0: return launch_h3<EPI_BIAS_ACT, H128>(a, s);
+    case 1: if (fit256) return launch_h3<EPI_BIAS_ACT, H256w8>(a, s); break;
+    case 2: if (fit256) return launch_h3<EPI_BIAS_ACT, H256w8k32>(a, s); break;
+    case 3: if (fit256) return launch_h3<EPI_BIAS_ACT, H256w16>(a, s); break;
+    case 4: if (m256) return launch_h3<EPI_BIAS_ACT, H256x128>(a, s); break;
+    case 5: if (n256) return launch_h3<EPI_BIAS_ACT, H128x256>(a, s); break;
+    case 6: if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s); break;
+    case 7: if (m256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256x128k32>(a, s); break;
+    default: break;
+  }
+  // automatic: 256x256 with BK 32 (8 waves of 128x64, one WG per CU) when its grid fills the
+  // chip -- 8-10% ahead of BK 16 and of 16 waves on the hidden layers (tools/h3_variants.py);
+  // otherwise 128x128 (BK 32 when K allows)
+  if (fit256 && K % 32 == 0 &&
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32::LDS, H256w8k32::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256w8k32>(a, s);
+  if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
+  return launch_h3<EPI_BIAS_ACT, H128>(a, s);
+}
+
+extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
+                                      int lda, long long strideA, const uint16_t* W2, long long strideW2,
+                                      const int* w_exp, long long strideWexp, const float* bias, long long strideBias,
+                                      float* preds, int ldp, long long strideP, const int* row_exp,
+                                      long long strideRexp, int rexp_slots, void* stream) {
+  AMX_CHECK_ARG(ctx && ctx->have_norm, "amx_gemm_out_unnorm_h3: context has no normalizers");
+  int rc = check_h3("amx_gemm_out_unnorm_h3", groups, rows, K, A, lda, W2, strideW2, w_exp, row_exp, rexp_slots);
+  if (rc) return rc;
+  AMX_CHECK_ARG(n_valid == ctx->S, "amx_gemm_out_unnorm_h3: n_valid=%d must equal S=%d", n_valid, ctx->S);
+  AMX_CHECK_ARG(bias && preds && ldp >= n_valid, "amx_gemm_out_unnorm_h3: null bias/preds or ldp=%d", ldp);
+  GemmArgs a = {};
+  a.A = A; a.strideA = strideA; a.lda = lda;
+  a.W2 = W2; a.strideW2 = strideW2; a.w_exp = w_exp; a.strideWexp = strideWexp;
+  a.bias = bias; a.strideBias = strideBias;
+  a.C = preds; a.strideC = strideP; a.ldc = ldp;
+  a.rows = rows; a.K = K; a.groups = groups;
+  a.n_valid = n_valid;
+  a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots;
+  const int S = ctx->S, Ad = ctx->A;
+  a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
+  a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
+  // weight rows padded to round_up(S, 128) (amx_layout n_out_pad); S <= 224 runs one 224-wide tile
+  const int n32 = amx::round_up(n_valid, 32);
+  if (n32 > 128 && n32 <= 224) {
+    a.N = 224;
+    AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
+    if (g_h3_out_variant == 0 || K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224w14>(a, (hipStream_t)stream);
+    return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);  // BK 32: 3% ahead
+  }
+  a.N = amx::round_up(n_valid, 128);
+  AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
+  return launch_h3<EPI_UNNORM, H128>(a, (hipStream_t)stream);
 }

@@ -97,6 +97,18 @@ def split_bf16x3(ctx: AmxContext, W: torch.Tensor) -> torch.Tensor:
     return W3
 
 
+def split_f16x2(ctx: AmxContext, W: torch.Tensor):
+    """Scaled 2-limb fp16 image [G][rows][K/16][2][16] (int16 bits) + row exponents [G][rows]
+    of a [G][rows][K] fp32 device weight (amx_split_f16x2), the operand of the amx_*_h3 GEMMs."""
+    G, rows, K = W.shape
+    W = W.contiguous()
+    W2 = torch.empty(G, rows, 2 * K, dtype=torch.int16, device=ctx.device)
+    wexp = torch.empty(G, rows, dtype=torch.int32, device=ctx.device)
+    N.check(ctx.lib.amx_split_f16x2(ctx.h, G, rows, K, W.data_ptr(), K, rows * K, W2.data_ptr(), rows * 2 * K,
+                                    wexp.data_ptr(), rows, ctx.stream), "amx_split_f16x2")
+    return W2, wexp
+
+
 def _check_dev(t: torch.Tensor, dtype, name: str, device) -> None:
     if not isinstance(t, torch.Tensor) or t.device != device or t.dtype != dtype or not t.is_contiguous():
         raise ValueError(f"{name}: expected a contiguous {dtype} tensor on {device}, got "
@@ -111,11 +123,12 @@ class DeviceEnsemble:
     All members share the normalizers (DynamicsEnsemble.load_ensemble, dynamics.py:128-131).
     """
 
-    GEMM_PRECISIONS = ("bf16x6", "f32")
+    GEMM_PRECISIONS = ("f16x3", "bf16x6", "f32")
 
     def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "bf16x6"):
         """gemm: "bf16x6" (fp32 operands split into 3 bf16 limbs, 6 limb products on the bf16
-        MFMA pipe: fp32-level error, amx_gemm_*_x6) or "f32" (v_mfma_f32_32x32x2_f32)."""
+        MFMA pipe: fp32-level error, amx_gemm_*_x6), "f16x3" (power-of-two scaled operands
+        split into 2 fp16 limbs, 3 products: amx_gemm_*_h3) or "f32" (v_mfma_f32_32x32x2_f32)."""
         if gemm not in self.GEMM_PRECISIONS:
             raise ValueError(f"gemm must be one of {self.GEMM_PRECISIONS}, got {gemm!r}")
         self.gemm = gemm
@@ -149,9 +162,12 @@ class DeviceEnsemble:
                 bp[m, :out_dim] = torch.as_tensor(b_m).float().cpu()
             self.W.append(Wp.to(dev).contiguous())
             self.b.append(bp.to(dev).contiguous())
-        self.W3 = None
+        self.W3 = self.W2 = self.wexp = None
         if gemm == "bf16x6":
             self.W3 = [split_bf16x3(ctx, W) for W in self.W]
+        elif gemm == "f16x3":
+            sp = [split_f16x2(ctx, W) for W in self.W]
+            self.W2, self.wexp = [x[0] for x in sp], [x[1] for x in sp]
         ctx.set_normalizers(norms)
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
@@ -171,7 +187,9 @@ class DeviceEnsemble:
         if ws is None:
             c = self.ctx
             ws = dict(Bp=Bp, act=torch.zeros(c.M, Bp, c.ldk, dtype=torch.float32, device=c.device),
-                      preds=torch.zeros(c.M, Bp, c.S, dtype=torch.float32, device=c.device))
+                      preds=torch.zeros(c.M, Bp, c.S, dtype=torch.float32, device=c.device),
+                      # f16x3: row exponents of the activation slices [M][L+1][Bp] (x0, h0..h_{L-1})
+                      rexp=torch.zeros(c.M, c.L + 1, Bp, dtype=torch.int32, device=c.device))
             self._ws[Bp] = ws
         return ws
 
@@ -194,16 +212,39 @@ class DeviceEnsemble:
         if not assembled:  # (the device policy can write x0 itself: amx_policy_act's fused assembly)
             N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
                                              c.ldk, B, s), "amx_assemble_input")
-        self._mlp(buf, preds, Bp, s)
+        self._mlp(buf, preds, Bp, s, ws["rexp"])
         return preds
 
-    def _mlp(self, buf, preds, Bp, s):
+    def _mlp_h3(self, buf, preds, Bp, s, rexp):
+        c = self.ctx
+        sA, sR, L = Bp * c.ldk, (c.L + 1) * Bp, c.L
+        for i in range(L):
+            K = c.k0_pad + i * c.Hp
+            N.check(c.lib.amx_gemm_bias_act_h3(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),
+                                               c.Hp * 2 * K, self.wexp[i].data_ptr(), c.Hp, self.b[i].data_ptr(), c.Hp,
+                                               buf.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, rexp.data_ptr(), sR,
+                                               i + 1, rexp[0, i + 1].data_ptr(), s), "amx_gemm_bias_act_h3")
+        N.check(c.lib.amx_gemm_out_unnorm_h3(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
+                                             self.W2[L].data_ptr(), c.n_out_pad * 2 * c.ldk, self.wexp[L].data_ptr(),
+                                             c.n_out_pad, self.b[L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
+                                             Bp * c.S, rexp.data_ptr(), sR, L + 1, s), "amx_gemm_out_unnorm_h3")
+
+    def _mlp(self, buf, preds, Bp, s, rexp):
         c = self.ctx
         sA = Bp * c.ldk
+        if self.W2 is not None:  # x0 row exponents (slot 0) + reset of the hidden slots
+            N.check(c.lib.amx_row_exponents(c.h, c.M, Bp, c.k0_pad, buf.data_ptr(), c.ldk, sA, rexp.data_ptr(),
+                                            (c.L + 1) * Bp, c.L + 1, s), "amx_row_exponents")
         ev = self.gemm_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
+        if self.W2 is not None:
+            self._mlp_h3(buf, preds, Bp, s, rexp)
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1, Bp))
+            return
         for i in range(c.L):
             K = c.k0_pad + i * c.Hp
             if self.W3 is not None:

@@ -30,8 +30,25 @@ sys.path.insert(0, ROOT)
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: Peak FP32 (matrix), v_mfma_f32_32x32x2_f32
 # bf16 dense MFMA: 256 CUs x 4 SIMDs x 1024 FLOP/clk (v_mfma_f32_32x32x16_bf16: 32 cycles) x 2.4 GHz
 BF16_MFMA_PEAK_TFLOPS = 2516.6
-# the bf16x6 GEMM issues 6 bf16 limb products per f32 multiply-add: its f32-equivalent ceiling
+# the bf16x6 GEMM issues 6 bf16 limb products per f32 multiply-add, the f16x3 GEMM 3 fp16 limb
+# products (fp16 dense MFMA = the bf16 rate): their f32-equivalent ceilings
 X6_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 6
+H3_PEAK_TFLOPS = BF16_MFMA_PEAK_TFLOPS / 3
+GEMM_INFO = {
+    "f16x3": dict(peak=H3_PEAK_TFLOPS, products=3,
+                  desc="f16x3: fp32 operands scaled by powers of two (per weight row / activation row) and split "
+                       "into 2 fp16 limbs, 3 limb products per f32 MAC accumulated in fp32 (error vs fp64 <= the "
+                       "f32 MFMA's, tools/h3_accuracy.py)",
+                  unit="TFLOP/s (f32-equivalent; peak = f16 dense 2516.6 / 3 limb products)",
+                  kernel="k_gemm_h3 (ensemble layers, v_mfma_f32_32x32x16_f16 x 3 per f32 MAC)"),
+    "bf16x6": dict(peak=X6_PEAK_TFLOPS, products=6,
+                   desc="bf16x6: fp32 operands split exactly into 3 bf16 limbs, 6 limb products per f32 MAC "
+                        "accumulated in fp32 (error vs fp64 = the f32 MFMA's, tools/x6_accuracy.py)",
+                   unit="TFLOP/s (f32-equivalent; peak = bf16 dense 2516.6 / 6 limb products)",
+                   kernel="k_gemm_x6 (ensemble layers, v_mfma_f32_32x32x16_bf16 x 6 per f32 MAC)"),
+    "f32": dict(peak=F32_MFMA_PEAK_TFLOPS, products=None, desc="f32 MFMA (v_mfma_f32_32x32x2_f32)",
+                unit="TFLOP/s", kernel="k_gemm_nt (ensemble layers, f32 MFMA 32x32x2)"),
+}
 
 
 def parse():
@@ -45,8 +62,9 @@ def parse():
     p.add_argument("--cost", choices=["mmd", "gail", "amp"], default="mmd",
                    help="amp: LS discriminator on AMP pose features of (s, s') with reference-motion resets "
                         "(BASELINE configs[4]; implies --faithful)")
-    p.add_argument("--gemm", choices=["bf16x6", "f32"], default="bf16x6",
-                   help="ensemble GEMM: 3-limb bf16 split on the bf16 MFMA pipe (fp32-level error) or f32 MFMA")
+    p.add_argument("--gemm", choices=["f16x3", "bf16x6", "f32"], default="f16x3",
+                   help="ensemble GEMM: scaled 2-limb fp16 split (3 products) or 3-limb bf16 split (6 products) on "
+                        "the 16-bit MFMA pipe (both fp32-level error), or f32 MFMA")
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
@@ -203,7 +221,7 @@ def main():
         step_flops = ens.mlp_flops_per_sample() + 2 * (cost.input_dim * 1024 + 1024 * 512 + 512)
     value = total_samples / elapsed
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", "gemm_traffic.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"gemm_traffic_{args.gemm}.json")
     if os.path.exists(pmc_path):
         try:
             with open(pmc_path) as f:
@@ -213,8 +231,8 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    x6 = args.gemm == "bf16x6"
-    peak = X6_PEAK_TFLOPS if x6 else F32_MFMA_PEAK_TFLOPS
+    gi = GEMM_INFO[args.gemm]
+    peak = gi["peak"]
     if rank == 0:
         out = {
             "metric": "learned-dynamics env steps/sec (humanoid3d, 40k-sample rollout)",
@@ -239,17 +257,14 @@ def main():
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
                 "parallelism": f"dp{world} (lane-sharded, 1 all-reduce/rollout)",
                 "termination_rate": round(term_rate, 5), "threshold": thr,
-                "gemm": ("bf16x6: fp32 operands split exactly into 3 bf16 limbs, 6 limb products per f32 MAC "
-                         "accumulated in fp32 (error vs fp64 = the f32 MFMA's, tools/x6_accuracy.py)") if x6
-                else "f32 MFMA (v_mfma_f32_32x32x2_f32)",
+                "gemm": gi["desc"],
             },
             "roofline": {
                 "bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": round(peak, 1),
-                "unit": "TFLOP/s" + (" (f32-equivalent; peak = bf16 dense 2516.6 / 6 limb products)" if x6 else ""),
+                "unit": gi["unit"],
                 "frac": round(achieved_tflops / peak, 4), "traffic": traffic,
-                "kernel": ("k_gemm_x6 (ensemble layers, v_mfma_f32_32x32x16_bf16 x 6 per f32 MAC)" if x6
-                           else "k_gemm_nt (ensemble layers, f32 MFMA 32x32x2)"),
-                "bf16_mfma_tflops": round(6 * achieved_tflops, 1) if x6 else None,
+                "kernel": gi["kernel"],
+                "matrix_pipe_tflops": round(gi["products"] * achieved_tflops, 1) if gi["products"] else None,
                 "avg_launch_us": round(gemm_ms * 1e3 / max(launches, 1), 2),
                 "flops_per_launch": flops_per_fwd / (ctx.L + 1),
             },

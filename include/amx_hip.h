@@ -146,6 +146,40 @@ int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const
                         const uint16_t* W3, const float* b, float scale, float* phi, int ldphi,
                         double* col_partials, const uint8_t* row_mask, void* stream);
 
+/* ---- f16x3: the same fp32 GEMMs as two scaled fp16 limbs, three products ---------------
+ * Each fp32 operand is scaled by a power of two (per weight row / per activation row) and
+ * split into two fp16 limbs (11 + 11 significant bits); a*b = a0b0 + a0b1 + a1b0 in fp32
+ * MFMA accumulators.  The per-term error (<= ~2^-22 |ab|) adds up like sqrt(K) while the
+ * fp32 accumulation's grows like K, so the GEMM error equals an fp32 GEMM's for K >= ~64
+ * (tools/x6_accuracy.py); 3 MFMA per 32x32x16 block instead of bf16x6's 6.  Same
+ * semantics, layouts and epilogues as amx_gemm_bias_act / amx_gemm_out_unnorm
+ * (BasicMLP.forward, milo/milo/dynamics.py:422-433 + DynamicsModel.forward :231-232).
+ *
+ * amx_split_f16x2: W [groups][rows][K] fp32 -> W2 [groups][rows][K/16][2][16] fp16 bits
+ * (row stride 2K) scaled by 2^(14 - E_r), E_r = w_exp[g][r] (max_k |W| < 2^E_r).
+ * Row exponents of A: row_exp [groups][slots][rows] int32 (group stride strideRexp, slot
+ * stride = rows); a GEMM scales row r by 2^(14 - max over slots 0..rexp_slots-1).
+ * amx_row_exponents writes slot 0 from A's first K columns and resets slots 1..n_slots-1;
+ * amx_gemm_bias_act_h3 with row_exp_out (the slot of the columns it writes; nullable)
+ * max-es the exponents of its output rows into it, so a dense-concat chain of layers
+ * (layer i reads slots 0..i, writes slot i+1) needs no other pass.  K % 16 == 0. */
+int amx_split_f16x2(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw,
+                    long long strideW, uint16_t* W2, long long strideW2, int* w_exp,
+                    long long strideWexp, void* stream);
+int amx_row_exponents(amx_ctx* ctx, int groups, int rows, int K, const float* A, int lda,
+                      long long strideA, int* row_exp, long long strideRexp, int n_slots,
+                      void* stream);
+int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
+                         long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
+                         long long strideWexp, const float* bias, long long strideBias, float* C,
+                         int ldc, long long strideC, int col_off, int act, const int* row_exp,
+                         long long strideRexp, int rexp_slots, int* row_exp_out, void* stream);
+int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
+                           int lda, long long strideA, const uint16_t* W2, long long strideW2,
+                           const int* w_exp, long long strideWexp, const float* bias,
+                           long long strideBias, float* preds, int ldp, long long strideP,
+                           const int* row_exp, long long strideRexp, int rexp_slots, void* stream);
+
 /* ---- reference-motion resets (SimEnv.reset -> DeepMimicCore reset_time, §8f #2) ----------
  * amx_set_motion: host blob (copied; amp_extensions_amd/motion.py build_blob): header[16]
  *   {J, D, F, loop, duration, -, -, -, cycle_delta xyz, ground_pad, ...}, joints [J][8]

@@ -1,0 +1,189 @@
+"""The f16x3 ensemble GEMM (power-of-two scaled operands split into two fp16 limbs, three
+products on the f16 MFMA pipe, fp32 accumulation): parity with the oracle's fp32 forward
+(dynamics.py:216-233, 422-433) at the f32 path's tolerance, per-row independence of the
+activation scaling (extreme, zero and non-finite rows), determinism, the weight split and
+the row-exponent slots, and the C ABI's argument checks."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import milo_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def offline(n, seed, S, A):
+    rs = np.random.RandomState(seed)
+    s = 0.5 * rs.randn(n, S)
+    s[:, 0] = rs.uniform(0.8, 0.95, n)
+    a = rs.randn(n, A)
+    s2 = s + 0.01 * rs.randn(n, S)
+    return s, a, s2
+
+
+def make(S, A, hidden, gemms=("f16x3", "f32"), M=4):
+    import amp_extensions_amd as amx
+    s, a, s2 = offline(2048, 0, S, A)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
+    ens_w = R.init_ensemble_weights(S, A, hidden, M, 100)
+    ctx = amx.AmxContext(S, A, n_models=M, hidden=hidden[0], n_hidden=len(hidden), feat_dim=512, device=DEV)
+    ens = {g: amx.DeviceEnsemble(ctx, ens_w, norms, gemm=g) for g in gemms}
+    return amx, ctx, ens, ens_w, norms, (s, a)
+
+
+def row_err(p, ref):
+    """max |p - ref| per row over max(1, max |ref row|), over members."""
+    d = np.abs(p - ref).max(axis=-1)
+    return (d / np.maximum(1.0, np.abs(ref).max(axis=-1))).max(axis=0)
+
+
+@pytest.mark.parametrize("S,A,hidden,B", [(197, 36, [512] * 4, 8192), (197, 36, [512] * 4, 640),
+                                          (100, 20, [256] * 3, 640), (300, 40, [128] * 2, 384),
+                                          (226, 28, [100] * 2, 200)])
+def test_f16x3_ensemble_matches_oracle_and_f32(S, A, hidden, B):
+    """Tile paths: 8192 lanes -> 256x256 BK32 hidden tiles, smaller grids -> 128x128; S=197 ->
+    the 128x224 output tile, S=100 -> 128, S=300 -> three 128 tiles; hidden 100 -> padded
+    columns.  Same tolerance as the f32 path (2e-5 of max(1, |ref|)) and within 1e-6 of it."""
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, hidden)
+    rs = np.random.RandomState(1)
+    ob = 0.5 * rs.randn(B, S)
+    ob[:, 0] = rs.uniform(0.8, 0.95, B)
+    ac = rs.randn(B, A)
+    obd, acd = torch.from_numpy(ob).to(DEV), torch.from_numpy(ac).to(DEV)
+    p3 = ens["f16x3"].forward_preds(obd, acd, B)[:, :B].cpu().numpy().astype(np.float64)
+    p32 = ens["f32"].forward_preds(obd, acd, B)[:, :B].cpu().numpy().astype(np.float64)
+    n = min(B, 1024)  # the fp32 CPU oracle on a prefix
+    ref = R.ensemble_preds(ens_w, norms, torch.from_numpy(ob[:n]).float(), torch.from_numpy(ac[:n]).float()).numpy()
+    scale = max(1.0, np.abs(ref).max())
+    assert np.abs(p3[:, :n] - ref).max() / scale <= 2e-5
+    assert np.abs(p32[:, :n] - ref).max() / scale <= 2e-5
+    assert np.abs(p3 - p32).max() / max(1.0, np.abs(p32).max()) <= 1e-6
+
+
+def _f64_forward(ens_w, norms, ob, ac):
+    mu_s, sd_s, mu_a, sd_a, mu_d, sd_d = [np.asarray(x, np.float64) for x in norms]
+    x = np.concatenate([(ob.astype(np.float32).astype(np.float64) - mu_s) / sd_s,
+                        (ac.astype(np.float32).astype(np.float64) - mu_a) / sd_a], 1)
+    out = []
+    for layers in ens_w:
+        h = x
+        for i, (W, b) in enumerate(layers):
+            y = h @ np.asarray(W, np.float64).T + np.asarray(b, np.float64)
+            if i < len(layers) - 1:
+                h = np.concatenate([h, np.maximum(y, 0.0)], 1)
+        out.append(y * sd_d + mu_d)
+    return np.stack(out)
+
+
+def test_f16x3_extreme_and_zero_rows():
+    """Rows 1e4x and 1e-4x the offline scale, rows exactly at the normalizer mean (x0 = 0) and
+    ordinary rows in one batch: each row is scaled by its own power of two, so every row's
+    error vs fp64 stays at fp32 level relative to that row, no worse than the f32 MFMA path's,
+    and the ordinary rows are bit-identical to a batch without the extreme ones."""
+    S, A, B = 197, 36, 512
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4)
+    rs = np.random.RandomState(2)
+    ob = 0.5 * rs.randn(B, S)
+    ob[:, 0] = rs.uniform(0.8, 0.95, B)
+    ac = rs.randn(B, A)
+    mu_s, mu_a = np.asarray(norms[0], np.float64), np.asarray(norms[2], np.float64)
+    ob2, ac2 = ob.copy(), ac.copy()
+    ob2[:64] = mu_s + (ob[:64] - mu_s) * 1e4
+    ac2[:64] = mu_a + (ac[:64] - mu_a) * 1e4
+    ob2[64:128] = mu_s + (ob[64:128] - mu_s) * 1e-4
+    ac2[64:128] = mu_a + (ac[64:128] - mu_a) * 1e-4
+    ob2[128:136] = mu_s.astype(np.float32)
+    ac2[128:136] = mu_a.astype(np.float32)
+    ref = _f64_forward(ens_w, norms, ob2, ac2)
+    e3 = ens["f16x3"]
+    p3 = e3.forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :B].cpu().numpy()
+    p32 = ens["f32"].forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :B].cpu().numpy()
+    r3, r32 = row_err(p3.astype(np.float64), ref), row_err(p32.astype(np.float64), ref)
+    assert r3.max() <= 2e-5, r3.max()
+    assert (r3 <= 2.0 * r32 + 1e-6).all()
+    clean = e3.forward_preds(torch.from_numpy(ob).to(DEV), torch.from_numpy(ac).to(DEV), B)[:, :B].cpu().numpy()
+    np.testing.assert_array_equal(p3[:, 136:], clean[:, 136:])
+
+
+def test_f16x3_nonfinite_rows_stay_local_and_deterministic():
+    """A NaN / inf state row propagates to that row's outputs only; the other rows match the
+    finite batch bit for bit; two forwards of the same input are bit-identical (the row
+    exponents come from per-layer slots, never read and written by one launch)."""
+    S, A, B = 197, 36, 384
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4, gemms=("f16x3",))
+    e3 = ens["f16x3"]
+    ob = torch.from_numpy(s[:B].copy()).to(DEV)
+    ac = torch.from_numpy(a[:B].copy()).to(DEV)
+    clean = e3.forward_preds(ob, ac, B)[:, :B].clone()
+    again = e3.forward_preds(ob, ac, B)[:, :B].clone()
+    assert torch.equal(clean, again)
+    bad = ob.clone()
+    bad[5, 3] = float("nan")
+    bad[77, 0] = float("inf")
+    got = e3.forward_preds(bad, ac, B)[:, :B].clone()
+    assert torch.isnan(got[:, 5]).all() and not torch.isfinite(got[:, 77]).all()
+    keep = torch.ones(B, dtype=torch.bool, device=DEV)
+    keep[5] = keep[77] = False
+    assert torch.equal(got[:, keep], clean[:, keep])
+
+
+def test_f16x3_split_and_row_exponent_slots():
+    """amx_split_f16x2: (limb0 + limb1) * 2^(E-14) reconstructs W to 2^-22 of the row max, with
+    2^(E-1) <= max|W_row| < 2^E (zero rows E = -100); after a forward, slot i+1 of the row
+    exponents holds the exponent of each row's largest h_i, slot 0 that of x0."""
+    S, A, B = 197, 36, 256
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4, gemms=("f16x3",))
+    from amp_extensions_amd import _native as N
+    from amp_extensions_amd.engine import split_f16x2
+    rs = np.random.RandomState(5)
+    W = (rs.randn(2, 128, 64) * np.exp(rs.uniform(-20, 20, (2, 128, 1)))).astype(np.float32)
+    W[1, 7] = 0.0
+    W2, wexp = split_f16x2(ctx, torch.from_numpy(W).to(DEV))
+    torch.cuda.synchronize()
+    E = wexp.cpu().numpy()
+    limbs = W2.cpu().numpy().view(np.float16).astype(np.float64).reshape(2, 128, 4, 2, 16)
+    rec = limbs.sum(axis=3).reshape(2, 128, 64) * np.exp2(E - 14.0)[..., None]
+    rmax = np.abs(W).max(axis=-1).astype(np.float64)
+    assert E[1, 7] == -100
+    nz = rmax > 0
+    assert (rmax[nz] < np.exp2(E[nz])).all() and (rmax[nz] >= np.exp2(E[nz] - 1.0)).all()
+    assert (np.abs(rec - W).max(axis=-1) <= rmax * 2.0 ** -22).all()
+    e3 = ens["f16x3"]
+    ob = torch.from_numpy(s[:B]).to(DEV)
+    ac = torch.from_numpy(a[:B]).to(DEV)
+    e3.forward_preds(ob, ac, B)
+    ws = e3.workspace(B)
+    torch.cuda.synchronize()
+    act, rexp = ws["act"].cpu().numpy(), ws["rexp"].cpu().numpy()
+    k0, Hp = ctx.k0_pad, ctx.Hp
+
+    def exps(x):
+        m = np.abs(x).max(axis=-1)
+        e = np.where(m > 0, np.frexp(m)[1], -100)
+        return np.clip(e, -100, 100)
+
+    np.testing.assert_array_equal(rexp[:, 0, :B], exps(act[:, :B, :k0]))
+    for i in range(ctx.L):
+        np.testing.assert_array_equal(rexp[:, i + 1, :B], exps(act[:, :B, k0 + i * Hp:k0 + (i + 1) * Hp]))
+
+
+def test_f16x3_abi_checks():
+    import amp_extensions_amd as amx
+    ctx = amx.AmxContext(226, 28, n_models=4, hidden=128, n_hidden=2, device=DEV)
+    lib, s = ctx.lib, ctx.stream
+    buf = torch.zeros(1, 128, 64, dtype=torch.float32, device=DEV)
+    W2 = torch.zeros(128, 128, dtype=torch.int16, device=DEV)
+    we = torch.zeros(128, dtype=torch.int32, device=DEV)
+    rc = lib.amx_gemm_bias_act_h3(ctx.h, 1, 128, 128, 64, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128,
+                                  we.data_ptr(), 128, buf.data_ptr(), 0, buf.data_ptr(), 128, 0, 0, 1, None, 0, 1,
+                                  None, s)
+    assert rc == -1 and b"null exponents" in lib.amx_last_error()
+    rc = lib.amx_gemm_bias_act_h3(ctx.h, 1, 100, 128, 64, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128,
+                                  we.data_ptr(), 128, buf.data_ptr(), 0, buf.data_ptr(), 128, 0, 0, 1, we.data_ptr(),
+                                  128, 1, None, s)
+    assert rc == -1 and b"multiple of 128" in lib.amx_last_error()
+    rc = lib.amx_split_f16x2(ctx.h, 1, 128, 40, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128, we.data_ptr(), 128, s)
+    assert rc == -1 and b"multiple of 16" in lib.amx_last_error()
+    rc = lib.amx_row_exponents(ctx.h, 1, 128, 64, buf.data_ptr(), 64, 0, we.data_ptr(), 128, 2, s)
+    assert rc == -1 and b"n_slots" in lib.amx_last_error()

@@ -67,10 +67,10 @@ def test_philox_matches_oracle(amx):
     np.testing.assert_array_equal(got, ref)
 
 
-@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
+@pytest.mark.parametrize("gemm", ["f16x3", "bf16x6", "f32"])
 @pytest.mark.parametrize("tag", ["h64", "h512"])
 def test_ensemble_vs_reference_golden(amx, golden, norms, tag, gemm):
-    """Device ensemble (both GEMM paths) vs the REFERENCE's own DynamicsModel.forward outputs."""
+    """Device ensemble (every GEMM path) vs the REFERENCE's own DynamicsModel.forward outputs."""
     g = golden(f"g1_ensemble_{tag}.npz")
     hidden = [int(x) for x in g["hidden"]]
     ctx, _, ens = make_ensemble(amx, hidden, norms, gemm=gemm)
@@ -87,7 +87,7 @@ def test_ensemble_vs_reference_golden(amx, golden, norms, tag, gemm):
     np.testing.assert_allclose(thr, float(g["threshold"]), rtol=1e-4)
 
 
-@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
+@pytest.mark.parametrize("gemm", ["f16x3", "bf16x6", "f32"])
 def test_ensemble_forward_f64_padding(amx, norms, gemm):
     """fp64 state input (SimEnv's ob) with B not a multiple of 128, full [512]*4 ensemble."""
     ctx, ens_w, ens = make_ensemble(amx, [512] * 4, norms, gemm=gemm)

@@ -1,4 +1,4 @@
-"""HBM traffic of the ensemble GEMM from rocprofv3 PMC passes -> profiles/gemm_traffic.json.
+"""HBM traffic of the ensemble GEMM from rocprofv3 PMC passes -> profiles/gemm_traffic_<gemm>.json.
 
 Two separate counter passes over the same bench command (MI355X_MICROARCH.md, HBM section:
 one counter per pass, FETCH_SIZE counts half of the wide coalesced loads on gfx950 -> x2):
@@ -8,9 +8,10 @@ one counter per pass, FETCH_SIZE counts half of the wide coalesced loads on gfx9
       python $R/bench.py --no-cpu-baseline --steps 3 --warmup 1
   rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- \
       python $R/bench.py --no-cpu-baseline --steps 3 --warmup 1
-  python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [lanes] [S] [A] [bf16x6|f32] > profiles/gemm_traffic.json
+  python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [lanes] [S] [A] [f16x3|bf16x6|f32] \
+      > profiles/gemm_traffic_<gemm>.json
 
-The last L+1 ensemble-layer dispatches (k_gemm_x6 / k_gemm_nt with the BIAS_ACT / UNNORM epilogues, i.e.
+The last L+1 ensemble-layer dispatches (k_gemm_h3 / k_gemm_x6 / k_gemm_nt with the BIAS_ACT / UNNORM epilogues, i.e.
 the final step's forward) are taken; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch,
 against the algorithmic bytes (activation panel read + weights + output write).
 """
@@ -45,9 +46,10 @@ def main():
     k0 = (S + A + 31) // 32 * 32
     n_out_pad = (S + 127) // 128 * 128
     rows = M * B
-    gemm = sys.argv[6] if len(sys.argv) > 6 else "bf16x6"
-    kernel = "k_gemm_x6" if gemm == "bf16x6" else "k_gemm_nt"
-    wb = 6 if gemm == "bf16x6" else 4  # weight bytes per element as the kernel reads them (3 bf16 limbs)
+    gemm = sys.argv[6] if len(sys.argv) > 6 else "f16x3"
+    kernel = {"f16x3": "k_gemm_h3", "bf16x6": "k_gemm_x6", "f32": "k_gemm_nt"}[gemm]
+    # weight bytes per element as the kernel reads them (3 bf16 limbs / 2 fp16 limbs / fp32)
+    wb = 6 if gemm == "bf16x6" else 4
     f = per_dispatch(fetch_dir, "FETCH_SIZE", kernel)[-(L + 1):]
     w = per_dispatch(write_dir, "WRITE_SIZE", kernel)[-(L + 1):]
     layers, tot_hbm, tot_alg = [], 0, 0
