@@ -28,6 +28,7 @@ SIGNATURES = {
     "amx_set_termination": (c_int, [vp, c_int, vp, vp, vp, vp, c_int, c_int, c_int, c_int, c_int,
                                     c_int, c_int, c_dbl, c_int, c_dbl]),
     "amx_assemble_input": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp]),
+    "amx_assemble_input_rexp": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp, c_ll, c_ll, c_int, vp]),
     "amx_gemm_bias_act": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
                                   vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp]),
     "amx_gemm_out_unnorm": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
@@ -57,6 +58,9 @@ SIGNATURES = {
     "amx_npg_pass": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp]),
     "amx_npg_reduce": (c_int, [vp, vp, c_int, c_int, vp, vp]),
     "amx_step": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_int, vp]),
+    "amx_step_rexp": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, c_int, vp]),
+    "amx_rff_features_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp, vp, c_flt, vp, c_int,
+                                    vp, vp, vp]),
     "amx_disagreement": (c_int, [vp, vp, c_int, c_ll, vp, c_int, vp]),
     "amx_reset_lanes": (c_int, [vp, vp, vp, c_int, vp, c_u64, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_policy_act": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, c_u64, c_int, vp, vp, vp, c_ll,

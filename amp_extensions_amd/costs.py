@@ -65,9 +65,10 @@ class RBFLinearCost:
 
     def __init__(self, expert_data: torch.Tensor, feature_dim=1024, input_type="ss", cost_range=(-1.0, 0.0),
                  bw_quantile=0.1, bw_samples=100000, lambda_b=1.0, lr=0.0, seed=100, ctx: AmxContext | None = None,
-                 device="cuda", gemm: str = "bf16x6", motion=None):
-        """`gemm` selects the feature GEMM: "bf16x6" (3-limb bf16 split, fp32-level error) or
-        "f32" (f32 MFMA); `motion` (a ReferenceMotion) is needed for input_type "amp" (expert
+                 device="cuda", gemm: str = "f16x3", motion=None):
+        """`gemm` selects the feature GEMM: "f16x3" (scaled 2-limb fp16 split) or "bf16x6"
+        (3-limb bf16 split), both fp32-level error, or "f32" (f32 MFMA); `motion` (a
+        ReferenceMotion) is needed for input_type "amp" (expert
         rows = AMP observations); everything else follows the reference constructor."""
         _check_input_type(input_type, motion)
         torch.manual_seed(seed)          # linear_cost.py:34-35

@@ -699,9 +699,12 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // NSUB 16-k granules per K-tile (BK = 16 NSUB); LDS row = NSUB x [limb0 16 | limb1 16] + 8 pad
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
-template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1>
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false>
 struct TileH3 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
+  // LATE: barrier -> publish tile t+1 -> issue the loads of t+2 -> compute t (write after
+  // the barrier: the LDS writes drain under the MFMAs, the loads get a whole K-tile)
+  static constexpr bool LATE = LATE_;
   static constexpr int LD = NSUB * 32 + 8;                     // f16 per LDS row
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
@@ -740,8 +743,38 @@ __device__ __forceinline__ void rs_step(uint32_t* v, int li) {
 // bias / activation / un-normalisation epilogue of the scaled path; for a hidden layer it also
 // reduces the exponents of the rows it wrote (over its columns) into row_exp_out.
 template <int EPI, class TL>
+__device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], const int* sExp,
+                                                 int g, int tm, int tn);
+
+// EPI_RFF: the accumulators are un-scaled in place (exact powers of two) and handed to the
+// shared RFF epilogue (cos, phi rows, fp64 column partials), which reuses the stage LDS
+template <int EPI, class TL>
 __device__ __forceinline__ void epilogue_h3(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], const int* sExp, int g,
                                             int tm, int tn) {
+  if constexpr (EPI == EPI_RFF) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm = wave / TL::WN, wn = wave % TL::WN, li = lane & 31, lh = lane >> 5;
+    const int* wexp = a.w_exp + (long long)g * a.strideWexp;
+#pragma unroll
+    for (int n = 0; n < TL::TN; ++n) {
+      const int ec = wexp[tn * TL::BN + wn * TL::TN * 32 + n * 32 + li] - 2 * HSC;
+#pragma unroll
+      for (int m = 0; m < TL::TM; ++m)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          acc[m][n][e] = __builtin_amdgcn_ldexpf(
+              acc[m][n][e], sExp[wm * TL::TM * 32 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh] + ec);
+    }
+    __syncthreads();  // every wave is done with the stage buffers (and with sExp)
+    epilogue<EPI_RFF, TL>(a, acc, g, tm, tn);
+  } else {
+    epilogue_h3_impl<EPI, TL>(a, acc, sExp, g, tm, tn);
+  }
+}
+
+template <int EPI, class TL>
+__device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], const int* sExp,
+                                                 int g, int tm, int tn) {
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN;
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -833,7 +866,11 @@ __device__ __forceinline__ void epilogue_h3(const GemmArgs& a, f32x16 (&acc)[TL:
   }
 }
 
-template <int EPI, class TL>
+// ABL != 0: ablations for the timing study only (tools/h3_variants.py, variants 91..95; wrong
+// results by design): 1 every K-tile loads tile 0 (L2-hot operands), 2 no barrier in the
+// loop, 3 A staged without the split (limb1 = limb0), 4 no loads / LDS writes in the loop,
+// 5 = 4 without the barrier (the bare fragment-read + MFMA loop)
+template <int EPI, class TL, int ABL = 0>
 __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
   constexpr int NT = TL::NT, STAGE = TL::STAGE;
@@ -907,6 +944,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   const int nk = a.K / BK;
   auto load = [&](int kt) {
     kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
+    if constexpr (ABL == 1) kt = 0;
 #pragma unroll
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
@@ -919,10 +957,14 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) {
         f32x4 x = ra[j];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
         u32x2 l0, l1;
-        split2(x, l0, l1);
+        if constexpr (ABL == 3) {
+          l0 = l1 = __builtin_bit_cast(u32x2, __builtin_convertvector(x, f16x4));
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
+          split2(x, l0, l1);
+        }
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
       }
@@ -935,41 +977,62 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   auto compute = [&](int base) {
     const uint16_t* As = sm + base + a_off;
     const uint16_t* Ws = sm + base + w_off;
+    // m-outer order: the W fragments of the granule stay in registers, the A fragments of
+    // block m+1 are read while block m's 3*TN MFMAs run (fewer live fragment registers than
+    // reading the whole granule up front; each accumulator still sees the same sequence)
+    f16x8 fb[TN][2], fa[2][2];
 #pragma unroll
     for (int sub = 0; sub < NSUB; ++sub) {
-      f16x8 fa[TM][2], fb[TN][2];
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int l = 0; l < 2; ++l)
-          fa[m][l] = *reinterpret_cast<const f16x8*>(As + m * 32 * LD + sub * 32 + l * 16);
 #pragma unroll
       for (int n = 0; n < TN; ++n)
 #pragma unroll
         for (int l = 0; l < 2; ++l)
           fb[n][l] = *reinterpret_cast<const f16x8*>(Ws + n * 32 * LD + sub * 32 + l * 16);
-      // small terms first: (a1,b0) (a0,b1) (a0,b0)
-      constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int l = 0; l < 2; ++l) fa[0][l] = *reinterpret_cast<const f16x8*>(As + sub * 32 + l * 16);
 #pragma unroll
-        for (int m = 0; m < TM; ++m)
+      for (int m = 0; m < TM; ++m) {
+        if (m + 1 < TM) {
+#pragma unroll
+          for (int l = 0; l < 2; ++l)
+            fa[(m + 1) & 1][l] = *reinterpret_cast<const f16x8*>(As + (m + 1) * 32 * LD + sub * 32 + l * 16);
+        }
+        // small terms first: (a1,b0) (a0,b1) (a0,b0)
+        constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
 #pragma unroll
           for (int n = 0; n < TN; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m & 1][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
+      }
     }
   };
 
+  if constexpr (TL::LATE) {
+    load(0);
+    publish(0);
+    load(1);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      __syncthreads();  // tile kt visible in buffer cur; buffer cur^1 (tile kt-1) fully read
+      publish((cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
+      load(kt + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(cur * STAGE);
+    }
+    epilogue_h3<EPI, TL>(a, acc, sExp, g, tm, tn);
+    return;
+  }
   load(0);
   publish(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    load(kt + 1);
+    if constexpr (ABL != 4 && ABL != 5) load(kt + 1);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMA block
     compute(cur * STAGE);
-    publish((cur ^ 1) * STAGE);
-    __syncthreads();
+    if constexpr (ABL != 4 && ABL != 5) publish((cur ^ 1) * STAGE);
+    if constexpr (ABL != 2 && ABL != 5) __syncthreads();
   }
   epilogue_h3<EPI, TL>(a, acc, sExp, g, tm, tn);
 }
@@ -1046,6 +1109,11 @@ using H128x256 = TileH3<2, 2, 2, 4, 2>;      // 128x256, 4 waves of 64x128
 using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;    // 128x128, BK 32 (74 KB): 2 WGs / CU
 using H256x128k32 = TileH3<2, 2, 4, 2, 1, 2>;  // 256x128, BK 32 (111 KB): 1 WG / CU
 using H128x224k32 = TileH3<2, 7, 2, 1, 4, 2>;  // output layer, BK 32
+using H128x224w4k32 = TileH3<4, 1, 1, 7, 1, 2>;  // output layer, 4 waves of 32x224, BK 32
+using H128x224w4 = TileH3<4, 1, 1, 7, 2, 1>;     // output layer, 4 waves of 32x224, BK 16 (56 KB)
+using H128x224w7k32 = TileH3<1, 7, 4, 1, 2, 2>;  // output layer, 7 waves of 128x32, BK 32
+using H256w16k32 = TileH3<4, 4, 2, 2, 4, 2>;     // 256x256, 16 waves of 64x64, BK 32
+using H256w8k32late = TileH3<2, 4, 4, 2, 2, 2, true>;  // H256w8k32, write-after-barrier schedule
 
 using X128 = TileX6<2, 2, 2, 2>;          // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
 using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
@@ -1427,13 +1495,15 @@ namespace {
 int g_h3_variant = -1;      // amx__set_h3_variant: hidden-layer tile (-1 automatic; see the switch)
 int g_h3_out_variant = -1;  // amx__set_h3_out_variant: output-layer tile (-1 automatic, 1 BK 32)
 
-template <int EPI, class TL>
+template <int EPI, class TL, int ABL = 0>
 int launch_h3(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
   a.tiles_n = a.N / TL::BN;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
+  hipLaunchKernelGGL((k_gemm_h3<EPI, TL, ABL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -1526,14 +1596,21 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 5: if (n256) return launch_h3<EPI_BIAS_ACT, H128x256>(a, s); break;
     case 6: if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s); break;
     case 7: if (m256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256x128k32>(a, s); break;
+    case 8: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32>(a, s); break;
+    case 9: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32late>(a, s); break;
+    case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
+    case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
+    case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
+    case 94: return launch_h3<EPI_BIAS_ACT, H256w8k32, 4>(a, s);
+    case 95: return launch_h3<EPI_BIAS_ACT, H256w8k32, 5>(a, s);
     default: break;
   }
-  // automatic: 256x256 with BK 32 (8 waves of 128x64, one WG per CU) when its grid fills the
-  // chip -- 8-10% ahead of BK 16 and of 16 waves on the hidden layers (tools/h3_variants.py);
-  // otherwise 128x128 (BK 32 when K allows)
+  // automatic: 256x256 with BK 32 (8 waves of 128x64, one WG per CU), write-after-barrier
+  // schedule, when its grid fills the chip -- 8-10% ahead of BK 16, 2% ahead of the
+  // write-before-barrier schedule (tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
   if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32::LDS, H256w8k32::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256w8k32>(a, s);
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32late::LDS, H256w8k32late::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256w8k32late>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1565,9 +1642,34 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (g_h3_out_variant == 0 || K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224w14>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
     return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);  // BK 32: 3% ahead
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
   return launch_h3<EPI_UNNORM, H128>(a, (hipStream_t)stream);
+}
+
+extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
+                                   const uint16_t* W2, const int* w_exp, const int* row_exp, const float* b,
+                                   float scale, float* phi, int ldphi, double* col_partials, const uint8_t* row_mask,
+                                   void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_rff_features_h3: null ctx");
+  int rc = check_h3("amx_rff_features_h3", 1, rows, K, x, ldx, W2, 0, w_exp, row_exp, 1);
+  if (rc) return rc;
+  AMX_CHECK_ARG(F > 0 && F % 128 == 0, "amx_rff_features_h3: F=%d must be a multiple of 128", F);
+  AMX_CHECK_ARG(b && phi && col_partials && ldphi >= F, "amx_rff_features_h3: null b/phi/partials or ldphi");
+  AMX_CHECK_ARG(n_valid >= 0 && n_valid <= rows, "amx_rff_features_h3: n_valid=%d rows=%d", n_valid, rows);
+  GemmArgs a = {};
+  a.A = x; a.lda = ldx;
+  a.W2 = W2; a.w_exp = w_exp;
+  a.row_exp = row_exp; a.rexp_slots = 1;
+  a.bias = b;
+  a.C = phi; a.ldc = ldphi;
+  a.rows = rows; a.N = F; a.K = K; a.groups = 1;
+  a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
+  if (K % 32 == 0) return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
+  return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);
 }

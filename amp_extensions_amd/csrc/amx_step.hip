@@ -22,12 +22,15 @@ __device__ inline double wave_sum(double v) {
 
 // ---- assemble -----------------------------------------------------------------------
 // x0 = [(s - mu_s)/sd_s, (a - mu_a)/sd_a, 0...] into every model's activation row.
-// One wave per lane row; writes k0_pad columns for each of M models.
+// One wave per lane row; writes k0_pad columns for each of M models.  With row_exp (the
+// f16x3 GEMM's row-exponent slots, amx_row_exponents' layout) it also writes slot 0 = the
+// exponent of the row's max |x0| and resets slots 1..n_slots-1 for every model.
 template <typename T>
 __global__ __launch_bounds__(256) void k_assemble(const T* __restrict__ ob, const T* __restrict__ act,
                                                   const float* __restrict__ norm, float* __restrict__ buf,
                                                   long long stride_m, int ldk, int S, int A, int M, int k0_pad,
-                                                  int B) {
+                                                  int B, int* __restrict__ row_exp, long long stride_rexp,
+                                                  long long slot_stride, int n_slots) {
   const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
@@ -35,6 +38,7 @@ __global__ __launch_bounds__(256) void k_assemble(const T* __restrict__ ob, cons
   const float* sd_s = norm + S;
   const float* mu_a = norm + 2 * S;
   const float* sd_a = norm + 2 * S + A;
+  uint32_t mx = 0;
   for (int j = lane; j < k0_pad; j += 64) {
     float x = 0.f;
     if (j < S) {
@@ -46,6 +50,20 @@ __global__ __launch_bounds__(256) void k_assemble(const T* __restrict__ ob, cons
       x = (v - mu_a[k]) / sd_a[k];
     }
     for (int m = 0; m < M; ++m) buf[m * stride_m + (long long)b * ldk + j] = x;
+    const uint32_t bits = __float_as_uint(x) & 0x7fffffffu;
+    mx = mx > bits ? mx : bits;
+  }
+  if (row_exp == nullptr) return;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
+    mx = mx > o ? mx : o;
+  }
+  if (lane < n_slots) {
+    int e = (int)(mx >> 23) - 126;  // max|x0| < 2^e, clamped as the GEMM's exponents
+    e = e < -100 ? -100 : (e > 100 ? 100 : e);
+    const int v = lane == 0 ? e : -100;
+    for (int m = 0; m < M; ++m) row_exp[m * stride_rexp + lane * slot_stride + b] = v;
   }
 }
 
@@ -124,6 +142,7 @@ struct StepArgs {
   const double* ob; double* ob_next;
   int32_t* num_steps; uint8_t* done; float* disc;
   float* cost_in; int ldc;
+  int* cost_rexp;  // nullable: exponent of each cost row's max |x| (f16x3 RFF GEMM's row_exp)
   uint8_t* nonfinite;
   int S, M, B;
   amx_termination term;
@@ -156,6 +175,7 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   // rescale of check_velocity (:264-267) when RecordVelAsPos and the check are enabled.
   const bool vscale = T.vel_check && T.record_vel_as_pos;
   bool vel_bad = false, bad = false;
+  uint32_t cmax = 0;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
     const int j = lane + 64 * it;
@@ -167,13 +187,28 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
       if (T.vel_check && j >= T.vel_offset) vel_bad |= fabs(v) > T.vel_thresh;
       bad |= !isfinite(v);
       if (a.cost_in) {
-        a.cost_in[(long long)b * a.ldc + j] = (float)o[it];
-        a.cost_in[(long long)b * a.ldc + S + j] = (float)v;
+        const float c0 = (float)o[it], c1 = (float)v;
+        a.cost_in[(long long)b * a.ldc + j] = c0;
+        a.cost_in[(long long)b * a.ldc + S + j] = c1;
+        const uint32_t u0 = __float_as_uint(c0) & 0x7fffffffu, u1 = __float_as_uint(c1) & 0x7fffffffu;
+        cmax = cmax > u0 ? cmax : u0;
+        cmax = cmax > u1 ? cmax : u1;
       }
     }
   }
   if (a.cost_in) {  // zero the K padding of the cost-input row
     for (int j = 2 * S + lane; j < a.ldc; j += 64) a.cost_in[(long long)b * a.ldc + j] = 0.f;
+    if (a.cost_rexp) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const uint32_t oo = (uint32_t)__shfl_xor((int)cmax, off);
+        cmax = cmax > oo ? cmax : oo;
+      }
+      if (lane == 0) {
+        int e = (int)(cmax >> 23) - 126;  // max|row| < 2^e (amx_row_exponents' clamp)
+        a.cost_rexp[b] = e < -100 ? -100 : (e > 100 ? 100 : e);
+      }
+    }
   }
 
   // fall check (sim_env.py:175-257): lane i < n evaluates body i; every lane takes part
@@ -518,31 +553,51 @@ inline dim3 lanes_grid(int B) { return dim3((unsigned)((B + 3) / 4)); }  // 4 la
 
 }  // namespace
 
-extern "C" int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
-                                  long long stride_m, int ldk, int B, void* stream) {
-  AMX_CHECK_ARG(ctx && ctx->have_norm, "amx_assemble_input: context has no normalizers");
-  AMX_CHECK_ARG(ob && act && act_buf, "amx_assemble_input: null pointer");
-  AMX_CHECK_ARG(B >= 0, "amx_assemble_input: B=%d", B);
-  AMX_CHECK_ARG(ldk >= ctx->k0_pad, "amx_assemble_input: ldk=%d < k0_pad=%d", ldk, ctx->k0_pad);
-  AMX_CHECK_ARG(ctx->M == 1 || stride_m >= (long long)ldk * B, "amx_assemble_input: stride_m too small");
+static int assemble(const char* fn, amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
+                    long long stride_m, int ldk, int B, int* row_exp, long long stride_rexp, long long slot_stride,
+                    int n_slots, void* stream) {
+  AMX_CHECK_ARG(ctx && ctx->have_norm, "%s: context has no normalizers", fn);
+  AMX_CHECK_ARG(ob && act && act_buf, "%s: null pointer", fn);
+  AMX_CHECK_ARG(B >= 0, "%s: B=%d", fn, B);
+  AMX_CHECK_ARG(ldk >= ctx->k0_pad, "%s: ldk=%d < k0_pad=%d", fn, ldk, ctx->k0_pad);
+  AMX_CHECK_ARG(ctx->M == 1 || stride_m >= (long long)ldk * B, "%s: stride_m too small", fn);
   if (B == 0) return AMX_OK;
   hipStream_t s = (hipStream_t)stream;
   if (in_dtype == AMX_IN_F64) {
     hipLaunchKernelGGL(k_assemble<double>, lanes_grid(B), dim3(256), 0, s, (const double*)ob, (const double*)act,
-                       ctx->d_norm, act_buf, stride_m, ldk, ctx->S, ctx->A, ctx->M, ctx->k0_pad, B);
+                       ctx->d_norm, act_buf, stride_m, ldk, ctx->S, ctx->A, ctx->M, ctx->k0_pad, B, row_exp,
+                       stride_rexp, slot_stride, n_slots);
   } else if (in_dtype == AMX_IN_F32) {
     hipLaunchKernelGGL(k_assemble<float>, lanes_grid(B), dim3(256), 0, s, (const float*)ob, (const float*)act,
-                       ctx->d_norm, act_buf, stride_m, ldk, ctx->S, ctx->A, ctx->M, ctx->k0_pad, B);
+                       ctx->d_norm, act_buf, stride_m, ldk, ctx->S, ctx->A, ctx->M, ctx->k0_pad, B, row_exp,
+                       stride_rexp, slot_stride, n_slots);
   } else {
-    AMX_CHECK_ARG(false, "amx_assemble_input: in_dtype=%d", in_dtype);
+    AMX_CHECK_ARG(false, "%s: in_dtype=%d", fn, in_dtype);
   }
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
 
-extern "C" int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
-                        const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
-                        float* cost_in, int ldc, uint8_t* nonfinite, int B, void* stream) {
+extern "C" int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
+                                  long long stride_m, int ldk, int B, void* stream) {
+  return assemble("amx_assemble_input", ctx, ob, act, in_dtype, act_buf, stride_m, ldk, B, nullptr, 0, 0, 0,
+                  stream);
+}
+
+extern "C" int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
+                                       long long stride_m, int ldk, int B, int* row_exp, long long strideRexp,
+                                       long long slot_stride, int n_slots, void* stream) {
+  AMX_CHECK_ARG(row_exp && n_slots >= 1 && n_slots <= 64 && slot_stride >= B &&
+                    (ctx == nullptr || ctx->M == 1 || strideRexp >= (long long)n_slots * slot_stride),
+                "amx_assemble_input_rexp: row_exp=%p n_slots=%d slot_stride=%lld strideRexp=%lld B=%d", (void*)row_exp,
+                n_slots, slot_stride, strideRexp, B);
+  return assemble("amx_assemble_input_rexp", ctx, ob, act, in_dtype, act_buf, stride_m, ldk, B, row_exp, strideRexp,
+                  slot_stride, n_slots, stream);
+}
+
+static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
+                     const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                     float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, int B, void* stream) {
   AMX_CHECK_ARG(ctx && ctx->have_term, "amx_step: context has no termination config");
   AMX_CHECK_ARG(preds && model_idx && ob && ob_next && num_steps && done, "amx_step: null pointer");
   AMX_CHECK_ARG(ldp >= ctx->S && B >= 0, "amx_step: ldp=%d B=%d", ldp, B);
@@ -554,7 +609,7 @@ extern "C" int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long str
   a.preds = preds; a.strideP = strideP; a.ldp = ldp;
   a.model_idx = model_idx; a.ob = ob; a.ob_next = ob_next;
   a.num_steps = num_steps; a.done = done; a.disc = disc;
-  a.cost_in = cost_in; a.ldc = ldc; a.nonfinite = nonfinite;
+  a.cost_in = cost_in; a.ldc = ldc; a.cost_rexp = cost_rexp; a.nonfinite = nonfinite;
   a.S = ctx->S; a.M = ctx->M; a.B = B; a.term = ctx->term;
   const int nit = (ctx->S + 63) / 64;
   switch (nit) {
@@ -567,6 +622,21 @@ extern "C" int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long str
   }
   AMX_CHECK_LAUNCH();
   return AMX_OK;
+}
+
+extern "C" int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
+                        const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                        float* cost_in, int ldc, uint8_t* nonfinite, int B, void* stream) {
+  return step_impl(ctx, preds, ldp, strideP, model_idx, ob, ob_next, num_steps, done, disc, cost_in, ldc, nullptr,
+                   nonfinite, B, stream);
+}
+
+extern "C" int amx_step_rexp(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
+                             const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                             float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, int B, void* stream) {
+  AMX_CHECK_ARG(cost_in && cost_rexp, "amx_step_rexp: cost_in and cost_rexp are required");
+  return step_impl(ctx, preds, ldp, strideP, model_idx, ob, ob_next, num_steps, done, disc, cost_in, ldc, cost_rexp,
+                   nonfinite, B, stream);
 }
 
 extern "C" int amx_disagreement(amx_ctx* ctx, const float* preds, int ldp, long long strideP, float* disc, int B,

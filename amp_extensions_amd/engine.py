@@ -125,7 +125,7 @@ class DeviceEnsemble:
 
     GEMM_PRECISIONS = ("f16x3", "bf16x6", "f32")
 
-    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "bf16x6"):
+    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "f16x3"):
         """gemm: "bf16x6" (fp32 operands split into 3 bf16 limbs, 6 limb products on the bf16
         MFMA pipe: fp32-level error, amx_gemm_*_x6), "f16x3" (power-of-two scaled operands
         split into 2 fp16 limbs, 3 products: amx_gemm_*_h3) or "f32" (v_mfma_f32_32x32x2_f32)."""
@@ -209,10 +209,15 @@ class DeviceEnsemble:
         Bp, buf, preds = ws["Bp"], ws["act"], ws["preds"]
         dt = N.AMX_IN_F64 if ob.dtype == torch.float64 else N.AMX_IN_F32
         s = c.stream
-        if not assembled:  # (the device policy can write x0 itself: amx_policy_act's fused assembly)
+        rexp = ws["rexp"]
+        if not assembled and self.W2 is not None:  # x0 + its row exponents in one pass
+            N.check(c.lib.amx_assemble_input_rexp(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
+                                                  c.ldk, B, rexp.data_ptr(), (c.L + 1) * Bp, Bp, c.L + 1, s),
+                    "amx_assemble_input_rexp")
+        elif not assembled:  # (the device policy can write x0 itself: amx_policy_act's fused assembly)
             N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
                                              c.ldk, B, s), "amx_assemble_input")
-        self._mlp(buf, preds, Bp, s, ws["rexp"])
+        self._mlp(buf, preds, Bp, s, rexp, row_exponents=assembled)
         return preds
 
     def _mlp_h3(self, buf, preds, Bp, s, rexp):
@@ -229,10 +234,10 @@ class DeviceEnsemble:
                                              c.n_out_pad, self.b[L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
                                              Bp * c.S, rexp.data_ptr(), sR, L + 1, s), "amx_gemm_out_unnorm_h3")
 
-    def _mlp(self, buf, preds, Bp, s, rexp):
+    def _mlp(self, buf, preds, Bp, s, rexp, row_exponents=True):
         c = self.ctx
         sA = Bp * c.ldk
-        if self.W2 is not None:  # x0 row exponents (slot 0) + reset of the hidden slots
+        if self.W2 is not None and row_exponents:  # x0 row exponents (slot 0) + reset of the hidden slots
             N.check(c.lib.amx_row_exponents(c.h, c.M, Bp, c.k0_pad, buf.data_ptr(), c.ldk, sA, rexp.data_ptr(),
                                             (c.L + 1) * Bp, c.L + 1, s), "amx_row_exponents")
         ev = self.gemm_events
@@ -315,8 +320,9 @@ class DeviceEnsemble:
 class RffMap:
     """phi(x) = cos(x W^T + b) * sqrt(2/F) on MFMA (linear_cost.py:64-71) with fp64 column sums."""
 
-    def __init__(self, ctx: AmxContext, W: torch.Tensor, b: torch.Tensor, gemm: str = "bf16x6"):
-        """gemm: "bf16x6" (amx_rff_features_x6 on the 3-limb image of W) or "f32"."""
+    def __init__(self, ctx: AmxContext, W: torch.Tensor, b: torch.Tensor, gemm: str = "f16x3"):
+        """gemm: "f16x3" (amx_rff_features_h3 on the scaled 2-limb image of W), "bf16x6"
+        (amx_rff_features_x6 on the 3-limb image) or "f32"."""
         if gemm not in DeviceEnsemble.GEMM_PRECISIONS:
             raise ValueError(f"gemm must be one of {DeviceEnsemble.GEMM_PRECISIONS}, got {gemm!r}")
         self.gemm = gemm
@@ -332,13 +338,32 @@ class RffMap:
         self.W = Wp.to(ctx.device).contiguous()
         self.b = b.float().to(ctx.device).contiguous()
         self.W3 = split_bf16x3(ctx, self.W.unsqueeze(0))[0] if gemm == "bf16x6" else None
+        self.W2 = self.wexp = None
+        if gemm == "f16x3":
+            W2, wexp = split_f16x2(ctx, self.W.unsqueeze(0))
+            self.W2, self.wexp = W2[0], wexp[0]
         # np.sqrt(2/F) is a float64 scalar; torch multiplies the fp32 tensor by it rounded to fp32
         self.scale = float(np.float32(np.sqrt(2 / F)))
 
     def features(self, x: torch.Tensor, rows: int, n_valid: int, phi: torch.Tensor, partials: torch.Tensor,
-                 row_mask: torch.Tensor | None = None, ldx: int | None = None) -> None:
+                 row_mask: torch.Tensor | None = None, ldx: int | None = None,
+                 row_exp: torch.Tensor | None = None) -> None:
+        """phi rows + fp64 column partials of x's `rows` rows.  f16x3: `row_exp` [rows] int32 =
+        the rows' exponents (amx_step_rexp writes them for the rollout's [s, s'] rows); None
+        computes them here (amx_row_exponents)."""
         c = self.ctx
         ldx = self.Kp if ldx is None else ldx
+        if self.W2 is not None:
+            if row_exp is None:
+                row_exp = torch.empty(rows, dtype=torch.int32, device=c.device)
+                N.check(c.lib.amx_row_exponents(c.h, 1, rows, self.Kp, x.data_ptr(), ldx, 0, row_exp.data_ptr(), rows,
+                                                1, c.stream), "amx_row_exponents")
+            N.check(c.lib.amx_rff_features_h3(c.h, rows, n_valid, self.F, self.Kp, x.data_ptr(), ldx,
+                                              self.W2.data_ptr(), self.wexp.data_ptr(), row_exp.data_ptr(),
+                                              self.b.data_ptr(), self.scale, phi.data_ptr(), phi.shape[-1],
+                                              partials.data_ptr(), None if row_mask is None else row_mask.data_ptr(),
+                                              c.stream), "amx_rff_features_h3")
+            return
         if self.W3 is not None:
             N.check(c.lib.amx_rff_features_x6(c.h, rows, n_valid, self.F, self.Kp, x.data_ptr(), ldx,
                                               self.W3.data_ptr(), self.b.data_ptr(), self.scale, phi.data_ptr(),

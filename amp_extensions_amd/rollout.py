@@ -104,6 +104,10 @@ class RolloutEngine:
             self.row_mask = ((torch.arange(K * Bp, device=dev) % Bp) < B).to(torch.uint8)
         self._scored = 0  # steps of the current rollout already scored
         self.means = z(K, B, A) if record_means else None
+        # f16x3 RFF GEMM: row exponents of the cost rows (the step kernel writes them for 'ss')
+        self.cost_rexp = None
+        if isinstance(cost, RBFLinearCost) and cost.map.W2 is not None:
+            self.cost_rexp = z(K, Bp, dt=torch.int32)
         if isinstance(cost, RBFLinearCost):
             self.phi = z(K, Bp, cost.feature_dim)
             self.partials = z(K, Bp // 128, cost.feature_dim, dt=torch.float64)
@@ -174,11 +178,18 @@ class RolloutEngine:
             self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode,
                             mean_out=None if self.means is None else self.means[t])
         preds = self.ens.forward_preds(ob, act, B)
-        N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
-                               ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
-                               self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
-                               self.cost_in[t].data_ptr() if self.cost_type == "ss" else None, self.kc,
-                               self.nonfinite[t].data_ptr(), B, s), "amx_step")
+        if self.cost_type == "ss" and self.cost_rexp is not None:
+            N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+                                        ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
+                                        self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                                        self.cost_in[t].data_ptr(), self.kc, self.cost_rexp[t].data_ptr(),
+                                        self.nonfinite[t].data_ptr(), B, s), "amx_step_rexp")
+        else:
+            N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+                                   ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
+                                   self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                                   self.cost_in[t].data_ptr() if self.cost_type == "ss" else None, self.kc,
+                                   self.nonfinite[t].data_ptr(), B, s), "amx_step")
         if self.cost is not None and self.cost_type != "ss":
             self._record_cost_input(t)
         if self.auto_reset and self.motion is not None:
@@ -236,8 +247,11 @@ class RolloutEngine:
         x = self.cost_in[t0:t1].view(rows, self.kc)
         if isinstance(cost, RBFLinearCost):
             mask = None if self.row_mask is None else self.row_mask[t0 * Bp:t1 * Bp]
+            rexp = None
+            if self.cost_rexp is not None and self.cost_type == "ss":
+                rexp = self.cost_rexp[t0:t1].view(rows)
             cost.map.features(x, rows, rows, self.phi[t0:t1].view(rows, -1),
-                              self.partials[t0:t1].view(rows // 128, -1), row_mask=mask)
+                              self.partials[t0:t1].view(rows // 128, -1), row_mask=mask, row_exp=rexp)
         elif isinstance(cost, GAILCost):
             cost.rewards_from_input(x, rows, rows, self.disc[t0:t1].view(rows) if c.M >= 2 else None,
                                     out=self.rewards[t0:t1].view(rows))

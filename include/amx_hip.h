@@ -99,6 +99,12 @@ int amx_set_termination(amx_ctx* ctx, int n_bodies, const int32_t* body_id, cons
  * in_dtype = AMX_IN_F64 (SimEnv's float64 ob, sim_env.py:155-156) or AMX_IN_F32. */
 int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
                        long long stride_m, int ldk, int B, void* stream);
+/* The same assembly for the f16x3 GEMM path: also writes slot 0 of the row exponents
+ * (row_exp[m][slot][b], slot stride slot_stride >= B, model stride strideRexp; the layout of
+ * amx_row_exponents) from max |x0| and resets slots 1..n_slots-1, for rows b < B. */
+int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
+                            long long stride_m, int ldk, int B, int* row_exp, long long strideRexp,
+                            long long slot_stride, int n_slots, void* stream);
 
 /* Grouped fp32 GEMM on MFMA with fused bias (+ReLU) epilogue: for g < groups,
  * C_g[r][col_off + n] = act(sum_k A_g[r][k] * W_g[n][k] + bias_g[n]).
@@ -180,6 +186,13 @@ int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int 
                            long long strideBias, float* preds, int ldp, long long strideP,
                            const int* row_exp, long long strideRexp, int rexp_slots, void* stream);
 
+/* f16x3 form of amx_rff_features (RBFLinearCost.get_rep, milo/milo/linear_cost.py:64-71):
+ * W2/w_exp = amx_split_f16x2 image of the [F][K] RFF weight, row_exp [rows] = exponents of x's
+ * rows (amx_step_rexp, or amx_row_exponents with one slot); same epilogue and outputs. */
+int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
+                        const uint16_t* W2, const int* w_exp, const int* row_exp, const float* b, float scale,
+                        float* phi, int ldphi, double* col_partials, const uint8_t* row_mask, void* stream);
+
 /* ---- reference-motion resets (SimEnv.reset -> DeepMimicCore reset_time, §8f #2) ----------
  * amx_set_motion: host blob (copied; amp_extensions_amd/motion.py build_blob): header[16]
  *   {J, D, F, loop, duration, -, -, -, cycle_delta xyz, ground_pad, ...}, joints [J][8]
@@ -253,6 +266,11 @@ int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, doub
 int amx_step(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
              const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
              float* cost_in, int ldc, uint8_t* nonfinite, int B, void* stream);
+/* amx_step that also writes cost_rexp[b] = the exponent of the [s, s'] cost row's max |x|
+ * (max < 2^e, clamped to [-100, 100]): the row_exp operand of amx_rff_features_h3. */
+int amx_step_rexp(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
+                  const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                  float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, int B, void* stream);
 
 /* Disagreement only (DynamicsEnsemble.get_action_discrepancy / compute_threshold,
  * milo/milo/dynamics.py:145-165). */

@@ -187,3 +187,40 @@ def test_f16x3_abi_checks():
     assert rc == -1 and b"multiple of 16" in lib.amx_last_error()
     rc = lib.amx_row_exponents(ctx.h, 1, 128, 64, buf.data_ptr(), 64, 0, we.data_ptr(), 128, 2, s)
     assert rc == -1 and b"n_slots" in lib.amx_last_error()
+
+
+def test_f16x3_rff_features_in_rollout():
+    """The rollout's RFF pass (f16x3, row exponents written by amx_step_rexp) equals the
+    same features with the exponents recomputed by amx_row_exponents bit for bit, and
+    matches phi = cos(x W^T + b) sqrt(2/F) in fp64 (linear_cost.py:64-71) to fp32 level;
+    the column partials are the fp64 sums of the phi rows."""
+    S, A, B, K = 197, 36, 256, 3
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4, gemms=("f16x3",))
+    rs = np.random.RandomState(3)
+    expert = torch.from_numpy(np.concatenate([s[:300], s[:300] + 0.01 * rs.randn(300, S)], 1)).float()
+    cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, bw_samples=5000, lambda_b=0.0025, seed=100,
+                             ctx=ctx)
+    assert cost.map.W2 is not None
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100)
+    pol = amx.DevicePolicy(ctx, pw, log_std, seed=1)
+    eng = amx.RolloutEngine(ens["f16x3"], s[:64], lanes=B, policy=pol, cost=cost, seed=2, max_steps=K)
+    eng.reset_all()
+    eng.rollout()
+    torch.cuda.synchronize()
+    rows = K * eng.Bp
+    x = eng.cost_in[:K].reshape(rows, -1)
+    phi2 = torch.empty_like(eng.phi[:K].reshape(rows, -1))
+    part2 = torch.empty_like(eng.partials[:K].reshape(rows // 128, -1))
+    cost.map.features(x, rows, rows, phi2, part2)  # exponents recomputed in a separate pass
+    torch.cuda.synchronize()
+    phi = eng.phi[:K].reshape(rows, -1)
+    assert torch.equal(phi, phi2)
+    xd = x.double().cpu().numpy()[:, :2 * S]
+    W = cost.rff_weight.double().numpy()
+    ref = np.cos(xd @ W.T + cost.rff_bias.double().numpy()) * np.sqrt(2.0 / 512)
+    # |x W^T| reaches ~1e2 here: fp32 rounding of the argument dominates (cos' <= 1)
+    arg = np.abs(xd) @ np.abs(W).T
+    err = np.abs(phi.double().cpu().numpy() - ref) / np.sqrt(2.0 / 512)
+    assert (err <= 4e-7 * arg + 1e-6).all(), float((err - 4e-7 * arg).max())
+    got = eng.partials[:K].reshape(rows // 128, -1).double().sum(0).cpu().numpy()
+    np.testing.assert_allclose(got, phi.double().cpu().numpy().sum(0), rtol=1e-9, atol=1e-9)

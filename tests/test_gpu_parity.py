@@ -43,7 +43,7 @@ def norms():
     return R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
 
 
-def make_ensemble(amx, hidden, norms, M=4, gemm="bf16x6"):
+def make_ensemble(amx, hidden, norms, M=4, gemm="f16x3"):
     ens_w = R.init_ensemble_weights(S, A, hidden, M, 100)
     ctx = amx.AmxContext(S, A, n_models=M, hidden=hidden[0], n_hidden=len(hidden), feat_dim=512, device=DEV)
     return ctx, ens_w, amx.DeviceEnsemble(ctx, ens_w, norms, gemm=gemm)
@@ -207,9 +207,9 @@ def test_reset_rows_and_model_rotation(amx, norms):
     np.testing.assert_array_equal(eng.num_steps.cpu().numpy(), np.zeros(300))
 
 
-@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
+@pytest.mark.parametrize("gemm", ["f16x3", "bf16x6", "f32"])
 def test_rff_mmd_vs_reference_golden(amx, golden, norms, gemm):
-    """Device RBFLinearCost (both feature-GEMM paths) vs the REFERENCE's outputs
+    """Device RBFLinearCost (every feature-GEMM path) vs the REFERENCE's outputs
     (bandwidth/W/b init bit-exact)."""
     g = golden("g5_rff_mmd.npz")
     es, _, es2 = synthetic_offline(512, 3)
