@@ -1112,8 +1112,15 @@ using H128x224k32 = TileH3<2, 7, 2, 1, 4, 2>;  // output layer, BK 32
 using H128x224w4k32 = TileH3<4, 1, 1, 7, 1, 2>;  // output layer, 4 waves of 32x224, BK 32
 using H128x224w4 = TileH3<4, 1, 1, 7, 2, 1>;     // output layer, 4 waves of 32x224, BK 16 (56 KB)
 using H128x224w7k32 = TileH3<1, 7, 4, 1, 2, 2>;  // output layer, 7 waves of 128x32, BK 32
+using H128x256w8k32 = TileH3<2, 4, 2, 2, 2, 2>;  // output layer on N padded to 256: 8 waves of 64x64, BK 32
+using H128x256w8 = TileH3<2, 4, 2, 2, 4, 1>;     //   same, BK 16 (61 KB: 2 WGs / CU)
+using H128x256w4k32 = TileH3<2, 2, 2, 4, 2, 2>;  //   4 waves of 64x128, BK 32
+using H128x256w8k32late = TileH3<2, 4, 2, 2, 2, 2, true>;
+using H128x224k32late = TileH3<2, 7, 2, 1, 4, 2, true>;  // output layer, 14 waves, BK 32, write-after-barrier
+using H128x256w16k32late = TileH3<4, 4, 1, 2, 4, 2, true>;  // N padded to 256: 16 waves of 32x64
 using H256w16k32 = TileH3<4, 4, 2, 2, 4, 2>;     // 256x256, 16 waves of 64x64, BK 32
 using H256w8k32late = TileH3<2, 4, 4, 2, 2, 2, true>;  // H256w8k32, write-after-barrier schedule
+using H256w16k32late = TileH3<4, 4, 2, 2, 4, 2, true>;  // H256w16k32, write-after-barrier schedule
 
 using X128 = TileX6<2, 2, 2, 2>;          // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
 using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
@@ -1598,6 +1605,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 7: if (m256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256x128k32>(a, s); break;
     case 8: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32>(a, s); break;
     case 9: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32late>(a, s); break;
+    case 11: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s); break;
     case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
     case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
     case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
@@ -1605,12 +1613,13 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 95: return launch_h3<EPI_BIAS_ACT, H256w8k32, 5>(a, s);
     default: break;
   }
-  // automatic: 256x256 with BK 32 (8 waves of 128x64, one WG per CU), write-after-barrier
-  // schedule, when its grid fills the chip -- 8-10% ahead of BK 16, 2% ahead of the
-  // write-before-barrier schedule (tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
+  // automatic: 256x256 with BK 32 (16 waves of 64x64, one WG per CU), write-after-barrier
+  // schedule, when its grid fills the chip -- 8-10% ahead of BK 16, 2-3% ahead of the
+  // write-before-barrier schedule and of 8 waves of 128x64 (tools/h3_variants.py); otherwise
+  // 128x128 (BK 32 when K allows)
   if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32late::LDS, H256w8k32late::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256w8k32late>(a, s);
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w16k32late::LDS, H256w16k32late::NT, 4))
+    return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1642,10 +1651,27 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (g_h3_out_variant == 0 || K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224w14>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 1) return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
-    return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);  // BK 32: 3% ahead
+
+    if (g_h3_out_variant == 10 && strideW2 >= 2LL * K * 256) {
+      a.N = 256;
+      return launch_h3<EPI_UNNORM, H128x256w16k32late>(a, (hipStream_t)stream);
+    }
+    if (g_h3_out_variant >= 5 && g_h3_out_variant <= 8 && strideW2 >= 2LL * K * 256) {
+      a.N = 256;  // the weight image has round_up(S, 128) = 256 rows (zero beyond S)
+      switch (g_h3_out_variant) {
+        case 5: return launch_h3<EPI_UNNORM, H128x256w8k32>(a, (hipStream_t)stream);
+        case 6: return launch_h3<EPI_UNNORM, H128x256w8>(a, (hipStream_t)stream);
+        case 7: return launch_h3<EPI_UNNORM, H128x256w4k32>(a, (hipStream_t)stream);
+        default: return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, (hipStream_t)stream);
+      }
+    }
+    // automatic: BK 32, write-after-barrier: 13% ahead of write-before-barrier and 3% ahead of
+    // 8 waves on N padded to 256 (tools/h3_variants.py)
+    return launch_h3<EPI_UNNORM, H128x224k32late>(a, (hipStream_t)stream);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);

@@ -1,8 +1,11 @@
 """Same-process A/B of GEMM tile variants on the real rollout (bench workload), interleaved
 rounds (cdna_hip_programming.md §5.4 rule 24).
 
-usage: python tools/rollout_ab.py [lanes] [variants, comma-separated; -1 = automatic]
+usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
+variant: f16x3 (default GEMM path) "h<hidden>o<output>" -> amx__set_h3_variant / amx__set_h3_out_variant
+(-1 = automatic, e.g. "h-1o-1", "h9o1"); f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
 """
+import re
 import ctypes
 import math
 import os
@@ -20,7 +23,7 @@ from amp_extensions_amd.ensemble import init_ensemble_weights  # noqa: E402
 from amp_extensions_amd.policy import init_mlp_policy_params  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
-VARIANTS = (sys.argv[2] if len(sys.argv) > 2 else "-1,-1p,0,4").split(",")
+VARIANTS = (sys.argv[2] if len(sys.argv) > 2 else "h-1o-1,h9o1").split(",")
 S, A = 197, 36
 dev = torch.device("cuda", 0)
 s, a, s2 = syn.offline(20000, S, A, 0)
@@ -40,9 +43,21 @@ _setv = lib.amx__set_gemm_variant
 _setv.argtypes = [ctypes.c_int]
 lib.amx__set_gemm_persistent.argtypes = [ctypes.c_int]
 
+lib.amx__set_h3_variant.argtypes = [ctypes.c_int]
+lib.amx__set_h3_out_variant.argtypes = [ctypes.c_int]
+
+
 def setv(v):
-    """'4' -> tile variant 4; a trailing 'p' -> persistent workgroups; 'auto'/'-1' -> automatic."""
+    """'h9o1' -> f16x3 hidden variant 9, output variant 1; '4' -> f32 tile variant 4; a trailing
+    'p' -> persistent workgroups; 'auto'/'-1' -> automatic."""
     s = str(v)
+    m = re.fullmatch(r"h(-?\d+)o(-?\d+)", s)
+    if m:
+        lib.amx__set_h3_variant(int(m.group(1)))
+        lib.amx__set_h3_out_variant(int(m.group(2)))
+        return
+    lib.amx__set_h3_variant(-1)
+    lib.amx__set_h3_out_variant(-1)
     lib.amx__set_gemm_persistent(int(s.endswith("p")))
     s = s.rstrip("p")
     _setv(-1 if s in ("auto", "-1", "") else int(s))
