@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 from . import _native as N
-from .engine import AmxContext, RffMap, round_up, split_bf16x3
+from .engine import AmxContext, RffMap, round_up, split_bf16x3, split_f16x2
 
 # cost-input row of a transition (linear_cost.py:115-127, gail_cost.py:258-268); "amp" is
 # the AMP observation of (s, s') (SceneImitateAMP::BuildAMPObs, via a ReferenceMotion)
@@ -201,10 +201,11 @@ class GAILCost:
     def __init__(self, expert_data: torch.Tensor, agent_rb=None, feature_dim: int = 1, hidden_dims=(1024, 512),
                  input_type: str = "ss", scaling_coef: float = 0.5, reg_coef: float = 0.05, lambda_b: float = 0.5,
                  seed=100, grad_lambda=10.0, disc_loss_type="least_squares", disc_opt="sgd", disc_opt_args=None,
-                 ctx: AmxContext | None = None, device="cuda", gemm: str = "bf16x6", motion=None):
+                 ctx: AmxContext | None = None, device="cuda", gemm: str = "f16x3", motion=None):
         """`motion` (a ReferenceMotion) is needed for input_type "amp" (discriminator on AMP
         observations); any disc_loss_type other than "least_squares" selects the
-        log-likelihood cost, as in the reference's get_costs (gail_cost.py:246-251)."""
+        log-likelihood cost, as in the reference's get_costs (gail_cost.py:246-251).  `gemm`:
+        the discriminator layers' GEMM ("f16x3", "bf16x6" or "f32", as DeviceEnsemble)."""
         _check_input_type(input_type, motion)
         if feature_dim != 1:
             raise ValueError("Discriminator output must be 1-D")
@@ -229,8 +230,8 @@ class GAILCost:
             S = self.input_dim // 2 if input_type == "ss" else self.input_dim
             ctx = AmxContext(S, 1, n_models=1, hidden=128, n_hidden=0, feat_dim=128, device=device)
         self.ctx = ctx
-        if gemm not in ("bf16x6", "f32"):
-            raise ValueError(f"gemm must be 'bf16x6' or 'f32', got {gemm!r}")
+        if gemm not in ("f16x3", "bf16x6", "f32"):
+            raise ValueError(f"gemm must be 'f16x3', 'bf16x6' or 'f32', got {gemm!r}")
         self.gemm = gemm
         self.load_weights(self.weights)
 
@@ -248,7 +249,12 @@ class GAILCost:
             bp = torch.zeros(out_p, dtype=torch.float32)
             bp[:out] = b.float().cpu()
             Wd = Wp.to(dev).contiguous()
-            W3 = split_bf16x3(self.ctx, Wd.unsqueeze(0))[0] if self.gemm == "bf16x6" else None
+            W3 = None
+            if self.gemm == "bf16x6":
+                W3 = split_bf16x3(self.ctx, Wd.unsqueeze(0))[0]
+            elif self.gemm == "f16x3":
+                W2, wexp = split_f16x2(self.ctx, Wd.unsqueeze(0))
+                W3 = (W2[0], wexp[0])
             self.dev_layers.append((Wd, bp.to(dev).contiguous(), out_p, k_pad, W3))
             k_in, k_pad = out, out_p
         W3, b3 = weights[-1]
@@ -259,13 +265,33 @@ class GAILCost:
         self.h_last = k_pad
         self._ws = {}
 
-    def _hidden(self, x_pad: torch.Tensor, rows: int) -> torch.Tensor:
+    def _hidden(self, x_pad: torch.Tensor, rows: int, row_exp: torch.Tensor | None = None) -> torch.Tensor:
+        """Hidden layers over `rows` padded input rows.  f16x3: `row_exp` [rows] int32 = the
+        input rows' exponents (amx_step_rexp for the rollout's [s, s'] rows; None computes them);
+        each layer's epilogue writes the exponents of its output rows for the next."""
         c = self.ctx
         ws = self._ws.get(rows)
         if ws is None:
             ws = [torch.empty(rows, L[2], dtype=torch.float32, device=c.device) for L in self.dev_layers]
+            ws.append(torch.empty(len(self.dev_layers) + 1, rows, dtype=torch.int32, device=c.device))
             self._ws[rows] = ws
         h = x_pad
+        if self.gemm == "f16x3":
+            rexp = ws[-1]
+            if row_exp is None:
+                N.check(c.lib.amx_row_exponents(c.h, 1, rows, self.Kin, h.data_ptr(), h.stride(0), 0, rexp.data_ptr(),
+                                                rows, 1, c.stream), "amx_row_exponents(disc)")
+                src = rexp[0]
+            else:
+                src = row_exp
+            rexp[1:].fill_(-100)
+            for i, ((Wp, bp, out_p, k_pad, (W2, wexp)), o) in enumerate(zip(self.dev_layers, ws)):
+                N.check(c.lib.amx_gemm_bias_act_h3(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0,
+                                                   W2.data_ptr(), 0, wexp.data_ptr(), 0, bp.data_ptr(), 0,
+                                                   o.data_ptr(), out_p, 0, 0, N.AMX_ACT_RELU, src.data_ptr(), 0, 1,
+                                                   rexp[i + 1].data_ptr(), c.stream), "amx_gemm_bias_act_h3(disc)")
+                h, src = o, rexp[i + 1]
+            return h
         for (Wp, bp, out_p, k_pad, W3), o in zip(self.dev_layers, ws):
             if W3 is not None:
                 N.check(c.lib.amx_gemm_bias_act_x6(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0,
@@ -280,10 +306,10 @@ class GAILCost:
 
     def rewards_from_input(self, x_pad: torch.Tensor, rows: int, n: int, disc: torch.Tensor | None,
                            out: torch.Tensor | None = None, logits: torch.Tensor | None = None,
-                           loss_code: int | None = None) -> torch.Tensor:
+                           loss_code: int | None = None, row_exp: torch.Tensor | None = None) -> torch.Tensor:
         """Fused discriminator + reward on already padded input rows [rows, Kin]."""
         c = self.ctx
-        h = self._hidden(x_pad, rows)
+        h = self._hidden(x_pad, rows, row_exp)
         out = torch.empty(n, dtype=torch.float32, device=c.device) if out is None else out
         N.check(c.lib.amx_disc_reward(c.h, self.loss_code if loss_code is None else loss_code, h.data_ptr(),
                                       h.stride(0), self.h_last, self.w3.data_ptr(), self.b3,

@@ -104,9 +104,11 @@ class RolloutEngine:
             self.row_mask = ((torch.arange(K * Bp, device=dev) % Bp) < B).to(torch.uint8)
         self._scored = 0  # steps of the current rollout already scored
         self.means = z(K, B, A) if record_means else None
-        # f16x3 RFF GEMM: row exponents of the cost rows (the step kernel writes them for 'ss')
+        # f16x3 RFF / discriminator GEMM: row exponents of the cost rows (the step kernel writes
+        # them for 'ss'; the other input types get them in the scoring pass)
         self.cost_rexp = None
-        if isinstance(cost, RBFLinearCost) and cost.map.W2 is not None:
+        if (isinstance(cost, RBFLinearCost) and cost.map.W2 is not None) or \
+                (isinstance(cost, GAILCost) and cost.gemm == "f16x3"):
             self.cost_rexp = z(K, Bp, dt=torch.int32)
         if isinstance(cost, RBFLinearCost):
             self.phi = z(K, Bp, cost.feature_dim)
@@ -253,8 +255,11 @@ class RolloutEngine:
             cost.map.features(x, rows, rows, self.phi[t0:t1].view(rows, -1),
                               self.partials[t0:t1].view(rows // 128, -1), row_mask=mask, row_exp=rexp)
         elif isinstance(cost, GAILCost):
+            rexp = None
+            if self.cost_rexp is not None and self.cost_type == "ss":
+                rexp = self.cost_rexp[t0:t1].view(rows)
             cost.rewards_from_input(x, rows, rows, self.disc[t0:t1].view(rows) if c.M >= 2 else None,
-                                    out=self.rewards[t0:t1].view(rows))
+                                    out=self.rewards[t0:t1].view(rows), row_exp=rexp)
         self._scored = t1
 
     # ------------------------------------------------------------------------------------

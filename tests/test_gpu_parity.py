@@ -235,7 +235,7 @@ def test_rff_mmd_vs_reference_golden(amx, golden, norms, gemm):
     np.testing.assert_allclose(float(cost.get_expert_cost()), float(g["expert_cost"]), rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("gemm", ["bf16x6", "f32"])
+@pytest.mark.parametrize("gemm", ["f16x3", "bf16x6", "f32"])
 @pytest.mark.parametrize("tag", ["h64", "h1024"])
 def test_gail_vs_reference_golden(amx, golden, norms, tag, gemm):
     g = golden(f"g6_gail_{tag}.npz")
