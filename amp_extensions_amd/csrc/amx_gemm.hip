@@ -699,9 +699,13 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // NSUB 16-k granules per K-tile (BK = 16 NSUB); LDS row = NSUB x [limb0 16 | limb1 16] + 8 pad
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
-template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false>
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true>
 struct TileH3 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
+  // AMAP (BK 32): the 16 lanes of a ds_write_b64 group stage rows r and r+2 (36-dword rows:
+  // 72 = 8 mod 32 banks apart, so their 2 x 8 dwords interleave) instead of r and r+1 (2-way
+  // bank conflict on every A limb store): 2% per layer (tools/h3_variants.py)
+  static constexpr bool AMAP = AMAP_;
   // LATE: barrier -> publish tile t+1 -> issue the loads of t+2 -> compute t (write after
   // the barrier: the LDS writes drain under the MFMAs, the loads get a whole K-tile)
   static constexpr bool LATE = LATE_;
@@ -914,7 +918,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   for (int j = 0; j < VA; ++j) {
     const int q = t + NT * j;
     a_ok[j] = (TL::NA % NT == 0 || j + 1 < VA) ? true : q < TL::NA;
-    const int r = a_ok[j] ? q / CPR : 0, c = q % CPR;
+    int r = a_ok[j] ? q / CPR : 0;
+    const int c = q % CPR;
+    if constexpr (TL::AMAP && CPR == 8)  // chunks q>>5 -> 4 rows; lanes 0-7 r, 8-15 r+2, 16-23 r+1, 24-31 r+3
+      r = a_ok[j] ? (q >> 5) * 4 + ((q >> 3) & 1) * 2 + ((q >> 4) & 1) : 0;
     a_src[j] = Ag + (long long)r * a.lda + 4 * c;
     a_dst[j] = r * LD + (c >> 2) * 32 + (c & 3) * 4;
     a_sh[j] = HSC - sExp[r];
