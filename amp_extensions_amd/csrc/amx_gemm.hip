@@ -80,6 +80,7 @@ struct GemmArgs {
   long long strideRexp;    //   between groups
   int rexp_slots;          //   slices of A read by this launch (exponent = max over them)
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
+  int abl_nostore;         // timing ablation only (h3 variant 96): skip the hidden-layer stores
 };
 
 long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
@@ -824,7 +825,7 @@ __device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc
           const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
           float v = __builtin_amdgcn_ldexpf(acc[m][n][e], er[e] + ec[n]) + bv[n];
           if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
-          Cg[(long long)row * a.ldc + a.col_off + col] = v;
+          if (!a.abl_nostore || v == 1234.5f) Cg[(long long)row * a.ldc + a.col_off + col] = v;
           const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
           mx[e] = mx[e] > b ? mx[e] : b;
         }
@@ -1618,6 +1619,8 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
     case 94: return launch_h3<EPI_BIAS_ACT, H256w8k32, 4>(a, s);
     case 95: return launch_h3<EPI_BIAS_ACT, H256w8k32, 5>(a, s);
+    case 96: a.abl_nostore = 1; return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
+    case 97: a.row_exp_out = nullptr; return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
     default: break;
   }
   // automatic: 256x256 with BK 32 (16 waves of 64x64, one WG per CU), write-after-barrier

@@ -326,6 +326,7 @@ __host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A) {
 struct PolicyArgs {
   const double* ob; const float* blob; int H1; int H2; const double* nscale; const double* noise;
   uint32_t k0, k1, ctr_lo, ctr_hi; int eval_mode;
+  const uint64_t* ctr_dev;  // nullable: the counter read from device memory (graph replays)
   double* act; float* mean_out;
   float* x0; long long stride_m; int ldk; int k0_pad; int M; const float* norm;
   int S, A, B;
@@ -473,8 +474,14 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
       } else {
         // Box-Muller on one Philox block: pair u/2 yields the normals of u = 2p, 2p+1
         const int pr = u >> 1;
+        uint32_t ctr_lo = p.ctr_lo, ctr_hi = p.ctr_hi;
+        if (p.ctr_dev) {
+          const uint64_t cv = *p.ctr_dev;
+          ctr_lo = (uint32_t)cv;
+          ctr_hi = (uint32_t)(cv >> 32);
+        }
         const amx::u32x4 r = amx::philox4x32_10(
-            {(uint32_t)b, p.ctr_lo, ((uint32_t)pr << 8) | (p.ctr_hi & 0xffu), amx::kTagPolicy}, p.k0, p.k1);
+            {(uint32_t)b, ctr_lo, ((uint32_t)pr << 8) | (ctr_hi & 0xffu), amx::kTagPolicy}, p.k0, p.k1);
         const double u1 = 1.0 - amx::u53(r.x, r.y);  // (0, 1]
         const double u2 = amx::u53(r.z, r.w);
         const double rad = sqrt(-2.0 * log(u1));
@@ -684,10 +691,10 @@ extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, i
   return AMX_OK;
 }
 
-extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
-                              const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
-                              int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
-                              void* stream) {
+static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
+                      const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
+                      const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
+                      long long stride_m, int ldk, void* stream) {
   AMX_CHECK_ARG(ctx && ob && blob && act, "amx_policy_act: null pointer");
   AMX_CHECK_ARG(amx::aligned16(blob), "amx_policy_act: blob must be 16-byte aligned");
   AMX_CHECK_ARG(eval_mode || noise_scale, "amx_policy_act: noise_scale required unless eval_mode");
@@ -704,7 +711,7 @@ extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float
   p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;
   p.nscale = noise_scale; p.noise = noise;
   p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32); p.ctr_lo = (uint32_t)counter;
-  p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode;
+  p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode; p.ctr_dev = counter_dev;
   p.act = act; p.mean_out = mean;
   p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
   p.S = ctx->S; p.A = ctx->A; p.B = B;
@@ -717,6 +724,42 @@ extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float
   else if (qh <= 2 && qa <= 3) hipLaunchKernelGGL((k_policy<2, 3>), grid, dim3(256), lds, st, p);
   else if (qh <= 4 && qa <= 4) hipLaunchKernelGGL((k_policy<4, 4>), grid, dim3(256), lds, st, p);
   else hipLaunchKernelGGL((k_policy<16, 16>), grid, dim3(256), lds, st, p);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
+                              const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
+                              int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
+                              void* stream) {
+  return policy_act(ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, counter, nullptr, eval_mode, act, mean,
+                    x0_buf, stride_m, ldk, stream);
+}
+
+extern "C" int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
+                                  const double* noise_scale, const double* noise, uint64_t seed,
+                                  const uint64_t* counter, int eval_mode, double* act, float* mean, float* x0_buf,
+                                  long long stride_m, int ldk, void* stream) {
+  AMX_CHECK_ARG(counter, "amx_policy_act_dev: null counter");
+  return policy_act(ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, 0, counter, eval_mode, act, mean, x0_buf,
+                    stride_m, ldk, stream);
+}
+
+__global__ void k_counter_add(uint64_t* c, long long d) { c[0] += (uint64_t)d; }
+
+// the GPU's constant 100 MHz realtime counter at the point the stream reaches this launch
+__global__ void k_timestamp(uint64_t* dst) { dst[0] = (uint64_t)__builtin_amdgcn_s_memrealtime(); }
+
+extern "C" int amx_timestamp(amx_ctx* ctx, uint64_t* dst, void* stream) {
+  AMX_CHECK_ARG(ctx && dst, "amx_timestamp: null pointer");
+  hipLaunchKernelGGL(k_timestamp, dim3(1), dim3(1), 0, (hipStream_t)stream, dst);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stream) {
+  AMX_CHECK_ARG(ctx && counter, "amx_counter_add: null pointer");
+  hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, delta);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

@@ -31,7 +31,6 @@ import torch
 
 from . import _native as N
 from .costs import GAILCost, RBFLinearCost, input_width
-from .dist import feature_mean
 from .engine import DeviceEnsemble, round_up
 from .humanoid import TerminationConfig
 from .policy import DevicePolicy
@@ -116,6 +115,11 @@ class RolloutEngine:
             self.phi_sum = z(cost.feature_dim, dt=torch.float64)
         self.t = 0              # steps taken in the current rollout
         self.step_counter = 0   # global step counter (policy RNG stream)
+        # the same counter on the device (the policy kernel reads it; amx_counter_add advances
+        # it after every step), so a captured HIP graph of a rollout draws fresh noise per replay
+        self.dev_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        # [sum phi (F) | count] of the rollout: the one buffer the cross-rank all-reduce touches
+        self._fbuf = z(cost.feature_dim + 1, dt=torch.float64) if isinstance(cost, RBFLinearCost) else None
         self.mb_mmd = None
 
     # ------------------------------------------------------------------------------------
@@ -178,7 +182,7 @@ class RolloutEngine:
             # (amx_policy_act can also write the ensemble's x0 rows itself, but measured slower
             # than the separate row-per-wave assembly kernel: 36.5 vs 20.4 + 8.6 us at 8192 lanes)
             self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode,
-                            mean_out=None if self.means is None else self.means[t])
+                            mean_out=None if self.means is None else self.means[t], counter_dev=self.dev_step)
         preds = self.ens.forward_preds(ob, act, B)
         if self.cost_type == "ss" and self.cost_rexp is not None:
             N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
@@ -206,6 +210,7 @@ class RolloutEngine:
             self.obs[t + 1].copy_(ob_next)
         self.t += 1
         self.step_counter += 1
+        N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), 1, s), "amx_counter_add")
         return t
 
     def _record_cost_input(self, t: int) -> None:
@@ -275,21 +280,73 @@ class RolloutEngine:
     def relabel(self, allreduce=None) -> dict:
         """Relabel the recorded transitions (batch_reinforce.py:103-169, MMD + ensemble).
         `allreduce(tensor)` sums a device tensor across ranks in place (None: one rank)."""
-        c, cost, T, B = self.ctx, self.cost, self.t, self.B
+        cost = self.cost
         self.score()
         if isinstance(cost, GAILCost):
             return {}  # rewards come from the discriminator pass
         if not isinstance(cost, RBFLinearCost):
             raise RuntimeError("relabel needs an RBFLinearCost or GAILCost")
-        phi_sum = self.feature_sum()
-        # one fused all-reduce of [sum phi, count] across ranks (dist.feature_mean); the
-        # fp64 mean is rounded to fp32 inside amx_mmd_fit (count passed as 1.0)
-        mean = feature_mean(phi_sum, float(T * B), allreduce if allreduce is not None else (lambda t: t))
-        self.mb_mmd = cost.fit_w_device(mean.contiguous(), 1.0)  # device tensor: no host sync
-        n = T * self.Bp
+        self.relabel_pre()
+        if allreduce is not None:
+            allreduce(self._fbuf)  # ONE fused all-reduce of [sum phi, count] across ranks
+        return self.relabel_post()
+
+    def relabel_pre(self) -> torch.Tensor:
+        """Rank-local half of the relabel: this rank's [sum phi | count] in the persistent
+        fp64 buffer that the cross-rank all-reduce sums (dist.feature_mean's message)."""
+        F = self.cost.feature_dim
+        self._fbuf[:F].copy_(self.feature_sum())
+        self._fbuf[F:].fill_(float(self.t * self.B))
+        return self._fbuf
+
+    def relabel_post(self) -> dict:
+        """Global half: mean -> witness w (the fp64 mean is rounded to fp32 inside amx_mmd_fit,
+        count passed as 1.0) -> per-sample rewards of every recorded transition."""
+        cost, F = self.cost, self.cost.feature_dim
+        mean = self._fbuf[:F] / self._fbuf[F]
+        self.mb_mmd = cost.fit_w_device(mean, 1.0)  # device tensor: no host sync
+        n = self.t * self.Bp
         cost.reward_launch(self.phi.data_ptr(), cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),
                            self.rewards.data_ptr(), self.ipm.data_ptr(), self.wbonus.data_ptr(), n)
         return {"mb_mmd": self.mb_mmd}
+
+    def graph_rollout(self, T: int | None = None, allreduce=None, tail=None):
+        """Capture one full rollout (K steps + scoring + relabel + `tail()`, e.g. the expert
+        cost) as HIP graph(s) on the current device and return `replay()`; replaying it is
+        equivalent to `rollout(T); relabel(allreduce); tail()` (the policy's Philox counter
+        lives on the device).  With `allreduce` (several ranks) the collective stays eager
+        between two graphs.  Run one eager rollout first (workspaces allocated, t == T)."""
+        T = self.K if T is None else T
+        if self.t != T:
+            raise RuntimeError("run one eager rollout(T) before capturing")
+        mmd = isinstance(self.cost, RBFLinearCost)
+        graphs = [torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()]
+        side = torch.cuda.Stream(self.ctx.device)
+        side.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(graphs[0], stream=side):
+                self.rollout(T)
+                if mmd:
+                    self.relabel_pre()
+                    if allreduce is None:
+                        self.relabel_post()
+                if tail is not None and (allreduce is None or not mmd):
+                    tail()
+            if mmd and allreduce is not None:
+                with torch.cuda.graph(graphs[1], stream=side):
+                    self.relabel_post()
+                    if tail is not None:
+                        tail()
+        torch.cuda.current_stream(self.ctx.device).wait_stream(side)
+        two = mmd and allreduce is not None
+
+        def replay():
+            graphs[0].replay()
+            if two:
+                allreduce(self._fbuf)
+                graphs[1].replay()
+            return T * self.B
+        return replay
 
     def advantages(self, baseline, gamma: float = 0.995, gae_lambda=0.97, whiten: bool = False,
                    eps: float = 1e-6) -> dict:

@@ -70,6 +70,9 @@ def parse():
     p.add_argument("--cpu-workers", type=int, default=0)
     p.add_argument("--cpu-samples", type=int, default=0)
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the whole rollout as one captured HIP graph (at 8192 lanes the eager launch "
+                        "path already keeps the GPU busy: same time within 1%%)")
     return p.parse_args()
 
 
@@ -184,16 +187,36 @@ def main():
         one_rollout()
     torch.cuda.synchronize()
 
+    # HIP graph: the whole rollout (steps, scoring, relabel, expert cost) is captured once and
+    # replayed, so per-kernel host launch overhead leaves the timed region (the RCCL all-reduce
+    # of N>1 runs eagerly between two graphs).  ROCm has no timing-event nodes in graphs, so
+    # the ensemble GEMM launches are bracketed by device realtime stamps (amx_timestamp,
+    # 100 MHz) captured with them; each replay's stamps are copied aside on the stream.
+    graph = None
+    if args.graph:
+        tail = cost.get_expert_cost if args.cost == "mmd" else None
+        stamps = torch.zeros(T, 2, dtype=torch.int64, device=dev)
+        ens.gemm_stamps = {"buf": stamps, "i": 0}
+        graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail)
+        ens.gemm_stamps = None
+        graph()  # warm replay
+        torch.cuda.synchronize()
+        all_stamps = torch.zeros(args.steps, T, 2, dtype=torch.int64, device=dev)
+
     # ---- timed region -----------------------------------------------------------------------
-    ens.gemm_events = []
+    ens.gemm_events = [] if graph is None else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     samples = 0
-    done_count = 0
-    for _ in range(args.steps):
-        samples += one_rollout()
+    if graph is None:
+        for _ in range(args.steps):
+            samples += one_rollout()
+    else:
+        for i in range(args.steps):
+            samples += graph()
+            all_stamps[i].copy_(stamps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -207,8 +230,13 @@ def main():
     total_samples = samples * world
 
     # dominant kernel: the ensemble GEMM launches (HIP events on the launch stream)
-    gemm_ms = sum(e0.elapsed_time(e1) for (e0, e1, _) in ens.gemm_events)
-    n_fwd = len(ens.gemm_events)
+    if graph is None:
+        gemm_ms = sum(e0.elapsed_time(e1) for (e0, e1, _) in ens.gemm_events)
+        n_fwd = len(ens.gemm_events)
+    else:
+        st = all_stamps.cpu().numpy()
+        gemm_ms = float((st[..., 1] - st[..., 0]).sum()) / 1e5  # 100 MHz ticks -> ms
+        n_fwd = args.steps * T
     launches = n_fwd * (ctx.L + 1)
     flops_per_fwd = ens.mlp_flops_per_sample() * B
     achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
@@ -253,6 +281,7 @@ def main():
                     "gail": "AMP/GAIL LS-disc reward on [s, s']",
                     "amp": "AMP LS-disc reward on AMP pose features of (s, s'), reference-motion resets"}[args.cost],
                 "samples_per_rollout_per_gpu": T * B, "lanes_per_gpu": B, "sync_steps": T,
+                "launch": "eager" if graph is None else "HIP graph replay of the whole rollout",
                 "state_dim": S, "action_dim": A, "ensemble": "4 x dense-connect [512]x4 ReLU",
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
                 "parallelism": f"dp{world} (lane-sharded, 1 all-reduce/rollout)",
@@ -266,6 +295,9 @@ def main():
                 "kernel": gi["kernel"],
                 "matrix_pipe_tflops": round(gi["products"] * achieved_tflops, 1) if gi["products"] else None,
                 "avg_launch_us": round(gemm_ms * 1e3 / max(launches, 1), 2),
+                "timing": ("HIP events around the GEMM launches" if graph is None else
+                           "device realtime stamps (amx_timestamp, 100 MHz) around the GEMM launches, captured in "
+                           "the graph (ROCm has no timing events in graphs)"),
                 "flops_per_launch": flops_per_fwd / (ctx.L + 1),
             },
             "step_flops_frac": round(value / world * step_flops / (peak * 1e12), 4),

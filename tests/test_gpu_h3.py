@@ -224,3 +224,42 @@ def test_f16x3_rff_features_in_rollout():
     assert (err <= 4e-7 * arg + 1e-6).all(), float((err - 4e-7 * arg).max())
     got = eng.partials[:K].reshape(rows // 128, -1).double().sum(0).cpu().numpy()
     np.testing.assert_allclose(got, phi.double().cpu().numpy().sum(0), rtol=1e-9, atol=1e-9)
+
+
+def test_graph_replay_matches_eager_rollouts():
+    """RolloutEngine.graph_rollout: replaying the captured rollout (steps, scoring, relabel,
+    expert cost) gives bit-identical lane states, actions, rewards and mb_mmd to the same
+    rollouts launched eagerly (the policy's Philox counter is device-resident)."""
+    S, A, B, K = 197, 36, 256, 3
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4, gemms=("f16x3",))
+    rs = np.random.RandomState(3)
+    expert = torch.from_numpy(np.concatenate([s[:300], s[:300] + 0.01 * rs.randn(300, S)], 1)).float()
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100)
+    runs = []
+    for graph in (False, True):
+        cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, bw_samples=5000, lambda_b=0.0025,
+                                 seed=100, ctx=ctx)
+        pol = amx.DevicePolicy(ctx, pw, log_std, seed=1)
+        eng = amx.RolloutEngine(ens["f16x3"], s[:64], lanes=B, policy=pol, cost=cost, seed=2, max_steps=K)
+        eng.reset_all()
+        eng.rollout()
+        eng.relabel()
+        out = []
+        if graph:
+            replay = eng.graph_rollout(K, tail=cost.get_expert_cost)
+            for _ in range(3):
+                replay()
+                out.append([x.clone() for x in (eng.obs, eng.acts, eng.rewards, eng.mb_mmd)])
+        else:
+            for _ in range(3):
+                eng.rollout()
+                eng.relabel()
+                cost.get_expert_cost()
+                out.append([x.clone() for x in (eng.obs, eng.acts, eng.rewards, eng.mb_mmd)])
+        torch.cuda.synchronize()
+        runs.append(out)
+    for ea, eb in zip(*runs):
+        for xa, xb in zip(ea, eb):
+            assert torch.equal(xa, xb)
+    # successive replays draw fresh policy noise
+    assert not torch.equal(runs[1][0][1], runs[1][1][1])
