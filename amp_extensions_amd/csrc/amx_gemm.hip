@@ -700,21 +700,29 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // NSUB 16-k granules per K-tile (BK = 16 NSUB); LDS row = NSUB x [limb0 16 | limb1 16] + 8 pad
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
-template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true>
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
+          bool M16_ = false>
 struct TileH3 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
+  // M16: v_mfma_f32_16x16x32_f16 on 16x16 blocks (BK 32; 4 fp32 accumulators per lane and
+  // block) instead of 32x32x16 -- the same cycles per FLOP at lower power per FLOP
+  // (MI355X_MICROARCH.md); LDS rows of 40 dwords (conflict-free for its lane->k map and for
+  // the plain A staging map), the row exponents live in the stage area (160 KB LDS)
+  static constexpr bool M16 = M16_;
+  static_assert(!M16 || NSUB == 2, "the 16x16x32 MFMA consumes a 32-deep K-tile");
   // AMAP (BK 32): the 16 lanes of a ds_write_b64 group stage rows r and r+2 (36-dword rows:
   // 72 = 8 mod 32 banks apart, so their 2 x 8 dwords interleave) instead of r and r+1 (2-way
   // bank conflict on every A limb store): 2% per layer (tools/h3_variants.py)
-  static constexpr bool AMAP = AMAP_;
+  static constexpr bool AMAP = AMAP_ && !M16_;
   // LATE: barrier -> publish tile t+1 -> issue the loads of t+2 -> compute t (write after
   // the barrier: the LDS writes drain under the MFMAs, the loads get a whole K-tile)
   static constexpr bool LATE = LATE_;
-  static constexpr int LD = NSUB * 32 + 8;                     // f16 per LDS row
+  static constexpr int LD = NSUB * 32 + (M16 ? 16 : 8);       // f16 per LDS row
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   static constexpr int STAGE = (BM + BN) * LD;                 // f16 of one stage (A + W)
-  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t) + BM * sizeof(int);
+  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t) + (M16 ? 0 : BM * sizeof(int));
+  static constexpr int SEXP = M16 ? STAGE : 2 * STAGE;         // f16 offset of the row exponents
   static constexpr int CPR = 4 * NSUB;                         // 16-B chunks per row and K-tile (A f32 and W)
   static constexpr int NA = BM * CPR, NW = BN * CPR;
   static constexpr int VA = (NA + NT - 1) / NT, VW = (NW + NT - 1) / NT;
@@ -871,6 +879,93 @@ __device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc
   }
 }
 
+// epilogue of the 16x16x32 form: block (m, n) of the wave holds, per lane, column n*16 + (l&15)
+// and rows m*16 + 4(l>>4) + j (j = reg); the row-exponent reduction is a reduce-scatter over
+// the 16 column lanes of the lane's MB*4 rows
+template <int EPI, class TL>
+__device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[2 * TL::TM][2 * TL::TN],
+                                                const int* sExp, int g, int tm, int tn) {
+  constexpr int MB = 2 * TL::TM, NB = 2 * TL::TN;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / TL::WN, wn = wave % TL::WN;
+  const int lc = lane & 15, lq = lane >> 4;
+  const int lrow0 = wm * TL::TM * 32;
+  const int row0 = tm * TL::BM + lrow0;
+  const int col0 = tn * TL::BN + wn * TL::TN * 32;
+  const float* bias = a.bias + (long long)g * a.strideBias;
+  const int* wexp = a.w_exp + (long long)g * a.strideWexp;
+  float* Cg = a.C + (long long)g * a.strideC;
+  if constexpr (EPI == EPI_BIAS_ACT) {
+    static_assert(MB * 4 == 16 || MB * 4 == 32, "row-exponent reduce-scatter: 16 or 32 rows per lane");
+    float bv[NB];
+    int ec[NB];
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int col = col0 + n * 16 + lc;
+      bv[n] = bias[col];
+      ec[n] = wexp[col] - 2 * HSC;
+    }
+    uint32_t mx[MB * 4];
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int4 ev = *reinterpret_cast<const int4*>(sExp + lrow0 + m * 16 + 4 * lq);
+      const int er[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mx[m * 4 + j] = 0u;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const int col = col0 + n * 16 + lc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = row0 + m * 16 + 4 * lq + j;
+          float v = __builtin_amdgcn_ldexpf(acc[m][n][j], er[j] + ec[n]) + bv[n];
+          if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
+          if (!a.abl_nostore || v == 1234.5f) Cg[(long long)row * a.ldc + a.col_off + col] = v;
+          const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
+          mx[m * 4 + j] = mx[m * 4 + j] > b ? mx[m * 4 + j] : b;
+        }
+      }
+    }
+    if (a.row_exp_out) {
+      // reduce-scatter over the 16 column lanes (bits 3..0 of lc): lane lc keeps the PER
+      // values of flat indices PER*lc .. PER*lc+PER-1 (flat index = m*4 + j)
+      constexpr int NV = MB * 4, PER = NV / 16;
+      rs_step<8, NV / 2>(mx, lc);
+      rs_step<4, NV / 4>(mx, lc);
+      rs_step<2, NV / 8>(mx, lc);
+      rs_step<1, NV / 16>(mx, lc);
+      int* out = a.row_exp_out + (long long)g * a.strideRexp;
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int i = PER * lc + u, m = i >> 2, j = i & 3;
+        atomicMax(out + row0 + m * 16 + 4 * lq + j, exp_of_bits(mx[u]));
+      }
+    }
+  } else {  // EPI_UNNORM
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const int col = col0 + n * 16 + lc;
+      if (col < a.n_valid) {
+        const float bv = bias[col];
+        const float sc = a.scale[col], sh = a.shift[col];
+        const int ec = wexp[col] - 2 * HSC;
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          const int4 ev = *reinterpret_cast<const int4*>(sExp + lrow0 + m * 16 + 4 * lq);
+          const int er[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = row0 + m * 16 + 4 * lq + j;
+            const float y = __builtin_amdgcn_ldexpf(acc[m][n][j], er[j] + ec) + bv;
+            const float prod = y * sc;    // two roundings, as torch's (y*scale)+mean
+            Cg[(long long)row * a.ldc + col] = prod + sh;
+          }
+        }
+      }
+    }
+  }
+}
+
 // ABL != 0: ablations for the timing study only (tools/h3_variants.py, variants 91..95; wrong
 // results by design): 1 every K-tile loads tile 0 (L2-hot operands), 2 no barrier in the
 // loop, 3 A staged without the split (limb1 = limb0), 4 no loads / LDS writes in the loop,
@@ -881,7 +976,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   constexpr int NT = TL::NT, STAGE = TL::STAGE;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
-  int* const sExp = reinterpret_cast<int*>(sm + 2 * STAGE);
+  int* sExp = reinterpret_cast<int*>(sm + TL::SEXP);
   int g, tm, tn;
   map_tile(a, blockIdx.x, g, tm, tn);
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
@@ -941,13 +1036,22 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
 
   f32x4 ra[VA];
   u32x4 rw[VW];
-  f32x16 acc[TM][TN];
+  constexpr int MB = 2 * TM, NB = 2 * TN;  // 16x16 blocks of the M16 form
+  using AccT = std::conditional_t<TL::M16, f32x4[MB][NB], f32x16[TM][TN]>;
+  AccT acc;
+  if constexpr (TL::M16) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < MB; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < NB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  }
 
   const int nk = a.K / BK;
   auto load = [&](int kt) {
@@ -982,7 +1086,42 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   };
   const int a_off = (wm * TM * 32 + li) * LD + lh * 8;
   const int w_off = BM * LD + (wn * TN * 32 + li) * LD + lh * 8;
+  // M16: lane l reads row l&15 of a block, k = 8(l>>4)..+7 = granule l>>5, half (l>>4)&1
+  const int koff16 = (lane >> 5) * 32 + ((lane >> 4) & 1) * 8;
+  const int a_off16 = (wm * TM * 32 + (lane & 15)) * LD + koff16;
+  const int w_off16 = BM * LD + (wn * TN * 32 + (lane & 15)) * LD + koff16;
+  auto compute16 = [&](int base) {
+    if constexpr (TL::M16) {
+    const uint16_t* As = sm + base + a_off16;
+    const uint16_t* Ws = sm + base + w_off16;
+    f16x8 gb[NB][2], ga[2][2];
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+#pragma unroll
+      for (int l = 0; l < 2; ++l) gb[n][l] = *reinterpret_cast<const f16x8*>(Ws + n * 16 * LD + l * 16);
+#pragma unroll
+    for (int l = 0; l < 2; ++l) ga[0][l] = *reinterpret_cast<const f16x8*>(As + l * 16);
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      if (m + 1 < MB) {
+#pragma unroll
+        for (int l = 0; l < 2; ++l)
+          ga[(m + 1) & 1][l] = *reinterpret_cast<const f16x8*>(As + (m + 1) * 16 * LD + l * 16);
+      }
+      constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};  // small terms first
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int n = 0; n < NB; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga[m & 1][PA[p]], gb[n][PB[p]], acc[m][n], 0, 0, 0);
+    }
+    }
+  };
   auto compute = [&](int base) {
+    if constexpr (TL::M16) {
+      compute16(base);
+      return;
+    } else {
     const uint16_t* As = sm + base + a_off;
     const uint16_t* Ws = sm + base + w_off;
     // m-outer order: the W fragments of the granule stay in registers, the A fragments of
@@ -1014,8 +1153,30 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m & 1][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
       }
     }
+    }
   };
 
+  auto finish = [&](AccT& ac) {
+    if constexpr (TL::M16) {
+      // the row exponents lived in stage buffer 1 during the prologue; re-read them into LDS
+      __syncthreads();
+      sExp = reinterpret_cast<int*>(sm);
+      const int* re = a.row_exp + (long long)g * a.strideRexp + (long long)tm * BM;
+      const long long slot = (long long)a.tiles_m * BM;
+      for (int r = t; r < BM; r += NT) {
+        int e = -100;
+        for (int s2 = 0; s2 < a.rexp_slots; ++s2) {
+          const int v = re[s2 * slot + r];
+          e = v > e ? v : e;
+        }
+        sExp[r] = e;
+      }
+      __syncthreads();
+      epilogue_h3_m16<EPI, TL>(a, ac, sExp, g, tm, tn);
+    } else {
+      epilogue_h3<EPI, TL>(a, ac, sExp, g, tm, tn);
+    }
+  };
   if constexpr (TL::LATE) {
     load(0);
     publish(0);
@@ -1028,7 +1189,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       compute(cur * STAGE);
     }
-    epilogue_h3<EPI, TL>(a, acc, sExp, g, tm, tn);
+    finish(acc);
     return;
   }
   load(0);
@@ -1042,7 +1203,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     if constexpr (ABL != 4 && ABL != 5) publish((cur ^ 1) * STAGE);
     if constexpr (ABL != 2 && ABL != 5) __syncthreads();
   }
-  epilogue_h3<EPI, TL>(a, acc, sExp, g, tm, tn);
+  finish(acc);
 }
 
 // fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
@@ -1129,6 +1290,10 @@ using H128x256w16k32late = TileH3<4, 4, 1, 2, 4, 2, true>;  // N padded to 256: 
 using H256w16k32 = TileH3<4, 4, 2, 2, 4, 2>;     // 256x256, 16 waves of 64x64, BK 32
 using H256w8k32late = TileH3<2, 4, 4, 2, 2, 2, true>;  // H256w8k32, write-after-barrier schedule
 using H256w16k32late = TileH3<4, 4, 2, 2, 4, 2, true>;  // H256w16k32, write-after-barrier schedule
+using H256w16k32lateM = TileH3<4, 4, 2, 2, 4, 2, true, true, true>;  // same on 16x16x32 MFMAs
+using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
+using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
+using H128x256w8k32lateM = TileH3<2, 4, 2, 2, 2, 2, true, true, true>;  // output on N padded to 256, 16x16x32
 
 using X128 = TileX6<2, 2, 2, 2>;          // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
 using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
@@ -1614,6 +1779,8 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 8: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32>(a, s); break;
     case 9: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32late>(a, s); break;
     case 11: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s); break;
+    case 13: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32lateM>(a, s); break;
+    case 14: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
     case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
     case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
     case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
@@ -1623,13 +1790,13 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 97: a.row_exp_out = nullptr; return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
     default: break;
   }
-  // automatic: 256x256 with BK 32 (16 waves of 64x64, one WG per CU), write-after-barrier
-  // schedule, when its grid fills the chip -- 8-10% ahead of BK 16, 2-3% ahead of the
-  // write-before-barrier schedule and of 8 waves of 128x64 (tools/h3_variants.py); otherwise
-  // 128x128 (BK 32 when K allows)
+  // automatic: 256x256 with BK 32 on 16x16x32 MFMAs (8 waves of 128x64, one WG per CU),
+  // write-after-barrier schedule, when its grid fills the chip -- 7% ahead of the same tile
+  // on 32x32x16 MFMAs with 16 waves (itself 8-10% ahead of BK 16, 2-3% ahead of the
+  // write-before-barrier schedule; tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
   if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w16k32late::LDS, H256w16k32late::NT, 4))
-    return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateM::LDS, H256w8k32lateM::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1662,10 +1829,15 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (g_h3_out_variant == 0 || K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224w14>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 1) return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 12) return launch_h3<EPI_UNNORM, H128x224k32lateM>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
 
+    if (g_h3_out_variant == 13 && strideW2 >= 2LL * K * 256) {
+      a.N = 256;
+      return launch_h3<EPI_UNNORM, H128x256w8k32lateM>(a, (hipStream_t)stream);
+    }
     if (g_h3_out_variant == 10 && strideW2 >= 2LL * K * 256) {
       a.N = 256;
       return launch_h3<EPI_UNNORM, H128x256w16k32late>(a, (hipStream_t)stream);
