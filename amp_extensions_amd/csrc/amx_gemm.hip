@@ -1857,7 +1857,17 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
-  return launch_h3<EPI_UNNORM, H128>(a, (hipStream_t)stream);
+  const hipStream_t s = (hipStream_t)stream;
+  if (K % 32 == 0) {
+    // the reference scene's S = 226 (and any N that is a multiple of 256): 128x256 tiles,
+    // 8 waves of 64x64, BK 32, write-after-barrier; other N: 128x128, BK 32
+    if (a.N % 256 == 0) {
+      if (g_h3_out_variant == 13) return launch_h3<EPI_UNNORM, H128x256w8k32lateM>(a, s);
+      return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, s);
+    }
+    return launch_h3<EPI_UNNORM, H128k32>(a, s);
+  }
+  return launch_h3<EPI_UNNORM, H128>(a, s);
 }
 
 extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,

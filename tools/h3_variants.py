@@ -25,7 +25,7 @@ from amp_extensions_amd.ensemble import init_ensemble_weights  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 HV = [int(v) for v in (sys.argv[2] if len(sys.argv) > 2 else "-1,0,1,2,3,4,5,6,7").split(",")]
 OV = [int(v) for v in (sys.argv[3] if len(sys.argv) > 3 else "-1,0").split(",")]
-S, A = 197, 36
+S, A = (int(v) for v in os.environ.get("AMX_SA", "197,36").split(","))  # AMX_SA=226,28: the scene layout
 ROUNDS, REPS = 5, 10
 
 torch.manual_seed(0)
