@@ -65,8 +65,8 @@ SIGNATURES = {
     "amx_reset_lanes": (c_int, [vp, vp, vp, c_int, vp, c_u64, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_policy_act": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, c_u64, c_int, vp, vp, vp, c_ll,
                                c_int, vp]),
-    "amx_policy_act_dev": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, vp, c_int, vp, vp, vp, c_ll,
-                                   c_int, vp]),
+    "amx_policy_act_dev": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, vp, c_u64, c_int, vp, vp, vp,
+                                   c_ll, c_int, vp]),
     "amx_counter_add": (c_int, [vp, vp, c_ll, vp]),
     "amx_timestamp": (c_int, [vp, vp, vp]),
     "amx_policy_blob_floats": (c_ll, [vp, c_int, c_int]),

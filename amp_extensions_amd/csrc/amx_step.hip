@@ -475,8 +475,8 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
         // Box-Muller on one Philox block: pair u/2 yields the normals of u = 2p, 2p+1
         const int pr = u >> 1;
         uint32_t ctr_lo = p.ctr_lo, ctr_hi = p.ctr_hi;
-        if (p.ctr_dev) {
-          const uint64_t cv = *p.ctr_dev;
+        if (p.ctr_dev) {  // device counter + the by-value offset
+          const uint64_t cv = *p.ctr_dev + ((uint64_t)p.ctr_hi << 32 | p.ctr_lo);
           ctr_lo = (uint32_t)cv;
           ctr_hi = (uint32_t)(cv >> 32);
         }
@@ -738,11 +738,11 @@ extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float
 
 extern "C" int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                                   const double* noise_scale, const double* noise, uint64_t seed,
-                                  const uint64_t* counter, int eval_mode, double* act, float* mean, float* x0_buf,
-                                  long long stride_m, int ldk, void* stream) {
+                                  const uint64_t* counter, uint64_t counter_offset, int eval_mode, double* act,
+                                  float* mean, float* x0_buf, long long stride_m, int ldk, void* stream) {
   AMX_CHECK_ARG(counter, "amx_policy_act_dev: null counter");
-  return policy_act(ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, 0, counter, eval_mode, act, mean, x0_buf,
-                    stride_m, ldk, stream);
+  return policy_act(ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, counter_offset, counter, eval_mode, act,
+                    mean, x0_buf, stride_m, ldk, stream);
 }
 
 __global__ void k_counter_add(uint64_t* c, long long d) { c[0] += (uint64_t)d; }

@@ -66,13 +66,14 @@ class DevicePolicy:
             counter_dev: torch.Tensor | None = None) -> torch.Tensor:
         """Actions of B lanes into `out` [B, A] f64.  `x0` (the ensemble workspace's activation
         buffer [M, B_pad, ldk]) fuses the ensemble's input assembly into the same launch.
-        `counter_dev` (int64 [1] on the device) replaces `counter` with a device-resident Philox
-        counter (amx_policy_act_dev: HIP-graph replays draw fresh noise)."""
+        `counter_dev` (int64 [1] on the device): the Philox counter is counter_dev[0] + `counter`
+        (amx_policy_act_dev: HIP-graph replays draw fresh noise)."""
         c = self.ctx
         if counter_dev is not None:
             N.check(c.lib.amx_policy_act_dev(
                 c.h, ob.data_ptr(), B, self.blob.data_ptr(), self.H1, self.H2, self.noise_scale.data_ptr(),
-                None if noise is None else noise.data_ptr(), self.seed, counter_dev.data_ptr(), int(eval_mode),
+                None if noise is None else noise.data_ptr(), self.seed, counter_dev.data_ptr(),
+                int(counter) & 0xFFFFFFFFFFFFFFFF, int(eval_mode),
                 out.data_ptr(), None if mean_out is None else mean_out.data_ptr(),
                 None if x0 is None else x0.data_ptr(), 0 if x0 is None else x0.stride(0),
                 0 if x0 is None else x0.stride(1), c.stream), "amx_policy_act_dev")

@@ -115,9 +115,11 @@ class RolloutEngine:
             self.phi_sum = z(cost.feature_dim, dt=torch.float64)
         self.t = 0              # steps taken in the current rollout
         self.step_counter = 0   # global step counter (policy RNG stream)
-        # the same counter on the device (the policy kernel reads it; amx_counter_add advances
-        # it after every step), so a captured HIP graph of a rollout draws fresh noise per replay
+        # graph mode: the counter of a captured rollout's step t is dev_step[0] + t, and the graph
+        # advances dev_step by T at its end, so every replay draws fresh noise
         self.dev_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._capturing = False
+        self._graph_ahead = False  # replays advanced dev_step past the host counter
         # [sum phi (F) | count] of the rollout: the one buffer the cross-rank all-reduce touches
         self._fbuf = z(cost.feature_dim + 1, dt=torch.float64) if isinstance(cost, RBFLinearCost) else None
         self.mb_mmd = None
@@ -181,8 +183,12 @@ class RolloutEngine:
                 raise RuntimeError("no policy and no actions given")
             # (amx_policy_act can also write the ensemble's x0 rows itself, but measured slower
             # than the separate row-per-wave assembly kernel: 36.5 vs 20.4 + 8.6 us at 8192 lanes)
-            self.policy.act(ob, B, act, self.step_counter, noise=noise, eval_mode=self.eval_mode,
-                            mean_out=None if self.means is None else self.means[t], counter_dev=self.dev_step)
+            if self._graph_ahead and not self._capturing:  # continue after graph replays
+                self.step_counter = int(self.dev_step.item())
+                self._graph_ahead = False
+            self.policy.act(ob, B, act, t if self._capturing else self.step_counter, noise=noise,
+                            eval_mode=self.eval_mode, mean_out=None if self.means is None else self.means[t],
+                            counter_dev=self.dev_step if self._capturing else None)
         preds = self.ens.forward_preds(ob, act, B)
         if self.cost_type == "ss" and self.cost_rexp is not None:
             N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
@@ -210,7 +216,6 @@ class RolloutEngine:
             self.obs[t + 1].copy_(ob_next)
         self.t += 1
         self.step_counter += 1
-        N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), 1, s), "amx_counter_add")
         return t
 
     def _record_cost_input(self, t: int) -> None:
@@ -320,24 +325,34 @@ class RolloutEngine:
         if self.t != T:
             raise RuntimeError("run one eager rollout(T) before capturing")
         mmd = isinstance(self.cost, RBFLinearCost)
+        c = self.ctx
+        if self._graph_ahead:
+            self.step_counter = int(self.dev_step.item())
+        self.dev_step.fill_(self.step_counter)  # the counter the next eager step would use
         graphs = [torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()]
-        side = torch.cuda.Stream(self.ctx.device)
-        side.wait_stream(torch.cuda.current_stream(self.ctx.device))
+        side = torch.cuda.Stream(c.device)
+        side.wait_stream(torch.cuda.current_stream(c.device))
         with torch.cuda.stream(side):
-            with torch.cuda.graph(graphs[0], stream=side):
-                self.rollout(T)
-                if mmd:
-                    self.relabel_pre()
-                    if allreduce is None:
-                        self.relabel_post()
-                if tail is not None and (allreduce is None or not mmd):
-                    tail()
-            if mmd and allreduce is not None:
-                with torch.cuda.graph(graphs[1], stream=side):
-                    self.relabel_post()
-                    if tail is not None:
+            self._capturing = True
+            try:
+                with torch.cuda.graph(graphs[0], stream=side):
+                    self.rollout(T)
+                    N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), T, c.stream), "amx_counter_add")
+                    if mmd:
+                        self.relabel_pre()
+                        if allreduce is None:
+                            self.relabel_post()
+                    if tail is not None and (allreduce is None or not mmd):
                         tail()
-        torch.cuda.current_stream(self.ctx.device).wait_stream(side)
+                if mmd and allreduce is not None:
+                    with torch.cuda.graph(graphs[1], stream=side):
+                        self.relabel_post()
+                        if tail is not None:
+                            tail()
+            finally:
+                self._capturing = False
+        torch.cuda.current_stream(c.device).wait_stream(side)
+        self._graph_ahead = True  # the captured steps did not run: the device counter is the truth
         two = mmd and allreduce is not None
 
         def replay():
@@ -345,6 +360,7 @@ class RolloutEngine:
             if two:
                 allreduce(self._fbuf)
                 graphs[1].replay()
+            self._graph_ahead = True
             return T * self.B
         return replay
 

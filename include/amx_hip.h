@@ -307,13 +307,13 @@ int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int
                    int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
                    void* stream);
 
-/* amx_policy_act with the Philox counter read from device memory (counter[0]) instead of
- * passed by value, so a captured HIP graph of the rollout draws fresh noise on every replay;
- * amx_counter_add(counter, delta) advances it on the stream (one thread). */
+/* amx_policy_act with the Philox counter = counter[0] (device memory) + counter_offset, so a
+ * captured HIP graph of a rollout (step t passes offset t) draws fresh noise on every replay;
+ * amx_counter_add(counter, delta) advances it on the stream (one thread, once per rollout). */
 int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                        const double* noise_scale, const double* noise, uint64_t seed,
-                       const uint64_t* counter, int eval_mode, double* act, float* mean, float* x0_buf,
-                       long long stride_m, int ldk, void* stream);
+                       const uint64_t* counter, uint64_t counter_offset, int eval_mode, double* act,
+                       float* mean, float* x0_buf, long long stride_m, int ldk, void* stream);
 int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stream);
 
 /* dst[0] = the device's 100 MHz realtime counter when the stream reaches this launch (a
