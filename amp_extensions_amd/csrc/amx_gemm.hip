@@ -81,6 +81,7 @@ struct GemmArgs {
   int rexp_slots;          //   slices of A read by this launch (exponent = max over them)
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
   int abl_nostore;         // timing ablation only (h3 variant 96): skip the hidden-layer stores
+  int prio;                // A/B only: 1 s_setprio(1) around each MFMA block, 2 static priority for waves >= NT/2
 };
 
 long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
@@ -701,7 +702,7 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
 template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
-          bool M16_ = false>
+          bool M16_ = false, int MB16_ = 0, int NB16_ = 0>
 struct TileH3 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
   // M16: v_mfma_f32_16x16x32_f16 on 16x16 blocks (BK 32; 4 fp32 accumulators per lane and
@@ -719,7 +720,11 @@ struct TileH3 {
   static constexpr bool LATE = LATE_;
   static constexpr int LD = NSUB * 32 + (M16 ? 16 : 8);       // f16 per LDS row
   static constexpr int NT = WM * WN * 64;
-  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+  // M16: MB x NB blocks of 16x16 per wave (default 2TM x 2TN; MB16_/NB16_ override, e.g. 7
+  // column blocks = 112 columns); 32x32 form: TM x TN blocks of 32x32
+  static constexpr int MB = (M16 && MB16_) ? MB16_ : 2 * TM, NB = (M16 && NB16_) ? NB16_ : 2 * TN;
+  static constexpr int WROWS = M16 ? MB * 16 : TM * 32, WCOLS = M16 ? NB * 16 : TN * 32;
+  static constexpr int BM = WM * WROWS, BN = WN * WCOLS;
   static constexpr int STAGE = (BM + BN) * LD;                 // f16 of one stage (A + W)
   static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t) + (M16 ? 0 : BM * sizeof(int));
   static constexpr int SEXP = M16 ? STAGE : 2 * STAGE;         // f16 offset of the row exponents
@@ -883,15 +888,15 @@ __device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc
 // and rows m*16 + 4(l>>4) + j (j = reg); the row-exponent reduction is a reduce-scatter over
 // the 16 column lanes of the lane's MB*4 rows
 template <int EPI, class TL>
-__device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[2 * TL::TM][2 * TL::TN],
-                                                const int* sExp, int g, int tm, int tn) {
-  constexpr int MB = 2 * TL::TM, NB = 2 * TL::TN;
+__device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[TL::MB][TL::NB], const int* sExp,
+                                                int g, int tm, int tn) {
+  constexpr int MB = TL::MB, NB = TL::NB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / TL::WN, wn = wave % TL::WN;
   const int lc = lane & 15, lq = lane >> 4;
-  const int lrow0 = wm * TL::TM * 32;
+  const int lrow0 = wm * TL::WROWS;
   const int row0 = tm * TL::BM + lrow0;
-  const int col0 = tn * TL::BN + wn * TL::TN * 32;
+  const int col0 = tn * TL::BN + wn * TL::WCOLS;
   const float* bias = a.bias + (long long)g * a.strideBias;
   const int* wexp = a.w_exp + (long long)g * a.strideWexp;
   float* Cg = a.C + (long long)g * a.strideC;
@@ -1036,7 +1041,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
 
   f32x4 ra[VA];
   u32x4 rw[VW];
-  constexpr int MB = 2 * TM, NB = 2 * TN;  // 16x16 blocks of the M16 form
+  constexpr int MB = TL::MB, NB = TL::NB;  // 16x16 blocks of the M16 form
   using AccT = std::conditional_t<TL::M16, f32x4[MB][NB], f32x16[TM][TN]>;
   AccT acc;
   if constexpr (TL::M16) {
@@ -1088,8 +1093,8 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   const int w_off = BM * LD + (wn * TN * 32 + li) * LD + lh * 8;
   // M16: lane l reads row l&15 of a block, k = 8(l>>4)..+7 = granule l>>5, half (l>>4)&1
   const int koff16 = (lane >> 5) * 32 + ((lane >> 4) & 1) * 8;
-  const int a_off16 = (wm * TM * 32 + (lane & 15)) * LD + koff16;
-  const int w_off16 = BM * LD + (wn * TN * 32 + (lane & 15)) * LD + koff16;
+  const int a_off16 = (wm * TL::WROWS + (lane & 15)) * LD + koff16;
+  const int w_off16 = BM * LD + (wn * TL::WCOLS + (lane & 15)) * LD + koff16;
   auto compute16 = [&](int base) {
     if constexpr (TL::M16) {
     const uint16_t* As = sm + base + a_off16;
@@ -1181,13 +1186,16 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     load(0);
     publish(0);
     load(1);
+    if (a.prio == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       __syncthreads();  // tile kt visible in buffer cur; buffer cur^1 (tile kt-1) fully read
       publish((cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
       load(kt + 2);
       __builtin_amdgcn_sched_barrier(0);
+      if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
       compute(cur * STAGE);
+      if (a.prio == 1) __builtin_amdgcn_s_setprio(0);
     }
     finish(acc);
     return;
@@ -1294,6 +1302,7 @@ using H256w16k32lateM = TileH3<4, 4, 2, 2, 4, 2, true, true, true>;  // same on 
 using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
 using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
 using H128x256w8k32lateM = TileH3<2, 4, 2, 2, 2, 2, true, true, true>;  // output on N padded to 256, 16x16x32
+using H128x224w8k32lateM = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 2, 7>;  // output: 8 waves of 32x112, 16x16x32
 
 using X128 = TileX6<2, 2, 2, 2>;          // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
 using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
@@ -1781,6 +1790,8 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 11: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s); break;
     case 13: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32lateM>(a, s); break;
     case 14: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
+    case 15: a.prio = 1; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
+    case 16: a.prio = 2; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
     case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
     case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
     case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
@@ -1830,6 +1841,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     if (g_h3_out_variant == 0 || K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224w14>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 1) return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 12) return launch_h3<EPI_UNNORM, H128x224k32lateM>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 14) return launch_h3<EPI_UNNORM, H128x224w8k32lateM>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
