@@ -702,8 +702,10 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
 template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
-          bool M16_ = false, int MB16_ = 0, int NB16_ = 0>
+          bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false>
 struct TileH3 {
+  // PIN: sched_barriers keep each block's fragment reads one MFMA group ahead of their use
+  static constexpr bool PIN = PIN_;
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
   // M16: v_mfma_f32_16x16x32_f16 on 16x16 blocks (BK 32; 4 fp32 accumulators per lane and
   // block) instead of 32x32x16 -- the same cycles per FLOP at lower power per FLOP
@@ -1106,6 +1108,8 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       for (int l = 0; l < 2; ++l) gb[n][l] = *reinterpret_cast<const f16x8*>(Ws + n * 16 * LD + l * 16);
 #pragma unroll
     for (int l = 0; l < 2; ++l) ga[0][l] = *reinterpret_cast<const f16x8*>(As + l * 16);
+    // the reads of block m+1 are pinned ahead of block m's MFMAs (sched_barrier): hipcc
+    // otherwise reloads one fragment register at a time and waits lgkmcnt(0) per MFMA group
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
       if (m + 1 < MB) {
@@ -1113,12 +1117,14 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
         for (int l = 0; l < 2; ++l)
           ga[(m + 1) & 1][l] = *reinterpret_cast<const f16x8*>(As + (m + 1) * 16 * LD + l * 16);
       }
+      if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
       constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};  // small terms first
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int n = 0; n < NB; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga[m & 1][PA[p]], gb[n][PB[p]], acc[m][n], 0, 0, 0);
+      if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
     }
     }
   };
@@ -1149,6 +1155,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
           for (int l = 0; l < 2; ++l)
             fa[(m + 1) & 1][l] = *reinterpret_cast<const f16x8*>(As + (m + 1) * 32 * LD + sub * 32 + l * 16);
         }
+        if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
         // small terms first: (a1,b0) (a0,b1) (a0,b0)
         constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
 #pragma unroll
@@ -1156,6 +1163,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
 #pragma unroll
           for (int n = 0; n < TN; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[m & 1][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
+        if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
       }
     }
     }
@@ -1301,6 +1309,8 @@ using H256w16k32late = TileH3<4, 4, 2, 2, 4, 2, true>;  // H256w16k32, write-aft
 using H256w16k32lateM = TileH3<4, 4, 2, 2, 4, 2, true, true, true>;  // same on 16x16x32 MFMAs
 using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
 using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
+using H256w8k32lateMP = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true>;  // + pinned fragment reads
+using H128x224k32lateP = TileH3<2, 7, 2, 1, 4, 2, true, true, false, 0, 0, true>;
 using H128x256w8k32lateM = TileH3<2, 4, 2, 2, 2, 2, true, true, true>;  // output on N padded to 256, 16x16x32
 using H128x224w8k32lateM = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 2, 7>;  // output: 8 waves of 32x112, 16x16x32
 
@@ -1792,6 +1802,9 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 14: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
     case 15: a.prio = 1; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
     case 16: a.prio = 2; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
+    case 17: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32lateM>(a, s); break;
+    case 19: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMP>(a, s); break;
+    case 18: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32late>(a, s); break;
     case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
     case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
     case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
@@ -1802,12 +1815,13 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     default: break;
   }
   // automatic: 256x256 with BK 32 on 16x16x32 MFMAs (8 waves of 128x64, one WG per CU),
-  // write-after-barrier schedule, when its grid fills the chip -- 7% ahead of the same tile
+  // write-after-barrier schedule, fragment reads pinned one MFMA group ahead (5% per rollout),
+  // when its grid fills the chip -- 7% ahead of the same tile
   // on 32x32x16 MFMAs with 16 waves (itself 8-10% ahead of BK 16, 2-3% ahead of the
   // write-before-barrier schedule; tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
   if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateM::LDS, H256w8k32lateM::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s);
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateMP::LDS, H256w8k32lateMP::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256w8k32lateMP>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1842,6 +1856,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     if (g_h3_out_variant == 1) return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 12) return launch_h3<EPI_UNNORM, H128x224k32lateM>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 14) return launch_h3<EPI_UNNORM, H128x224w8k32lateM>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 15) return launch_h3<EPI_UNNORM, H128x224k32lateP>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
