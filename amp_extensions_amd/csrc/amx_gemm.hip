@@ -1311,6 +1311,9 @@ using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
 using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
 using H256w8k32lateMP = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true>;  // + pinned fragment reads
 using H128x224k32lateP = TileH3<2, 7, 2, 1, 4, 2, true, true, false, 0, 0, true>;
+using H128k32late = TileH3<2, 2, 2, 2, 2, 2, true>;
+using H128k32lateP = TileH3<2, 2, 2, 2, 2, 2, true, true, false, 0, 0, true>;
+using H128k32P = TileH3<2, 2, 2, 2, 2, 2, false, true, false, 0, 0, true>;
 using H128x256w8k32lateM = TileH3<2, 4, 2, 2, 2, 2, true, true, true>;  // output on N padded to 256, 16x16x32
 using H128x224w8k32lateM = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 2, 7>;  // output: 8 waves of 32x112, 16x16x32
 
@@ -1693,6 +1696,7 @@ extern "C" int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, i
 namespace {
 int g_h3_variant = -1;      // amx__set_h3_variant: hidden-layer tile (-1 automatic; see the switch)
 int g_h3_out_variant = -1;  // amx__set_h3_out_variant: output-layer tile (-1 automatic, 1 BK 32)
+int g_h3_rff_variant = -1;  // amx__set_h3_rff_variant: RFF tile (-1 automatic, 1 late, 2 late+pinned, 3 pinned)
 
 template <int EPI, class TL, int ABL = 0>
 int launch_h3(GemmArgs& a, hipStream_t stream) {
@@ -1915,6 +1919,18 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.C = phi; a.ldc = ldphi;
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
-  if (K % 32 == 0) return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
+  if (K % 32 == 0) {
+    switch (g_h3_rff_variant) {
+      case 1: return launch_h3<EPI_RFF, H128k32late>(a, (hipStream_t)stream);
+      case 2: return launch_h3<EPI_RFF, H128k32lateP>(a, (hipStream_t)stream);
+      case 3: return launch_h3<EPI_RFF, H128k32P>(a, (hipStream_t)stream);
+      default: return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
+    }
+  }
   return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);
+}
+
+extern "C" int amx__set_h3_rff_variant(int v) {
+  g_h3_rff_variant = v;
+  return AMX_OK;
 }
