@@ -702,8 +702,9 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
 template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
-          bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false>
+          bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false, bool EARLY_ = false>
 struct TileH3 {
+  static constexpr bool EARLY = EARLY_ && M16_ && LATE_;  // first fragment reads before the publish
   // PIN: sched_barriers keep each block's fragment reads one MFMA group ahead of their use
   static constexpr bool PIN = PIN_;
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
@@ -1097,17 +1098,25 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   const int koff16 = (lane >> 5) * 32 + ((lane >> 4) & 1) * 8;
   const int a_off16 = (wm * TL::WROWS + (lane & 15)) * LD + koff16;
   const int w_off16 = BM * LD + (wn * TL::WCOLS + (lane & 15)) * LD + koff16;
+  f16x8 gb[NB][2], ga[2][2];
+  // the first fragments of the K-tile in buffer `base` (EARLY: issued right after the barrier,
+  // ahead of the LDS writes of the next tile, so the first MFMAs do not wait for those writes)
+  auto frag0 = [&](int base) {
+    if constexpr (TL::M16) {
+      const uint16_t* As = sm + base + a_off16;
+      const uint16_t* Ws = sm + base + w_off16;
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int l = 0; l < 2; ++l) gb[n][l] = *reinterpret_cast<const f16x8*>(Ws + n * 16 * LD + l * 16);
+#pragma unroll
+      for (int l = 0; l < 2; ++l) ga[0][l] = *reinterpret_cast<const f16x8*>(As + l * 16);
+    }
+  };
   auto compute16 = [&](int base) {
     if constexpr (TL::M16) {
     const uint16_t* As = sm + base + a_off16;
-    const uint16_t* Ws = sm + base + w_off16;
-    f16x8 gb[NB][2], ga[2][2];
-#pragma unroll
-    for (int n = 0; n < NB; ++n)
-#pragma unroll
-      for (int l = 0; l < 2; ++l) gb[n][l] = *reinterpret_cast<const f16x8*>(Ws + n * 16 * LD + l * 16);
-#pragma unroll
-    for (int l = 0; l < 2; ++l) ga[0][l] = *reinterpret_cast<const f16x8*>(As + l * 16);
+    if constexpr (!TL::EARLY) frag0(base);
     // the reads of block m+1 are pinned ahead of block m's MFMAs (sched_barrier): hipcc
     // otherwise reloads one fragment register at a time and waits lgkmcnt(0) per MFMA group
 #pragma unroll
@@ -1198,6 +1207,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       __syncthreads();  // tile kt visible in buffer cur; buffer cur^1 (tile kt-1) fully read
+      if constexpr (TL::EARLY) {
+        frag0(cur * STAGE);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       publish((cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
       load(kt + 2);
       __builtin_amdgcn_sched_barrier(0);
@@ -1310,6 +1323,9 @@ using H256w16k32lateM = TileH3<4, 4, 2, 2, 4, 2, true, true, true>;  // same on 
 using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
 using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
 using H256w8k32lateMP = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true>;  // + pinned fragment reads
+using H256w8k32lateMPE = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true>;  // + early first reads
+using H128x224k32lateMPE = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true>;  // output, 16x16x32
+using H128x256w8k32lateMPE = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true>;  // S = 226 output
 using H128x224k32lateP = TileH3<2, 7, 2, 1, 4, 2, true, true, false, 0, 0, true>;
 using H128k32late = TileH3<2, 2, 2, 2, 2, 2, true>;
 using H128k32lateP = TileH3<2, 2, 2, 2, 2, 2, true, true, false, 0, 0, true>;
@@ -1808,6 +1824,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 16: a.prio = 2; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
     case 17: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32lateM>(a, s); break;
     case 19: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMP>(a, s); break;
+    case 20: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPE>(a, s); break;
     case 18: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32late>(a, s); break;
     case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
     case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
@@ -1819,13 +1836,14 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     default: break;
   }
   // automatic: 256x256 with BK 32 on 16x16x32 MFMAs (8 waves of 128x64, one WG per CU),
-  // write-after-barrier schedule, fragment reads pinned one MFMA group ahead (5% per rollout),
+  // write-after-barrier schedule, fragment reads pinned one MFMA group ahead (5% per rollout)
+  // and the K-tile's first reads issued ahead of the next tile's LDS writes (+0.7%),
   // when its grid fills the chip -- 7% ahead of the same tile
   // on 32x32x16 MFMAs with 16 waves (itself 8-10% ahead of BK 16, 2-3% ahead of the
   // write-before-barrier schedule; tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
   if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateMP::LDS, H256w8k32lateMP::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256w8k32lateMP>(a, s);
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateMPE::LDS, H256w8k32lateMPE::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPE>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1861,6 +1879,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     if (g_h3_out_variant == 12) return launch_h3<EPI_UNNORM, H128x224k32lateM>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 14) return launch_h3<EPI_UNNORM, H128x224w8k32lateM>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 15) return launch_h3<EPI_UNNORM, H128x224k32lateP>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 16) return launch_h3<EPI_UNNORM, H128x224k32lateMPE>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
     if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
@@ -1882,9 +1901,12 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
         default: return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, (hipStream_t)stream);
       }
     }
-    // automatic: BK 32, write-after-barrier: 13% ahead of write-before-barrier and 3% ahead of
-    // 8 waves on N padded to 256 (tools/h3_variants.py)
-    return launch_h3<EPI_UNNORM, H128x224k32late>(a, (hipStream_t)stream);
+    if (g_h3_out_variant == 9) return launch_h3<EPI_UNNORM, H128x224k32late>(a, (hipStream_t)stream);
+    // automatic: BK 32, write-after-barrier, 14 waves of 64x32 on 16x16x32 MFMAs with pinned /
+    // early fragment reads: 13% ahead of write-before-barrier, 3% ahead of 8 waves on N padded
+    // to 256 and 1.4% per rollout ahead of the same tile on 32x32x16 (tools/h3_variants.py,
+    // tools/rollout_ab.py)
+    return launch_h3<EPI_UNNORM, H128x224k32lateMPE>(a, (hipStream_t)stream);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
@@ -1894,7 +1916,8 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     // 8 waves of 64x64, BK 32, write-after-barrier; other N: 128x128, BK 32
     if (a.N % 256 == 0) {
       if (g_h3_out_variant == 13) return launch_h3<EPI_UNNORM, H128x256w8k32lateM>(a, s);
-      return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, s);
+      if (g_h3_out_variant == 18) return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, s);
+      return launch_h3<EPI_UNNORM, H128x256w8k32lateMPE>(a, s);  // 16x16x32 pinned/early: 7% ahead
     }
     return launch_h3<EPI_UNNORM, H128k32>(a, s);
   }
