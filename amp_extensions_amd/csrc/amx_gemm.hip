@@ -702,9 +702,13 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
 // distinct 4-bank slots)
 template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
-          bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false, bool EARLY_ = false>
+          bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false, bool EARLY_ = false,
+          bool SPLIT_ = false>
 struct TileH3 {
   static constexpr bool EARLY = EARLY_ && M16_ && LATE_;  // first fragment reads before the publish
+  // SPLIT: the publish of tile t+1 and the loads of t+2 are cut into one piece per m-block and
+  // placed behind that block's MFMAs (the guide's split write-after-barrier schedule)
+  static constexpr bool SPLIT = SPLIT_ && EARLY;
   // PIN: sched_barriers keep each block's fragment reads one MFMA group ahead of their use
   static constexpr bool PIN = PIN_;
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
@@ -1092,6 +1096,30 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     for (int j = 0; j < VW; ++j)
       if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
   };
+  // one staging piece (SPLIT): publish A/W chunk j of the registered tile, then reload chunk j
+  // of tile kt (clamped as load())
+  auto piece = [&](int q, int base, int kt) {
+    kt = kt < nk ? kt : nk - 1;
+    if (q < VA) {
+      const int j = q;
+      if (a_ok[j]) {
+        f32x4 x = ra[j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
+        u32x2 l0, l1;
+        split2(x, l0, l1);
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+        ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
+      }
+    } else if (q < VA + VW) {
+      const int j = q - VA;
+      if (w_ok[j]) {
+        *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+        rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
+      }
+    }
+  };
   const int a_off = (wm * TM * 32 + li) * LD + lh * 8;
   const int w_off = BM * LD + (wn * TN * 32 + li) * LD + lh * 8;
   // M16: lane l reads row l&15 of a block, k = 8(l>>4)..+7 = granule l>>5, half (l>>4)&1
@@ -1113,6 +1141,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       for (int l = 0; l < 2; ++l) ga[0][l] = *reinterpret_cast<const f16x8*>(As + l * 16);
     }
   };
+  int split_base = 0, split_kt = 0;  // SPLIT: where compute16's pieces publish / what they load
   auto compute16 = [&](int base) {
     if constexpr (TL::M16) {
     const uint16_t* As = sm + base + a_off16;
@@ -1134,6 +1163,14 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
         for (int n = 0; n < NB; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga[m & 1][PA[p]], gb[n][PB[p]], acc[m][n], 0, 0, 0);
       if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (TL::SPLIT) {
+        piece(m, split_base, split_kt);
+        if (m == MB - 1) {
+#pragma unroll
+          for (int q = MB; q < VA + VW; ++q) piece(q, split_base, split_kt);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     }
   };
@@ -1210,6 +1247,12 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       if constexpr (TL::EARLY) {
         frag0(cur * STAGE);
         __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (TL::SPLIT) {  // tile kt+1's publish and tile kt+2's loads run inside compute
+        split_base = (cur ^ 1) * STAGE;
+        split_kt = kt + 2;
+        compute(cur * STAGE);
+        continue;
       }
       publish((cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
       load(kt + 2);
@@ -1324,7 +1367,10 @@ using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
 using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
 using H256w8k32lateMP = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true>;  // + pinned fragment reads
 using H256w8k32lateMPE = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true>;  // + early first reads
+using H256w8k32lateMPES = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;  // + split staging
 using H128x224k32lateMPE = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true>;  // output, 16x16x32
+using H128x224k32lateMPES = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true>;
+using H128x256w8k32lateMPES = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 using H128x256w8k32lateMPE = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true>;  // S = 226 output
 using H128x224k32lateP = TileH3<2, 7, 2, 1, 4, 2, true, true, false, 0, 0, true>;
 using H128k32late = TileH3<2, 2, 2, 2, 2, 2, true>;
@@ -1825,6 +1871,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     case 17: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32lateM>(a, s); break;
     case 19: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMP>(a, s); break;
     case 20: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPE>(a, s); break;
+    case 21: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPES>(a, s); break;
     case 18: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32late>(a, s); break;
     case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
     case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
@@ -1837,13 +1884,14 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   }
   // automatic: 256x256 with BK 32 on 16x16x32 MFMAs (8 waves of 128x64, one WG per CU),
   // write-after-barrier schedule, fragment reads pinned one MFMA group ahead (5% per rollout)
-  // and the K-tile's first reads issued ahead of the next tile's LDS writes (+0.7%),
+  // and the K-tile's first reads issued ahead of the next tile's LDS writes (+0.7%), the
+  // staging of the next tiles cut into one piece per m-block behind its MFMAs (+3.1%),
   // when its grid fills the chip -- 7% ahead of the same tile
   // on 32x32x16 MFMAs with 16 waves (itself 8-10% ahead of BK 16, 2-3% ahead of the
   // write-before-barrier schedule; tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
   if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateMPE::LDS, H256w8k32lateMPE::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPE>(a, s);
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateMPES::LDS, H256w8k32lateMPES::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPES>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1906,7 +1954,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     // early fragment reads: 13% ahead of write-before-barrier, 3% ahead of 8 waves on N padded
     // to 256 and 1.4% per rollout ahead of the same tile on 32x32x16 (tools/h3_variants.py,
     // tools/rollout_ab.py)
-    return launch_h3<EPI_UNNORM, H128x224k32lateMPE>(a, (hipStream_t)stream);
+    return launch_h3<EPI_UNNORM, H128x224k32lateMPES>(a, (hipStream_t)stream);  // + split staging: -9%
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
@@ -1917,7 +1965,8 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     if (a.N % 256 == 0) {
       if (g_h3_out_variant == 13) return launch_h3<EPI_UNNORM, H128x256w8k32lateM>(a, s);
       if (g_h3_out_variant == 18) return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, s);
-      return launch_h3<EPI_UNNORM, H128x256w8k32lateMPE>(a, s);  // 16x16x32 pinned/early: 7% ahead
+      if (g_h3_out_variant == 17) return launch_h3<EPI_UNNORM, H128x256w8k32lateMPE>(a, s);
+      return launch_h3<EPI_UNNORM, H128x256w8k32lateMPES>(a, s);  // 16x16x32 pinned/early/split: 17% ahead
     }
     return launch_h3<EPI_UNNORM, H128k32>(a, s);
   }

@@ -1,12 +1,12 @@
 """A/B the f16x3 GEMM tile variants per ensemble layer, interleaved in one process (GPU box).
 
-Hidden-layer variants (amx__set_h3_variant): -1 automatic (= 20) | 0 128x128 | 1 256x256 8 waves |
+Hidden-layer variants (amx__set_h3_variant): -1 automatic (= 21) | 0 128x128 | 1 256x256 8 waves |
 2 256x256 BK32 | 3 256x256 16 waves | 4 256x128 | 5 128x256 | 6 128x128 BK32 | 7 256x128 BK32 |
 8 256x256 BK32 16 waves | 9 = 2, write-after-barrier | 11 = 8, write-after-barrier |
-13 = 11 on 16x16x32 | 14 = 9 on 16x16x32 | 15,16 = 14 + s_setprio | 17,18 128x256 | 19 = 14, pinned reads | 20 = 19 + early first reads |
+13 = 11 on 16x16x32 | 14 = 9 on 16x16x32 | 15,16 = 14 + s_setprio | 17,18 128x256 | 19 = 14, pinned reads | 20 = 19 + early first reads | 21 = 20 + split staging |
 91..95 ablations (k_gemm_h3 ABL).
-Output layer (amx__set_h3_out_variant): -1 automatic (= 16) | 9 128x224 14 waves 32x32x16 BK 32 late |
-16 same on 16x16x32, pinned + early reads | 18 (S=226) 128x256 32x32x16 (automatic: 16x16x32 pinned + early) |
+Output layer (amx__set_h3_out_variant): -1 automatic (= 16 + split staging) | 9 128x224 14 waves 32x32x16 BK 32 late |
+16 same on 16x16x32, pinned + early reads | 17,18 (S=226) 128x256 16x16x32 pinned + early, 32x32x16 (automatic: 17 + split) |
 0 same, BK 16 | 1 BK 32 | 2,3 4 waves of 32x224 | 4 7 waves | 5-8 N padded to 256 (8 = 8 waves, late) |
 10 N 256, 16 waves.
 Every variant's output must be bit-identical to the automatic one (same k order per element).
