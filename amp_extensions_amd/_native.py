@@ -43,9 +43,9 @@ SIGNATURES = {
     "amx_split_f16x2": (c_int, [vp, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll, vp]),
     "amx_row_exponents": (c_int, [vp, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, c_int, vp]),
     "amx_gemm_bias_act_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll,
-                                     vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp, c_ll, c_int, vp, vp]),
+                                     vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp, c_ll, c_int, vp, c_int, vp]),
     "amx_gemm_out_unnorm_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll,
-                                       vp, c_ll, vp, c_int, c_ll, vp, c_ll, c_int, vp]),
+                                       vp, c_ll, vp, c_int, c_ll, vp, c_ll, c_int, c_int, vp]),
     "amx_set_motion": (c_int, [vp, vp, c_ll]),
     "amx_motion_duration": (c_dbl, [vp]),
     "amx_motion_states": (c_int, [vp, vp, c_int, c_int, vp, c_ll, vp]),

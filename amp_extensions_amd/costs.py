@@ -289,7 +289,8 @@ class GAILCost:
                 N.check(c.lib.amx_gemm_bias_act_h3(c.h, 1, rows, out_p, k_pad, h.data_ptr(), h.stride(0), 0,
                                                    W2.data_ptr(), 0, wexp.data_ptr(), 0, bp.data_ptr(), 0,
                                                    o.data_ptr(), out_p, 0, 0, N.AMX_ACT_RELU, src.data_ptr(), 0, 1,
-                                                   rexp[i + 1].data_ptr(), c.stream), "amx_gemm_bias_act_h3(disc)")
+                                                   rexp[i + 1].data_ptr(), 0, c.stream),
+                        "amx_gemm_bias_act_h3(disc)")
                 h, src = o, rexp[i + 1]
             return h
         for (Wp, bp, out_p, k_pad, W3), o in zip(self.dev_layers, ws):

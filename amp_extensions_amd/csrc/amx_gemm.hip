@@ -80,6 +80,8 @@ struct GemmArgs {
   long long strideRexp;    //   between groups
   int rexp_slots;          //   slices of A read by this launch (exponent = max over them)
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
+  int k_shared;            // leading K columns of A read from group 0's rows for every group
+                           //   (the ensemble's x0 slice, assembled once; multiple of the tile's BK)
   int abl_nostore;         // timing ablation only (h3 variant 96): skip the hidden-layer stores
   int prio;                // A/B only: 1 s_setprio(1) around each MFMA block, 2 static priority for waves >= NT/2
 };
@@ -992,6 +994,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   int g, tm, tn;
   map_tile(a, blockIdx.x, g, tm, tn);
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
+  const float* __restrict__ Ag0 = a.A + (long long)tm * BM * a.lda;  // group 0: the shared K slice
   const long long ldw2 = 2LL * a.K;
   const uint16_t* __restrict__ Wg = a.W2 + (long long)g * a.strideW2 + (long long)tn * TL::BN * ldw2;
 
@@ -1019,9 +1022,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   // staging maps: A chunk q = t + NT*j -> row q/CPR, k 4*(q%CPR); W chunk q -> row q/CPR,
   // 16-B piece q%CPR (the image's [granule][limb][16] order is the LDS row's order)
   constexpr int CPR = TL::CPR, NSUB = TL::NSUB, BK = TL::BK;
-  const float* a_src[VA];
+  int a_src[VA];  // element offsets from the tile's first row (group g, or group 0 below k_shared)
   int a_dst[VA], a_sh[VA];
   bool a_ok[VA];
+  const int nks = a.k_shared / BK;
 #pragma unroll
   for (int j = 0; j < VA; ++j) {
     const int q = t + NT * j;
@@ -1030,7 +1034,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     const int c = q % CPR;
     if constexpr (TL::AMAP && CPR == 8)  // chunks q>>5 -> 4 rows; lanes 0-7 r, 8-15 r+2, 16-23 r+1, 24-31 r+3
       r = a_ok[j] ? (q >> 5) * 4 + ((q >> 3) & 1) * 2 + ((q >> 4) & 1) : 0;
-    a_src[j] = Ag + (long long)r * a.lda + 4 * c;
+    a_src[j] = r * a.lda + 4 * c;
     a_dst[j] = r * LD + (c >> 2) * 32 + (c & 3) * 4;
     a_sh[j] = HSC - sExp[r];
   }
@@ -1069,9 +1073,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   auto load = [&](int kt) {
     kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
     if constexpr (ABL == 1) kt = 0;
+    const float* Ab = kt < nks ? Ag0 : Ag;
 #pragma unroll
     for (int j = 0; j < VA; ++j)
-      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
+      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(Ab + a_src[j] + kt * BK);
 #pragma unroll
     for (int j = 0; j < VW; ++j)
       if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
@@ -1110,7 +1115,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
         split2(x, l0, l1);
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
-        ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
+        ra[j] = *reinterpret_cast<const f32x4*>((kt < nks ? Ag0 : Ag) + a_src[j] + kt * BK);
       }
     } else if (q < VA + VW) {
       const int j = q - VA;
@@ -1774,7 +1779,7 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
 }
 
 int check_h3(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W2,
-             long long strideW2, const int* w_exp, const int* row_exp, int rexp_slots) {
+             long long strideW2, const int* w_exp, const int* row_exp, int rexp_slots, int k_shared = 0) {
   AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
   AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
                 AMX_ROW_TILE);
@@ -1783,6 +1788,8 @@ int check_h3(const char* fn, int groups, int rows, int K, const float* A, int ld
   AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
   AMX_CHECK_ARG(strideW2 % 8 == 0, "%s: strideW2=%lld must be a multiple of 8", fn, strideW2);
   AMX_CHECK_ARG(w_exp && row_exp && rexp_slots >= 1, "%s: null exponents or rexp_slots=%d", fn, rexp_slots);
+  AMX_CHECK_ARG(k_shared >= 0 && k_shared <= K && k_shared % 32 == 0,
+                "%s: k_shared=%d must be a multiple of 32 in [0, K=%d]", fn, k_shared, K);
   return AMX_OK;
 }
 }  // namespace
@@ -1831,9 +1838,11 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
                                     long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
                                     long long strideWexp, const float* bias, long long strideBias, float* C, int ldc,
                                     long long strideC, int col_off, int act, const int* row_exp,
-                                    long long strideRexp, int rexp_slots, int* row_exp_out, void* stream) {
+                                    long long strideRexp, int rexp_slots, int* row_exp_out, int k_shared,
+                                    void* stream) {
   AMX_CHECK_ARG(ctx, "amx_gemm_bias_act_h3: null ctx");
-  int rc = check_h3("amx_gemm_bias_act_h3", groups, rows, K, A, lda, W2, strideW2, w_exp, row_exp, rexp_slots);
+  int rc = check_h3("amx_gemm_bias_act_h3", groups, rows, K, A, lda, W2, strideW2, w_exp, row_exp, rexp_slots,
+                    k_shared);
   if (rc) return rc;
   AMX_CHECK_ARG(N > 0 && N % 128 == 0, "amx_gemm_bias_act_h3: N=%d must be a multiple of 128", N);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * N || groups == 1, "amx_gemm_bias_act_h3: strideW2=%lld < 2*K*N", strideW2);
@@ -1849,6 +1858,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   a.C = C; a.strideC = strideC; a.ldc = ldc; a.col_off = col_off;
   a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
   a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots; a.row_exp_out = row_exp_out;
+  a.k_shared = k_shared;
   const hipStream_t s = (hipStream_t)stream;
   const bool fit256 = rows % 256 == 0 && N % 256 == 0;
   const bool m256 = rows % 256 == 0, n256 = N % 256 == 0;
@@ -1900,9 +1910,10 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
                                       int lda, long long strideA, const uint16_t* W2, long long strideW2,
                                       const int* w_exp, long long strideWexp, const float* bias, long long strideBias,
                                       float* preds, int ldp, long long strideP, const int* row_exp,
-                                      long long strideRexp, int rexp_slots, void* stream) {
+                                      long long strideRexp, int rexp_slots, int k_shared, void* stream) {
   AMX_CHECK_ARG(ctx && ctx->have_norm, "amx_gemm_out_unnorm_h3: context has no normalizers");
-  int rc = check_h3("amx_gemm_out_unnorm_h3", groups, rows, K, A, lda, W2, strideW2, w_exp, row_exp, rexp_slots);
+  int rc = check_h3("amx_gemm_out_unnorm_h3", groups, rows, K, A, lda, W2, strideW2, w_exp, row_exp, rexp_slots,
+                    k_shared);
   if (rc) return rc;
   AMX_CHECK_ARG(n_valid == ctx->S, "amx_gemm_out_unnorm_h3: n_valid=%d must equal S=%d", n_valid, ctx->S);
   AMX_CHECK_ARG(bias && preds && ldp >= n_valid, "amx_gemm_out_unnorm_h3: null bias/preds or ldp=%d", ldp);
@@ -1913,7 +1924,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   a.C = preds; a.strideC = strideP; a.ldc = ldp;
   a.rows = rows; a.K = K; a.groups = groups;
   a.n_valid = n_valid;
-  a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots;
+  a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots; a.k_shared = k_shared;
   const int S = ctx->S, Ad = ctx->A;
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d

@@ -22,7 +22,8 @@ __device__ inline double wave_sum(double v) {
 
 // ---- assemble -----------------------------------------------------------------------
 // x0 = [(s - mu_s)/sd_s, (a - mu_a)/sd_a, 0...] into every model's activation row.
-// One wave per lane row; writes k0_pad columns for each of M models.  With row_exp (the
+// One wave per lane row; writes k0_pad columns for each of M models (once when stride_m is 0:
+// the f16x3 GEMMs then read every model's x0 slice from model 0's rows).  With row_exp (the
 // f16x3 GEMM's row-exponent slots, amx_row_exponents' layout) it also writes slot 0 = the
 // exponent of the row's max |x0| and resets slots 1..n_slots-1 for every model.
 template <typename T>
@@ -39,6 +40,7 @@ __global__ __launch_bounds__(256) void k_assemble(const T* __restrict__ ob, cons
   const float* mu_a = norm + 2 * S;
   const float* sd_a = norm + 2 * S + A;
   uint32_t mx = 0;
+  const int copies = stride_m == 0 ? 1 : M;  // stride 0: the models share one x0 slice
   for (int j = lane; j < k0_pad; j += 64) {
     float x = 0.f;
     if (j < S) {
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void k_assemble(const T* __restrict__ ob, cons
       const float v = (float)act[(long long)b * A + k];
       x = (v - mu_a[k]) / sd_a[k];
     }
-    for (int m = 0; m < M; ++m) buf[m * stride_m + (long long)b * ldk + j] = x;
+    for (int m = 0; m < copies; ++m) buf[m * stride_m + (long long)b * ldk + j] = x;
     const uint32_t bits = __float_as_uint(x) & 0x7fffffffu;
     mx = mx > bits ? mx : bits;
   }
@@ -567,7 +569,7 @@ static int assemble(const char* fn, amx_ctx* ctx, const void* ob, const void* ac
   AMX_CHECK_ARG(ob && act && act_buf, "%s: null pointer", fn);
   AMX_CHECK_ARG(B >= 0, "%s: B=%d", fn, B);
   AMX_CHECK_ARG(ldk >= ctx->k0_pad, "%s: ldk=%d < k0_pad=%d", fn, ldk, ctx->k0_pad);
-  AMX_CHECK_ARG(ctx->M == 1 || stride_m >= (long long)ldk * B, "%s: stride_m too small", fn);
+  AMX_CHECK_ARG(ctx->M == 1 || stride_m == 0 || stride_m >= (long long)ldk * B, "%s: stride_m too small", fn);
   if (B == 0) return AMX_OK;
   hipStream_t s = (hipStream_t)stream;
   if (in_dtype == AMX_IN_F64) {

@@ -132,6 +132,7 @@ class DeviceEnsemble:
         if gemm not in self.GEMM_PRECISIONS:
             raise ValueError(f"gemm must be one of {self.GEMM_PRECISIONS}, got {gemm!r}")
         self.gemm = gemm
+        self.shared_x0 = True  # f16x3: x0 assembled once, read by every member (k_shared)
         self.ctx = ctx
         S, A, M, Hp, L = ctx.S, ctx.A, ctx.M, ctx.Hp, ctx.L
         if len(weights) != M:
@@ -214,17 +215,20 @@ class DeviceEnsemble:
         dt = N.AMX_IN_F64 if ob.dtype == torch.float64 else N.AMX_IN_F32
         s = c.stream
         rexp = ws["rexp"]
+        k_shared = 0
         if not assembled and self.W2 is not None:  # x0 + its row exponents in one pass
-            N.check(c.lib.amx_assemble_input_rexp(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
-                                                  c.ldk, B, rexp.data_ptr(), (c.L + 1) * Bp, Bp, c.L + 1, s),
-                    "amx_assemble_input_rexp")
+            # shared_x0: one x0 copy (model 0's rows) that every model's GEMMs read (k_shared)
+            k_shared = c.k0_pad if self.shared_x0 else 0
+            N.check(c.lib.amx_assemble_input_rexp(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(),
+                                                  0 if k_shared else Bp * c.ldk, c.ldk, B, rexp.data_ptr(),
+                                                  (c.L + 1) * Bp, Bp, c.L + 1, s), "amx_assemble_input_rexp")
         elif not assembled:  # (the device policy can write x0 itself: amx_policy_act's fused assembly)
             N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), Bp * c.ldk,
                                              c.ldk, B, s), "amx_assemble_input")
-        self._mlp(buf, preds, Bp, s, rexp, row_exponents=assembled)
+        self._mlp(buf, preds, Bp, s, rexp, row_exponents=assembled, k_shared=k_shared)
         return preds
 
-    def _mlp_h3(self, buf, preds, Bp, s, rexp):
+    def _mlp_h3(self, buf, preds, Bp, s, rexp, k_shared=0):
         c = self.ctx
         sA, sR, L = Bp * c.ldk, (c.L + 1) * Bp, c.L
         for i in range(L):
@@ -232,13 +236,14 @@ class DeviceEnsemble:
             N.check(c.lib.amx_gemm_bias_act_h3(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),
                                                c.Hp * 2 * K, self.wexp[i].data_ptr(), c.Hp, self.b[i].data_ptr(), c.Hp,
                                                buf.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, rexp.data_ptr(), sR,
-                                               i + 1, rexp[0, i + 1].data_ptr(), s), "amx_gemm_bias_act_h3")
+                                               i + 1, rexp[0, i + 1].data_ptr(), k_shared, s), "amx_gemm_bias_act_h3")
         N.check(c.lib.amx_gemm_out_unnorm_h3(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
                                              self.W2[L].data_ptr(), c.n_out_pad * 2 * c.ldk, self.wexp[L].data_ptr(),
                                              c.n_out_pad, self.b[L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
-                                             Bp * c.S, rexp.data_ptr(), sR, L + 1, s), "amx_gemm_out_unnorm_h3")
+                                             Bp * c.S, rexp.data_ptr(), sR, L + 1, k_shared, s),
+                "amx_gemm_out_unnorm_h3")
 
-    def _mlp(self, buf, preds, Bp, s, rexp, row_exponents=True):
+    def _mlp(self, buf, preds, Bp, s, rexp, row_exponents=True, k_shared=0):
         c = self.ctx
         sA = Bp * c.ldk
         if self.W2 is not None and row_exponents:  # x0 row exponents (slot 0) + reset of the hidden slots
@@ -251,7 +256,7 @@ class DeviceEnsemble:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         if self.W2 is not None:
-            self._mlp_h3(buf, preds, Bp, s, rexp)
+            self._mlp_h3(buf, preds, Bp, s, rexp, k_shared)
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1, Bp))

@@ -101,7 +101,9 @@ int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act, int in_dty
                        long long stride_m, int ldk, int B, void* stream);
 /* The same assembly for the f16x3 GEMM path: also writes slot 0 of the row exponents
  * (row_exp[m][slot][b], slot stride slot_stride >= B, model stride strideRexp; the layout of
- * amx_row_exponents) from max |x0| and resets slots 1..n_slots-1, for rows b < B. */
+ * amx_row_exponents) from max |x0| and resets slots 1..n_slots-1, for rows b < B.
+ * stride_m = 0: x0 is written once (model 0's rows) and the f16x3 GEMMs read it for every
+ * model (their k_shared); the exponent slots are still written for every model. */
 int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
                             long long stride_m, int ldk, int B, int* row_exp, long long strideRexp,
                             long long slot_stride, int n_slots, void* stream);
@@ -168,7 +170,11 @@ int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const
  * amx_row_exponents writes slot 0 from A's first K columns and resets slots 1..n_slots-1;
  * amx_gemm_bias_act_h3 with row_exp_out (the slot of the columns it writes; nullable)
  * max-es the exponents of its output rows into it, so a dense-concat chain of layers
- * (layer i reads slots 0..i, writes slot i+1) needs no other pass.  K % 16 == 0. */
+ * (layer i reads slots 0..i, writes slot i+1) needs no other pass.  K % 16 == 0.
+ * k_shared (multiple of 32, 0 = off): A's first k_shared columns are read from group 0's rows
+ * for every group -- the ensemble's x0 slice assembled once (amx_assemble_input_rexp with
+ * stride_m = 0) instead of one copy per model; each group's row_exp slot 0 still holds its
+ * exponents. */
 int amx_split_f16x2(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw,
                     long long strideW, uint16_t* W2, long long strideW2, int* w_exp,
                     long long strideWexp, void* stream);
@@ -179,12 +185,14 @@ int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, int K, const
                          long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
                          long long strideWexp, const float* bias, long long strideBias, float* C,
                          int ldc, long long strideC, int col_off, int act, const int* row_exp,
-                         long long strideRexp, int rexp_slots, int* row_exp_out, void* stream);
+                         long long strideRexp, int rexp_slots, int* row_exp_out, int k_shared,
+                         void* stream);
 int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
                            int lda, long long strideA, const uint16_t* W2, long long strideW2,
                            const int* w_exp, long long strideWexp, const float* bias,
                            long long strideBias, float* preds, int ldp, long long strideP,
-                           const int* row_exp, long long strideRexp, int rexp_slots, void* stream);
+                           const int* row_exp, long long strideRexp, int rexp_slots, int k_shared,
+                           void* stream);
 
 /* f16x3 form of amx_rff_features (RBFLinearCost.get_rep, milo/milo/linear_cost.py:64-71):
  * W2/w_exp = amx_split_f16x2 image of the [F][K] RFF weight, row_exp [rows] = exponents of x's

@@ -61,6 +61,26 @@ def test_f16x3_ensemble_matches_oracle_and_f32(S, A, hidden, B):
     assert np.abs(p3 - p32).max() / max(1.0, np.abs(p32).max()) <= 1e-6
 
 
+@pytest.mark.parametrize("S,A,B", [(197, 36, 8192), (197, 36, 640), (226, 28, 2048)])
+def test_f16x3_shared_x0_matches_per_member_copies(S, A, B):
+    """x0 assembled once (model 0's rows, amx_assemble_input_rexp with stride_m 0) and read by
+    every member's GEMMs through k_shared gives the same bits as one x0 copy per member; the
+    other members' x0 columns are not written."""
+    amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4, gemms=("f16x3",))
+    e3 = ens["f16x3"]
+    rs = np.random.RandomState(3)
+    ob = torch.from_numpy(0.5 * rs.randn(B, S)).to(DEV)
+    ac = torch.from_numpy(rs.randn(B, A)).to(DEV)
+    e3.shared_x0 = False
+    ref = e3.forward_preds(ob, ac, B)[:, :B].clone()
+    buf = e3.workspace(B)["act"]
+    buf[1:, :, :ctx.k0_pad].fill_(float("nan"))  # stale copies must not be read
+    e3.shared_x0 = True
+    got = e3.forward_preds(ob, ac, B)[:, :B].clone()
+    assert torch.equal(got, ref)
+    assert torch.isnan(buf[1:, :B, :ctx.k0_pad]).all()
+
+
 def _f64_forward(ens_w, norms, ob, ac):
     mu_s, sd_s, mu_a, sd_a, mu_d, sd_d = [np.asarray(x, np.float64) for x in norms]
     x = np.concatenate([(ob.astype(np.float32).astype(np.float64) - mu_s) / sd_s,
@@ -163,7 +183,8 @@ def test_f16x3_split_and_row_exponent_slots():
         e = np.where(m > 0, np.frexp(m)[1], -100)
         return np.clip(e, -100, 100)
 
-    np.testing.assert_array_equal(rexp[:, 0, :B], exps(act[:, :B, :k0]))
+    x0_exp = exps(act[0, :B, :k0])  # the shared x0 slice lives in member 0's rows
+    np.testing.assert_array_equal(rexp[:, 0, :B], np.broadcast_to(x0_exp, rexp[:, 0, :B].shape))
     for i in range(ctx.L):
         np.testing.assert_array_equal(rexp[:, i + 1, :B], exps(act[:, :B, k0 + i * Hp:k0 + (i + 1) * Hp]))
 
@@ -177,12 +198,16 @@ def test_f16x3_abi_checks():
     we = torch.zeros(128, dtype=torch.int32, device=DEV)
     rc = lib.amx_gemm_bias_act_h3(ctx.h, 1, 128, 128, 64, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128,
                                   we.data_ptr(), 128, buf.data_ptr(), 0, buf.data_ptr(), 128, 0, 0, 1, None, 0, 1,
-                                  None, s)
+                                  None, 0, s)
     assert rc == -1 and b"null exponents" in lib.amx_last_error()
     rc = lib.amx_gemm_bias_act_h3(ctx.h, 1, 100, 128, 64, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128,
                                   we.data_ptr(), 128, buf.data_ptr(), 0, buf.data_ptr(), 128, 0, 0, 1, we.data_ptr(),
-                                  128, 1, None, s)
+                                  128, 1, None, 0, s)
     assert rc == -1 and b"multiple of 128" in lib.amx_last_error()
+    rc = lib.amx_gemm_bias_act_h3(ctx.h, 1, 128, 128, 64, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128,
+                                  we.data_ptr(), 128, buf.data_ptr(), 0, buf.data_ptr(), 128, 0, 0, 1, we.data_ptr(),
+                                  128, 1, None, 48, s)
+    assert rc == -1 and b"k_shared" in lib.amx_last_error()
     rc = lib.amx_split_f16x2(ctx.h, 1, 128, 40, buf.data_ptr(), 64, 0, W2.data_ptr(), 128 * 128, we.data_ptr(), 128, s)
     assert rc == -1 and b"multiple of 16" in lib.amx_last_error()
     rc = lib.amx_row_exponents(ctx.h, 1, 128, 64, buf.data_ptr(), 64, 0, we.data_ptr(), 128, 2, s)

@@ -3,7 +3,8 @@ rounds (cdna_hip_programming.md §5.4 rule 24).
 
 usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
 variant: f16x3 (default GEMM path) "h<hidden>o<output>" -> amx__set_h3_variant / amx__set_h3_out_variant
-(-1 = automatic, e.g. "h-1o-1", "h9o1"); f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
+(-1 = automatic, e.g. "h-1o-1", "h9o1"); "s0"/"s1": automatic tiles without / with the shared x0
+slice (DeviceEnsemble.shared_x0); f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
 """
 import re
 import ctypes
@@ -51,6 +52,9 @@ def setv(v):
     """'h9o1' -> f16x3 hidden variant 9, output variant 1; '4' -> f32 tile variant 4; a trailing
     'p' -> persistent workgroups; 'auto'/'-1' -> automatic."""
     s = str(v)
+    ens.shared_x0 = s != "s0"  # "s0": one x0 copy per member (no k_shared)
+    if s in ("s0", "s1"):
+        s = "h-1o-1"
     m = re.fullmatch(r"h(-?\d+)o(-?\d+)", s)
     if m:
         lib.amx__set_h3_variant(int(m.group(1)))
