@@ -993,6 +993,11 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   int* sExp = reinterpret_cast<int*>(sm + TL::SEXP);
   int g, tm, tn;
   map_tile(a, blockIdx.x, g, tm, tn);
+  long long clk0 = 0, rt0 = 0, rt1 = 0, clk1 = 0;  // clock probe (diagnostics: tools/h3_clock.py)
+  if (a.clock_probe) {
+    clk0 = (long long)__builtin_amdgcn_s_memtime();
+    rt0 = (long long)__builtin_amdgcn_s_memrealtime();
+  }
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const float* __restrict__ Ag0 = a.A + (long long)tm * BM * a.lda;  // group 0: the shared K slice
   const long long ldw2 = 2LL * a.K;
@@ -1266,7 +1271,19 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       compute(cur * STAGE);
       if (a.prio == 1) __builtin_amdgcn_s_setprio(0);
     }
+    if (a.clock_probe) {
+      clk1 = (long long)__builtin_amdgcn_s_memtime();
+      rt1 = (long long)__builtin_amdgcn_s_memrealtime();
+    }
     finish(acc);
+    if (a.clock_probe) {  // per WG: start, main-loop end, epilogue end (stores drained), loop clocks
+      __builtin_amdgcn_s_waitcnt(0);
+      const long long rt2 = (long long)__builtin_amdgcn_s_memrealtime();
+      if (threadIdx.x == 0) {
+        long long* p = a.clock_probe + 4LL * blockIdx.x;
+        p[0] = rt0; p[1] = rt1; p[2] = rt2; p[3] = clk1 - clk0;
+      }
+    }
     return;
   }
   load(0);
@@ -1418,6 +1435,7 @@ int launch_x6(GemmArgs& a, hipStream_t stream) {
   a.clock_probe = g_clock_probe;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
+  a.clock_probe = g_clock_probe;
   // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
   constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
   hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
@@ -1771,6 +1789,7 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   a.tiles_n = a.N / TL::BN;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
+  a.clock_probe = g_clock_probe;
   // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
   constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL, ABL>), dim3(nwg), dim3(TL::NT), lds, stream, a);

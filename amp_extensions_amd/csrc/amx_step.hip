@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_disagreement(const float* __restrict__ 
 // ---- step + termination -----------------------------------------------------------------
 struct StepArgs {
   const float* preds; long long strideP; int ldp;
-  const int32_t* model_idx;
+  const int32_t* model_idx; int32_t* model_idx_out;  // (model_idx_out: fused reset only)
   const double* ob; double* ob_next;
   int32_t* num_steps; uint8_t* done; float* disc;
   float* cost_in; int ldc;
@@ -148,6 +148,10 @@ struct StepArgs {
   uint8_t* nonfinite;
   int S, M, B;
   amx_termination term;
+  // fused reset (amx_step_reset; ob_out null = amx_step): done lanes restart from a table row
+  // exactly as amx_reset_lanes(mask = done), the others copy ob' from registers
+  double* ob_out; const double* table; int R; const int32_t* rows; uint32_t k0, k1;
+  int32_t* reset_count; int32_t* row_out;
 };
 
 // NIT = ceil(S/64) state elements per lane, kept in registers: all loads of the row are
@@ -249,11 +253,42 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   float d = 0.f;
   if (a.disc) d = disagreement_dispatch(a.M, a.preds, a.strideP, a.ldp, b, S, lane);
 
+  const int ns = a.num_steps[b] + 1;  // sim_env.py:153 (every lane: a broadcast load)
+  const bool horizon_done = ns >= T.horizon;  // :170
+  const bool dn = horizon_done || collided || vexp;  // wave-uniform
+  bool reset = false;
+  if (a.ob_out) {  // the next step's observation (amx_reset_lanes with mask = done)
+    double* oo = a.ob_out + (long long)b * S;
+    if (!dn) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int j = lane + 64 * it;
+        if (j < S) oo[j] = x[it];
+      }
+      if (lane == 0 && a.row_out) a.row_out[b] = -1;
+    } else {
+      reset = true;
+      const int rc = a.reset_count[b] + 1;  // sim_env.py:282
+      int row;
+      if (a.rows) {
+        row = a.rows[b];
+      } else {
+        const amx::u32x4 r = amx::philox4x32_10({(uint32_t)b, (uint32_t)rc, 0u, amx::kTagReset}, a.k0, a.k1);
+        row = (int)((((uint64_t)r.y << 32) | r.x) % (uint64_t)a.R);
+      }
+      const double* src = a.table + (long long)row * S;
+      for (int j = lane; j < S; j += 64) oo[j] = src[j];
+      if (lane == 0) {
+        a.reset_count[b] = rc;
+        a.model_idx_out[b] = rc % a.M;  // :282-283
+        if (a.row_out) a.row_out[b] = row;
+      }
+    }
+  }
+
   if (lane == 0) {
-    const int ns = a.num_steps[b] + 1;  // sim_env.py:153
-    a.num_steps[b] = ns;
-    const bool horizon_done = ns >= T.horizon;  // :170
-    a.done[b] = (horizon_done || collided || vexp) ? 1 : 0;
+    a.num_steps[b] = reset ? 0 : ns;  // a reset restarts the episode counter (:277)
+    a.done[b] = dn ? 1 : 0;
     if (a.disc) a.disc[b] = d;
     if (a.nonfinite) a.nonfinite[b] = nf ? 1 : 0;
   }
@@ -604,9 +639,15 @@ extern "C" int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void*
                   slot_stride, n_slots, stream);
 }
 
+struct ResetArgs {  // amx_step_reset's reset half (amx_reset_lanes' arguments)
+  const double* table; int R; const int32_t* rows; uint64_t seed; double* ob_out; int32_t* model_idx;
+  int32_t* reset_count; int32_t* row_out;
+};
+
 static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
                      const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
-                     float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, int B, void* stream) {
+                     float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, int B, void* stream,
+                     const ResetArgs* rs = nullptr) {
   AMX_CHECK_ARG(ctx && ctx->have_term, "amx_step: context has no termination config");
   AMX_CHECK_ARG(preds && model_idx && ob && ob_next && num_steps && done, "amx_step: null pointer");
   AMX_CHECK_ARG(ldp >= ctx->S && B >= 0, "amx_step: ldp=%d B=%d", ldp, B);
@@ -620,6 +661,17 @@ static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long stride
   a.num_steps = num_steps; a.done = done; a.disc = disc;
   a.cost_in = cost_in; a.ldc = ldc; a.cost_rexp = cost_rexp; a.nonfinite = nonfinite;
   a.S = ctx->S; a.M = ctx->M; a.B = B; a.term = ctx->term;
+  a.model_idx_out = nullptr; a.ob_out = nullptr; a.table = nullptr; a.R = 0; a.rows = nullptr; a.k0 = a.k1 = 0;
+  a.reset_count = nullptr; a.row_out = nullptr;
+  if (rs) {
+    AMX_CHECK_ARG(rs->table && rs->ob_out && rs->model_idx && rs->reset_count && rs->R > 0,
+                  "amx_step_reset: null reset pointer or R=%d", rs->R);
+    AMX_CHECK_ARG(rs->ob_out != ob && rs->ob_out != ob_next && (const int32_t*)rs->model_idx == model_idx,
+                  "amx_step_reset: ob_out must be a third buffer and model_idx the step's");
+    a.model_idx_out = rs->model_idx; a.ob_out = rs->ob_out; a.table = rs->table; a.R = rs->R; a.rows = rs->rows;
+    a.k0 = (uint32_t)rs->seed; a.k1 = (uint32_t)(rs->seed >> 32);
+    a.reset_count = rs->reset_count; a.row_out = rs->row_out;
+  }
   const int nit = (ctx->S + 63) / 64;
   switch (nit) {
 #define AMX_STEP_CASE(N) \
@@ -646,6 +698,17 @@ extern "C" int amx_step_rexp(amx_ctx* ctx, const float* preds, int ldp, long lon
   AMX_CHECK_ARG(cost_in && cost_rexp, "amx_step_rexp: cost_in and cost_rexp are required");
   return step_impl(ctx, preds, ldp, strideP, model_idx, ob, ob_next, num_steps, done, disc, cost_in, ldc, cost_rexp,
                    nonfinite, B, stream);
+}
+
+extern "C" int amx_step_reset(amx_ctx* ctx, const float* preds, int ldp, long long strideP, int32_t* model_idx,
+                              const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                              float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, const double* table,
+                              int R, const int32_t* rows, uint64_t seed, double* ob_out, int32_t* reset_count,
+                              int32_t* row_out, int B, void* stream) {
+  AMX_CHECK_ARG(!cost_rexp || cost_in, "amx_step_reset: cost_rexp needs cost_in");
+  const ResetArgs rs = {table, R, rows, seed, ob_out, model_idx, reset_count, row_out};
+  return step_impl(ctx, preds, ldp, strideP, model_idx, ob, ob_next, num_steps, done, disc, cost_in, ldc, cost_rexp,
+                   nonfinite, B, stream, &rs);
 }
 
 extern "C" int amx_disagreement(amx_ctx* ctx, const float* preds, int ldp, long long strideP, float* disc, int B,

@@ -51,6 +51,7 @@ class RolloutEngine:
         self.cost = cost
         self.eval_mode = eval_mode
         self.auto_reset = auto_reset
+        self.fuse_reset = True  # table resets run inside the step kernel (amx_step_reset)
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
         from .motion import ReferenceMotion
@@ -190,7 +191,19 @@ class RolloutEngine:
                             eval_mode=self.eval_mode, mean_out=None if self.means is None else self.means[t],
                             counter_dev=self.dev_step if self._capturing else None)
         preds = self.ens.forward_preds(ob, act, B)
-        if self.cost_type == "ss" and self.cost_rexp is not None:
+        fused = self.auto_reset and self.motion is None and self.fuse_reset
+        if fused:  # step + table reset in one pass (amx_step_reset)
+            ss = self.cost_type == "ss"
+            N.check(c.lib.amx_step_reset(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+                                         ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
+                                         self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                                         self.cost_in[t].data_ptr() if ss else None, self.kc,
+                                         self.cost_rexp[t].data_ptr() if ss and self.cost_rexp is not None else None,
+                                         self.nonfinite[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
+                                         None if reset_rows is None else reset_rows.data_ptr(), self.seed,
+                                         self.obs[t + 1].data_ptr(), self.reset_count.data_ptr(),
+                                         self.reset_rows[t].data_ptr(), B, s), "amx_step_reset")
+        elif self.cost_type == "ss" and self.cost_rexp is not None:
             N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                         ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
                                         self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
@@ -204,7 +217,9 @@ class RolloutEngine:
                                    self.nonfinite[t].data_ptr(), B, s), "amx_step")
         if self.cost is not None and self.cost_type != "ss":
             self._record_cost_input(t)
-        if self.auto_reset and self.motion is not None:
+        if fused:
+            pass
+        elif self.auto_reset and self.motion is not None:
             self._reset_motion(self.done[t], reset_rows, ob_next, self.obs[t + 1], self.reset_times[t])
         elif self.auto_reset:
             N.check(c.lib.amx_reset_lanes(c.h, self.done[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],

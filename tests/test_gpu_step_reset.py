@@ -1,0 +1,64 @@
+"""amx_step_reset: the step kernel with the table reset of done lanes fused in (RolloutEngine's
+default) against amx_step / amx_step_rexp followed by amx_reset_lanes(mask = done) — every
+lane buffer bit-identical over rollouts with horizon and fall resets (sim_env.py:150-285)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import milo_ref as R
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _engines(cost_kind):
+    import amp_extensions_amd as amx
+    from amp_extensions_amd.humanoid import TerminationConfig
+    S, A, B = 197, 36, 320
+    rs = np.random.RandomState(0)
+    s = 0.5 * rs.randn(2048, S)
+    s[:, 0] = rs.uniform(0.8, 0.95, 2048)
+    a = rs.randn(2048, A)
+    s2 = s + 0.01 * rs.randn(2048, S)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
+    ctx = amx.AmxContext(S, A, n_models=4, hidden=512, n_hidden=4, feat_dim=512, device=DEV)
+    ctx.set_termination(TerminationConfig(horizon=3))  # horizon resets every third step
+    ens = amx.DeviceEnsemble(ctx, R.init_ensemble_weights(S, A, [512] * 4, 4, 100), norms)
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100)
+    expert = torch.from_numpy(np.concatenate([s[:300], s2[:300]], 1)).float()
+    out = []
+    for fused in (False, True):
+        if cost_kind == "mmd":
+            cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, bw_samples=5000, lambda_b=0.0025,
+                                     seed=100, ctx=ctx)
+        elif cost_kind == "gail":
+            cost = amx.GAILCost(expert, hidden_dims=[256, 128], lambda_b=0.4, seed=100, ctx=ctx)
+        else:
+            cost = None
+        pol = amx.DevicePolicy(ctx, pw, log_std, seed=1)
+        eng = amx.RolloutEngine(ens, s[:97], lanes=B, policy=pol, cost=cost, seed=2, max_steps=8)
+        eng.fuse_reset = fused
+        out.append(eng)
+    return out
+
+
+@pytest.mark.parametrize("cost_kind", ["mmd", "gail", "none"])
+def test_fused_step_reset_matches_step_then_reset(cost_kind):
+    engs = _engines(cost_kind)
+    for eng in engs:
+        eng.reset_all()
+        for _ in range(2):
+            eng.rollout()
+    torch.cuda.synchronize()
+    ref, got = engs
+    names = ["obs", "next_obs", "acts", "done", "disc", "num_steps", "model_idx", "reset_count", "reset_rows",
+             "nonfinite", "cost_in", "cost_rexp"]
+    for n in names:
+        x, y = getattr(ref, n), getattr(got, n)
+        if x is None:
+            assert y is None
+            continue
+        assert torch.equal(x, y), n
+    done = ref.done.bool()
+    assert done.any() and not done.all()  # both branches ran
+    assert (ref.reset_rows[done[:, :ref.B]] >= 0).all()

@@ -35,13 +35,13 @@ def run(layer, reps):
                                                e.W2[layer].data_ptr(), c.Hp * 2 * K, e.wexp[layer].data_ptr(), c.Hp,
                                                e.b[layer].data_ptr(), c.Hp, out.data_ptr(), c.ldk, sA, K,
                                                N.AMX_ACT_RELU, rexp.data_ptr(), sR, layer + 1,
-                                               scratch[0, layer + 1].data_ptr(), 0, c.stream), "h3")
+                                               scratch[0, layer + 1].data_ptr(), c.k0_pad, c.stream), "h3")
         else:
             N.check(c.lib.amx_gemm_out_unnorm_h3(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
                                                  e.W2[c.L].data_ptr(), c.n_out_pad * 2 * c.ldk,
                                                  e.wexp[c.L].data_ptr(), c.n_out_pad, e.b[c.L].data_ptr(),
                                                  c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, rexp.data_ptr(), sR,
-                                                 c.L + 1, 0, c.stream), "h3 out")
+                                                 c.L + 1, c.k0_pad, c.stream), "h3 out")
     torch.cuda.synchronize()
 
 

@@ -56,12 +56,12 @@ def layer(i):
         N.check(lib.amx_gemm_bias_act_h3(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, e.W2[i].data_ptr(),
                                          c.Hp * 2 * K, e.wexp[i].data_ptr(), c.Hp, e.b[i].data_ptr(), c.Hp,
                                          out.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, rexp.data_ptr(), sR, i + 1,
-                                         scratch[0, i + 1].data_ptr(), 0, s), "h3")
+                                         scratch[0, i + 1].data_ptr(), c.k0_pad, s), "h3")
     else:
         N.check(lib.amx_gemm_out_unnorm_h3(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA, e.W2[c.L].data_ptr(),
                                            c.n_out_pad * 2 * c.ldk, e.wexp[c.L].data_ptr(), c.n_out_pad,
                                            e.b[c.L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S,
-                                           rexp.data_ptr(), sR, c.L + 1, 0, s), "h3 out")
+                                           rexp.data_ptr(), sR, c.L + 1, c.k0_pad, s), "h3 out")
 
 
 def result(i):

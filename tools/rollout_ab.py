@@ -4,7 +4,7 @@ rounds (cdna_hip_programming.md §5.4 rule 24).
 usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
 variant: f16x3 (default GEMM path) "h<hidden>o<output>" -> amx__set_h3_variant / amx__set_h3_out_variant
 (-1 = automatic, e.g. "h-1o-1", "h9o1"); "s0"/"s1": automatic tiles without / with the shared x0
-slice (DeviceEnsemble.shared_x0); f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
+slice (DeviceEnsemble.shared_x0); "r0"/"r1": separate / fused step + reset (RolloutEngine.fuse_reset); f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
 """
 import re
 import ctypes
@@ -53,7 +53,8 @@ def setv(v):
     'p' -> persistent workgroups; 'auto'/'-1' -> automatic."""
     s = str(v)
     ens.shared_x0 = s != "s0"  # "s0": one x0 copy per member (no k_shared)
-    if s in ("s0", "s1"):
+    eng.fuse_reset = s != "r0"  # "r0": amx_step + amx_reset_lanes instead of amx_step_reset
+    if s in ("s0", "s1", "r0", "r1"):
         s = "h-1o-1"
     m = re.fullmatch(r"h(-?\d+)o(-?\d+)", s)
     if m:
