@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256) void k_reset(const uint8_t* __restrict__ mask,
 }
 
 // ---- policy ----------------------------------------------------------------------------------
-// One workgroup = 256 threads serving POL_LANES = 16 lanes, POL_TPL = 16 threads per lane.
+// One workgroup = 256 threads serving 256/TPL lanes, TPL = 16 or 32 threads per lane.
 // The whole MLP (W1 [H1][S], W2, W3) and the lanes' float32 observations are staged in LDS
 // once per workgroup.  Thread (lane l, u0) owns output units u = u0 + 16q of every layer; each
 // inner step loads one float4 of the lane's input row (broadcast over the lane's 16 threads)
@@ -354,9 +354,9 @@ __host__ __device__ inline int pol_blob_floats(int S, int H1, int H2, int A) {
   return (H1 * s1 + H2 * s2 + A * s3 + H1 + H2 + A + 3) & ~3;
 }
 
-__host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A) {
+__host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A, int lanes = POL_LANES) {
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
-  const size_t fl = (size_t)pol_blob_floats(S, H1, H2, A) + POL_LANES * (s1 + s2 + s3 + A);
+  const size_t fl = (size_t)pol_blob_floats(S, H1, H2, A) + lanes * (s1 + s2 + s3 + A);
   return fl * sizeof(float);
 }
 
@@ -417,7 +417,7 @@ __device__ inline void pol_stage_all(float* __restrict__ img, const float* __res
   }
 }
 
-template <int Q>
+template <int TPL, int Q>
 __device__ inline void pol_layer(const float* __restrict__ w, int ws, const float* __restrict__ x, int n4,
                                  const float* __restrict__ bias, int H, int u0, float (&out)[Q], bool tanh_act) {
   float acc[Q];
@@ -425,7 +425,7 @@ __device__ inline void pol_layer(const float* __restrict__ w, int ws, const floa
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     acc[q] = 0.f;
-    const int u = u0 + POL_TPL * q;
+    const int u = u0 + TPL * q;
     wr[q] = w + (u < H ? u : H - 1) * ws;
   }
 #pragma unroll 2
@@ -444,14 +444,15 @@ __device__ inline void pol_layer(const float* __restrict__ w, int ws, const floa
   }
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
-    const int u = u0 + POL_TPL * q;
+    const int u = u0 + TPL * q;
     const float z = acc[q] + bias[u < H ? u : H - 1];
     out[q] = tanh_act ? tanhf(z) : z;
   }
 }
 
-template <int QH, int QA>
+template <int TPL, int QH, int QA>
 __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
+  constexpr int POL_LANES = 256 / TPL;  // lanes per workgroup
   extern __shared__ __attribute__((aligned(16))) float psm[];
   const int S = p.S, A = p.A, H1 = p.H1, H2 = p.H2;
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
@@ -477,27 +478,27 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   for (int i = t; i < POL_LANES * (s2 + s3); i += 256) h1[i] = 0.f;  // pads of h1/h2
   __syncthreads();
 
-  const int l = t / POL_TPL, u0 = t % POL_TPL;
+  const int l = t / TPL, u0 = t % TPL;
   const int b = b0 + l;
   {
     float o[QH];
-    pol_layer<QH>(w1, s1, so + l * s1, (S + 3) >> 2, bb1, H1, u0, o, true);
+    pol_layer<TPL, QH>(w1, s1, so + l * s1, (S + 3) >> 2, bb1, H1, u0, o, true);
 #pragma unroll
-    for (int q = 0; q < QH; ++q) if (u0 + POL_TPL * q < H1) h1[l * s2 + u0 + POL_TPL * q] = o[q];
+    for (int q = 0; q < QH; ++q) if (u0 + TPL * q < H1) h1[l * s2 + u0 + TPL * q] = o[q];
   }
   __syncthreads();
   {
     float o[QH];
-    pol_layer<QH>(w2, s2, h1 + l * s2, (H1 + 3) >> 2, bb2, H2, u0, o, true);
+    pol_layer<TPL, QH>(w2, s2, h1 + l * s2, (H1 + 3) >> 2, bb2, H2, u0, o, true);
 #pragma unroll
-    for (int q = 0; q < QH; ++q) if (u0 + POL_TPL * q < H2) h2[l * s3 + u0 + POL_TPL * q] = o[q];
+    for (int q = 0; q < QH; ++q) if (u0 + TPL * q < H2) h2[l * s3 + u0 + TPL * q] = o[q];
   }
   __syncthreads();
   float o[QA];
-  pol_layer<QA>(w3, s3, h2 + l * s3, (H2 + 3) >> 2, bb3, A, u0, o, false);
+  pol_layer<TPL, QA>(w3, s3, h2 + l * s3, (H2 + 3) >> 2, bb3, A, u0, o, false);
 #pragma unroll
   for (int q = 0; q < QA; ++q) {
-    const int u = u0 + POL_TPL * q;
+    const int u = u0 + TPL * q;
     if (u >= A || b >= p.B) continue;
     const float m = o[q];  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
     if (p.mean_out) p.mean_out[(long long)b * A + u] = m;
@@ -756,6 +757,13 @@ extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, i
   return AMX_OK;
 }
 
+static int g_pol_tpl = 0;  // amx__set_policy_tpl: 0 automatic (16), 32 threads per lane (A/B)
+
+extern "C" int amx__set_policy_tpl(int tpl) {
+  g_pol_tpl = tpl;
+  return AMX_OK;
+}
+
 static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                       const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                       const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
@@ -770,7 +778,13 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
                             (ctx->M == 1 || stride_m >= (long long)ldk * B)),
                 "amx_policy_act: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B");
   if (B == 0) return AMX_OK;
-  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
+  // threads per lane: 16 (16 lanes per workgroup).  amx__set_policy_tpl(32) selects 8 lanes
+  // of 32 threads (twice the waves, one output per thread) when H <= 32, A <= 64 -- measured
+  // 1.3 % slower per rollout (tools/rollout_ab.py p16,p32), so not the default
+  const int hmax = H1 > H2 ? H1 : H2;
+  const int tpl = (g_pol_tpl == 32 && hmax <= 32 && ctx->A <= 64) ? 32 : 16;
+  const int lanes = 256 / tpl;
+  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A, lanes);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S/H too large for LDS staging (%zu B)", lds);
   PolicyArgs p;
   p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;
@@ -780,15 +794,16 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
   p.act = act; p.mean_out = mean;
   p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
   p.S = ctx->S; p.A = ctx->A; p.B = B;
-  dim3 grid((B + POL_LANES - 1) / POL_LANES);
+  dim3 grid((B + lanes - 1) / lanes);
   // outputs per thread, rounded up to a compiled width: hidden layers QH, action layer QA
-  const int qh = ((H1 > H2 ? H1 : H2) + POL_TPL - 1) / POL_TPL;
-  const int qa = (ctx->A + POL_TPL - 1) / POL_TPL;
+  const int qh = (hmax + tpl - 1) / tpl;
+  const int qa = (ctx->A + tpl - 1) / tpl;
   hipStream_t st = (hipStream_t)stream;
-  if (qh <= 2 && qa <= 2) hipLaunchKernelGGL((k_policy<2, 2>), grid, dim3(256), lds, st, p);
-  else if (qh <= 2 && qa <= 3) hipLaunchKernelGGL((k_policy<2, 3>), grid, dim3(256), lds, st, p);
-  else if (qh <= 4 && qa <= 4) hipLaunchKernelGGL((k_policy<4, 4>), grid, dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((k_policy<16, 16>), grid, dim3(256), lds, st, p);
+  if (tpl == 32) hipLaunchKernelGGL((k_policy<32, 1, 2>), grid, dim3(256), lds, st, p);
+  else if (qh <= 2 && qa <= 2) hipLaunchKernelGGL((k_policy<16, 2, 2>), grid, dim3(256), lds, st, p);
+  else if (qh <= 2 && qa <= 3) hipLaunchKernelGGL((k_policy<16, 2, 3>), grid, dim3(256), lds, st, p);
+  else if (qh <= 4 && qa <= 4) hipLaunchKernelGGL((k_policy<16, 4, 4>), grid, dim3(256), lds, st, p);
+  else hipLaunchKernelGGL((k_policy<16, 16, 16>), grid, dim3(256), lds, st, p);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

@@ -62,3 +62,38 @@ def test_fused_step_reset_matches_step_then_reset(cost_kind):
     done = ref.done.bool()
     assert done.any() and not done.all()  # both branches ran
     assert (ref.reset_rows[done[:, :ref.B]] >= 0).all()
+
+
+@pytest.mark.parametrize("hidden", [(32, 32), (64, 48)])
+def test_policy_threads_per_lane_bit_identical(hidden):
+    """k_policy with 32 threads per lane (8 lanes per workgroup, amx__set_policy_tpl(32) for
+    H <= 32) and with 16 (automatic) gives the same actions, means and fused x0 rows bit for bit (each
+    output unit keeps its sequential fma order); wider layers always run the 16-thread form."""
+    import ctypes
+    import amp_extensions_amd as amx
+    S, A, B = 197, 36, 1000
+    rs = np.random.RandomState(4)
+    s = 0.5 * rs.randn(2048, S)
+    a = rs.randn(2048, A)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s + 0.01)])
+    ctx = amx.AmxContext(S, A, n_models=4, hidden=512, n_hidden=4, feat_dim=512, device=DEV)
+    ctx.set_normalizers(norms)
+    pw, log_std = R.init_policy_weights(S, A, hidden, seed=100)
+    pol = amx.DevicePolicy(ctx, pw, log_std, seed=1)
+    ctx.lib.amx__set_policy_tpl.argtypes = [ctypes.c_int]
+    ob = torch.from_numpy(0.5 * rs.randn(B, S)).to(DEV)
+    outs = []
+    for tpl in (16, 32):
+        ctx.lib.amx__set_policy_tpl(tpl)
+        act = torch.empty(B, A, dtype=torch.float64, device=DEV)
+        mean = torch.empty(B, A, dtype=torch.float32, device=DEV)
+        x0 = torch.zeros(4, 1024, ctx.ldk, dtype=torch.float32, device=DEV)
+        pol.act(ob, B, act, 7, mean_out=mean, x0=x0)
+        outs.append((act, mean, x0))
+    ctx.lib.amx__set_policy_tpl(0)
+    torch.cuda.synchronize()
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    obn = ob.cpu().numpy()
+    ref = np.stack([R.policy_mean(pw, obn[i]) for i in range(0, B, 37)])  # the oracle's float32 MLP
+    np.testing.assert_allclose(outs[1][1].cpu().numpy()[::37], ref, rtol=1e-5, atol=1e-6)

@@ -53,12 +53,15 @@ def main():
     f = per_dispatch(fetch_dir, "FETCH_SIZE", kernel)[-(L + 1):]
     w = per_dispatch(write_dir, "WRITE_SIZE", kernel)[-(L + 1):]
     layers, tot_hbm, tot_alg = [], 0, 0
+    # f16x3: the x0 slice is assembled once and read for all M members (k_shared), so its
+    # compulsory bytes are B*k0*4, not M*B*k0*4
+    a_bytes = (lambda K: (rows * (K - k0) + B * k0) * 4) if gemm == "f16x3" else (lambda K: rows * K * 4)
     for i in range(L + 1):
         K = k0 + i * H
         if i < L:
-            alg = rows * K * 4 + M * H * K * wb + rows * H * 4
+            alg = a_bytes(K) + M * H * K * wb + rows * H * 4
         else:
-            alg = rows * K * 4 + M * n_out_pad * K * wb + rows * S * 4
+            alg = a_bytes(K) + M * n_out_pad * K * wb + rows * S * 4
         hbm = int((2 * f[i] + w[i]) * 1024)
         layers.append({"layer": i, "K": K, "fetch_kb": f[i], "write_kb": w[i], "hbm_bytes": hbm, "alg_bytes": alg})
         tot_hbm += hbm
