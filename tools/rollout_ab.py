@@ -5,7 +5,7 @@ usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
 variant: f16x3 (default GEMM path) "h<hidden>o<output>" -> amx__set_h3_variant / amx__set_h3_out_variant
 (-1 = automatic, e.g. "h-1o-1", "h9o1"); "s0"/"s1": automatic tiles without / with the shared x0
 slice (DeviceEnsemble.shared_x0); "r0"/"r1": separate / fused step + reset (RolloutEngine.fuse_reset); "p16"/"p32": policy kernel with 16 / 32
-threads per lane (amx__set_policy_tpl); f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
+threads per lane (amx__set_policy_tpl); "o0"/"o1": batched / per-step side-stream scoring; f32 path (--gemm f32 ensembles) "<k>[p]" -> amx__set_gemm_variant.
 """
 import re
 import ctypes
@@ -57,7 +57,9 @@ def setv(v):
     ens.shared_x0 = s != "s0"  # "s0": one x0 copy per member (no k_shared)
     eng.fuse_reset = s != "r0"  # "r0": amx_step + amx_reset_lanes instead of amx_step_reset
     lib.amx__set_policy_tpl(16 if s == "p16" else (32 if s == "p32" else 0))  # policy threads per lane
-    if s in ("s0", "s1", "r0", "r1", "p16", "p32"):
+    if s in ("o0", "o1"):  # per-step scoring on a side stream (RolloutEngine.overlap_score)
+        eng.overlap_score = s == "o1"
+    if s in ("s0", "s1", "r0", "r1", "p16", "p32", "o0", "o1"):
         s = "h-1o-1"
     m = re.fullmatch(r"h(-?\d+)o(-?\d+)", s)
     if m:
