@@ -45,6 +45,7 @@ __global__ __launch_bounds__(256) void k_mmd_fit(const double* __restrict__ phi_
                                                  float* __restrict__ mmd) {
   __shared__ double red[4];
   double acc = 0.0;
+  if (count == 0.0) count = phi_sum[F];  // the fused [sum phi | count] message
   for (int f = threadIdx.x; f < F; f += blockDim.x) {
     const float mean = (float)(phi_sum[f] / count);
     const float wf = mean - phi_e[f];
@@ -193,7 +194,7 @@ extern "C" int amx_sum_partials(amx_ctx* ctx, const double* partials, int n_part
 extern "C" int amx_mmd_fit(amx_ctx* ctx, const double* phi_sum, double count, const float* phi_e, int F,
                            float* w, float* mmd, void* stream) {
   AMX_CHECK_ARG(ctx && phi_sum && phi_e && w && mmd && F > 0, "amx_mmd_fit: bad argument");
-  AMX_CHECK_ARG(count > 0.0, "amx_mmd_fit: count must be positive (empty rollout)");
+  AMX_CHECK_ARG(count > 0.0 || count == 0.0, "amx_mmd_fit: count must be positive (empty rollout), or 0: read phi_sum[F]");
   hipLaunchKernelGGL(k_mmd_fit, dim3(1), dim3(256), 0, (hipStream_t)stream, phi_sum, count, phi_e, F, w, mmd);
   AMX_CHECK_LAUNCH();
   return AMX_OK;

@@ -118,7 +118,6 @@ class RolloutEngine:
         if isinstance(cost, RBFLinearCost):
             self.phi = z(K, Bp, cost.feature_dim)
             self.partials = z(K, Bp // 128, cost.feature_dim, dt=torch.float64)
-            self.phi_sum = z(cost.feature_dim, dt=torch.float64)
         self.t = 0              # steps taken in the current rollout
         self.step_counter = 0   # global step counter (policy RNG stream)
         # graph mode: the counter of a captured rollout's step t is dev_step[0] + t, and the graph
@@ -128,6 +127,9 @@ class RolloutEngine:
         self._graph_ahead = False  # replays advanced dev_step past the host counter
         # [sum phi (F) | count] of the rollout: the one buffer the cross-rank all-reduce touches
         self._fbuf = z(cost.feature_dim + 1, dt=torch.float64) if isinstance(cost, RBFLinearCost) else None
+        self._fbuf_count = None  # the count the message buffer's last slot holds (None: unknown)
+        if self._fbuf is not None:  # feature_sum()'s output is the message's first F slots
+            self.phi_sum = self._fbuf[:cost.feature_dim]  # (the global sums once all-reduced)
         self.mb_mmd = None
 
     # ------------------------------------------------------------------------------------
@@ -329,22 +331,25 @@ class RolloutEngine:
         self.relabel_pre()
         if allreduce is not None:
             allreduce(self._fbuf)  # ONE fused all-reduce of [sum phi, count] across ranks
+            self._fbuf_count = None
         return self.relabel_post()
 
     def relabel_pre(self) -> torch.Tensor:
         """Rank-local half of the relabel: this rank's [sum phi | count] in the persistent
         fp64 buffer that the cross-rank all-reduce sums (dist.feature_mean's message)."""
         F = self.cost.feature_dim
-        self._fbuf[:F].copy_(self.feature_sum())
-        self._fbuf[F:].fill_(float(self.t * self.B))
+        self.feature_sum()  # phi_sum is a view of the message's first F slots: no copy
+        n = float(self.t * self.B)
+        if self._capturing or self._fbuf_count != n:  # the count slot changes only with T or an all-reduce
+            self._fbuf[F:].fill_(n)
+            self._fbuf_count = None if self._capturing else n
         return self._fbuf
 
     def relabel_post(self) -> dict:
         """Global half: mean -> witness w (the fp64 mean is rounded to fp32 inside amx_mmd_fit,
-        count passed as 1.0) -> per-sample rewards of every recorded transition."""
-        cost, F = self.cost, self.cost.feature_dim
-        mean = self._fbuf[:F] / self._fbuf[F]
-        self.mb_mmd = cost.fit_w_device(mean, 1.0)  # device tensor: no host sync
+        which reads the count from the message's last slot) -> per-sample rewards of every recorded transition."""
+        cost = self.cost
+        self.mb_mmd = cost.fit_w_device(self._fbuf, 0.0)  # count 0: read from the message; no host sync
         n = self.t * self.Bp
         cost.reward_launch(self.phi.data_ptr(), cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),
                            self.rewards.data_ptr(), self.ipm.data_ptr(), self.wbonus.data_ptr(), n)
@@ -394,6 +399,7 @@ class RolloutEngine:
             graphs[0].replay()
             if two:
                 allreduce(self._fbuf)
+                self._fbuf_count = None
                 graphs[1].replay()
             self._graph_ahead = True
             return T * self.B

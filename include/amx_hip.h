@@ -368,7 +368,8 @@ int amx_sum_partials(amx_ctx* ctx, const double* partials, int n_parts, int F, d
                      void* stream);
 
 /* fit_cost closed form (milo/milo/linear_cost.py:84-94) after the cross-rank sum:
- * phi_pi = (float)(phi_sum / count); w = phi_pi - phi_e; mmd[0] = dot(w, w) (fp32). */
+ * phi_pi = (float)(phi_sum / count); w = phi_pi - phi_e; mmd[0] = dot(w, w) (fp32).
+ * count = 0: the count is read from phi_sum[F] (the all-reduced [sum phi | count] message). */
 int amx_mmd_fit(amx_ctx* ctx, const double* phi_sum, double count, const float* phi_e, int F,
                 float* w, float* mmd, void* stream);
 
