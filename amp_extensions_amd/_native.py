@@ -79,7 +79,7 @@ SIGNATURES = {
     "amx_mmd_fit": (c_int, [vp, vp, c_dbl, vp, c_int, vp, vp, vp]),
     "amx_mmd_reward": (c_int, [vp, vp, c_int, vp, c_int, vp, c_flt, c_dbl, c_flt, c_flt, vp, vp, vp, c_int, vp]),
     "amx_mmd_reward_raw": (c_int, [vp, vp, c_int, vp, c_int, vp, c_dbl, vp, vp, vp, c_int, vp]),
-    "amx_expert_cost": (c_int, [vp, vp, c_int, vp, c_int, c_int, c_flt, c_flt, vp, vp]),
+    "amx_expert_cost": (c_int, [vp, vp, c_int, vp, c_int, c_int, c_flt, c_flt, vp, vp, c_dbl, vp]),
     "amx_amp_reward": (c_int, [vp, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
     "amx_disc_reward": (c_int, [vp, c_int, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
     "amx_cost_rows": (c_int, [vp, vp, c_ll, c_int, vp, c_ll, c_int, vp, c_ll, c_int, c_int, vp, c_int, vp]),

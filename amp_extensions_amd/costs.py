@@ -103,6 +103,7 @@ class RBFLinearCost:
         self.n_expert = expert_cpu.shape[0]
         self.phi_e = (tot / self.n_expert).float()
         self._expert_out = torch.empty(1 + 1024, dtype=torch.float64, device=ctx.device)
+        self._expert_mean = None  # fp32 [1]: get_expert_cost's result (amx_expert_cost mean_out)
 
     # linear_cost.py:73-82
     def fit_bandwidth(self, data: torch.Tensor) -> float:
@@ -177,11 +178,15 @@ class RBFLinearCost:
         if self.cost_range is None:   # the reference clamps with c_min/c_max, unset without a range
             raise AttributeError("'RBFLinearCost' object has no attribute 'c_min'")
         c = self.ctx
+        if self._expert_mean is None:
+            self._expert_mean = torch.empty(1, dtype=torch.float32, device=c.device)
         N.check(c.lib.amx_expert_cost(c.h, self.expert_rep.data_ptr(), self.expert_rep.stride(0), self.w.data_ptr(),
                                       self.feature_dim, self.n_expert, self.c_min, self.c_max,
-                                      self._expert_out.data_ptr(), c.stream), "amx_expert_cost")
-        mean = (self._expert_out[0] / self.n_expert).float()
-        return np.float32(1 - self.lambda_b) * mean
+                                      self._expert_out.data_ptr(), self._expert_mean.data_ptr(),
+                                      float(self.lambda_b), c.stream), "amx_expert_cost")
+        # (1 - lambda) * mean in fp32 as the reference's torch expression; a 0-dim view of a
+        # persistent buffer, overwritten by the next call
+        return self._expert_mean[0]
 
     def get_bonus_costs(self, states, actions, ensemble, next_states=None):
         """linear_cost.py:111-152: cost [T, 1] and the info dict."""

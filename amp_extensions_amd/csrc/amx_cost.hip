@@ -127,7 +127,8 @@ __global__ __launch_bounds__(256) void k_expert_cost(const float* __restrict__ p
 
 // Deterministic sum of n partials: thread t sums t, t+256, ... then a fixed-shape tree.
 __global__ __launch_bounds__(256) void k_sum_small(const double* __restrict__ partials, int n,
-                                                   double* __restrict__ out) {
+                                                   double* __restrict__ out, float* __restrict__ mean_out = nullptr,
+                                                   int n_rows = 1, float scale = 1.f) {
   __shared__ double red[256];
   double s = 0.0;
   for (int i = threadIdx.x; i < n; i += 256) s += partials[i];
@@ -137,7 +138,10 @@ __global__ __launch_bounds__(256) void k_sum_small(const double* __restrict__ pa
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = red[0];
+  if (threadIdx.x == 0) {
+    out[0] = red[0];
+    if (mean_out) mean_out[0] = scale * (float)(red[0] / (double)n_rows);  // fp32 product, as torch
+  }
 }
 
 // LOSS 0: least squares (get_ls_costs, gail_cost.py:231-236); LOSS 1: log-likelihood
@@ -233,7 +237,8 @@ extern "C" int amx_mmd_reward_raw(amx_ctx* ctx, const float* phi, int ldphi, con
 }
 
 extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
-                               float c_min, float c_max, double* out, void* stream) {
+                               float c_min, float c_max, double* out, float* mean_out, double lambda_b,
+                               void* stream) {
   AMX_CHECK_ARG(ctx && phi_e_rows && w && out, "amx_expert_cost: null pointer");
   AMX_CHECK_ARG(F > 0 && F % 256 == 0 && ldphi >= F && ldphi % 4 == 0, "amx_expert_cost: F=%d ldphi=%d", F, ldphi);
   AMX_CHECK_ARG(n > 0, "amx_expert_cost: n=%d", n);
@@ -242,7 +247,8 @@ extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi,
   hipLaunchKernelGGL(k_expert_cost, dim3(nb), dim3(256), 0, (hipStream_t)stream, phi_e_rows, ldphi, w, F, n, c_min,
                      c_max, out + 1);
   AMX_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_sum_small, dim3(1), dim3(256), 0, (hipStream_t)stream, out + 1, nb, out);
+  hipLaunchKernelGGL(k_sum_small, dim3(1), dim3(256), 0, (hipStream_t)stream, out + 1, nb, out, mean_out, n,
+                     (float)(1.0 - lambda_b));
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

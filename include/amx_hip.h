@@ -388,10 +388,12 @@ int amx_mmd_reward_raw(amx_ctx* ctx, const float* phi, int ldphi, const float* w
                        double lambda_b, float* reward, float* ipm, float* wbonus, int n, void* stream);
 
 /* get_expert_cost (milo/milo/linear_cost.py:105-109): partial fp64 sums over row
- * blocks of clamp(phi_E[r].w, c_min, c_max); out[0] = sum (fp64), caller scales by
- * (1-lambda)/N_e.  Uses the resident expert features. */
+ * blocks of clamp(phi_E[r].w, c_min, c_max); out[0] = sum (fp64; out holds 1 + 1024
+ * doubles).  mean_out (nullable) receives the finished cost in fp32:
+ * (float)(1 - lambda_b) * (float)(sum / n).  Uses the resident expert features. */
 int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
-                    float c_min, float c_max, double* out, void* stream);
+                    float c_min, float c_max, double* out, float* mean_out, double lambda_b,
+                    void* stream);
 
 /* ---- AMP / GAIL least-squares discriminator reward ---------------------------- */
 
