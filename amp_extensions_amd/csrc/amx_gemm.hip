@@ -909,6 +909,54 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
   const float* bias = a.bias + (long long)g * a.strideBias;
   const int* wexp = a.w_exp + (long long)g * a.strideWexp;
   float* Cg = a.C + (long long)g * a.strideC;
+  if constexpr (EPI == EPI_RFF) {  // the 32x32 path's RFF epilogue on the 16x16 accumulator layout
+    static_assert(TL::BM == 128 && TL::BN == 128 && TL::NT == 256, "RFF epilogue assumes the 128x128 tile");
+    constexpr int CLD = 128 + 4;
+    // un-scale in place (exact powers of two) while sExp (in the stage area) is readable
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int4 ev = *reinterpret_cast<const int4*>(sExp + lrow0 + m * 16 + 4 * lq);
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const int ec = wexp[col0 + n * 16 + lc] - 2 * HSC;
+        acc[m][n][0] = __builtin_amdgcn_ldexpf(acc[m][n][0], ev.x + ec);
+        acc[m][n][1] = __builtin_amdgcn_ldexpf(acc[m][n][1], ev.y + ec);
+        acc[m][n][2] = __builtin_amdgcn_ldexpf(acc[m][n][2], ev.z + ec);
+        acc[m][n][3] = __builtin_amdgcn_ldexpf(acc[m][n][3], ev.w + ec);
+      }
+    }
+    __syncthreads();
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* Cs = smem;  // [128][CLD] over the stage buffers
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          Cs[(lrow0 + m * 16 + 4 * lq + j) * CLD + wn * TL::WCOLS + n * 16 + lc] = acc[m][n][j];
+    __syncthreads();
+    const int t = threadIdx.x, c = t & 127, half = t >> 7;
+    const int col = tn * 128 + c;
+    const float bv = a.bias[col];
+    double csum = 0.0;
+#pragma unroll 2
+    for (int i = 0; i < 64; ++i) {
+      const int r = half * 64 + i;
+      const int row = tm * 128 + r;
+      const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
+      const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
+      a.C[(long long)row * a.ldc + col] = phi;
+      const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
+      csum += valid ? (double)phi : 0.0;
+    }
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(smem);
+    if (half == 1) red[c] = csum;
+    __syncthreads();
+    if (half == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[c];
+    return;
+  }
   if constexpr (EPI == EPI_BIAS_ACT) {
     static_assert(MB * 4 == 16 || MB * 4 == 32, "row-exponent reduce-scatter: 16 or 32 rows per lane");
     float bv[NB];
@@ -1397,6 +1445,7 @@ using H128x256w8k32lateMPE = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, tr
 using H128x224k32lateP = TileH3<2, 7, 2, 1, 4, 2, true, true, false, 0, 0, true>;
 using H128k32late = TileH3<2, 2, 2, 2, 2, 2, true>;
 using H128k32lateP = TileH3<2, 2, 2, 2, 2, 2, true, true, false, 0, 0, true>;
+using H128k32lateMPES = TileH3<2, 2, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;  // RFF, 16x16x32
 using H128k32P = TileH3<2, 2, 2, 2, 2, 2, false, true, false, 0, 0, true>;
 using H128x256w8k32lateM = TileH3<2, 4, 2, 2, 2, 2, true, true, true>;  // output on N padded to 256, 16x16x32
 using H128x224w8k32lateM = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 2, 7>;  // output: 8 waves of 32x112, 16x16x32
@@ -2026,6 +2075,7 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
       case 1: return launch_h3<EPI_RFF, H128k32late>(a, (hipStream_t)stream);
       case 2: return launch_h3<EPI_RFF, H128k32lateP>(a, (hipStream_t)stream);
       case 3: return launch_h3<EPI_RFF, H128k32P>(a, (hipStream_t)stream);
+      case 4: return launch_h3<EPI_RFF, H128k32lateMPES>(a, (hipStream_t)stream);
       default: return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
     }
   }
