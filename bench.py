@@ -40,7 +40,7 @@ GEMM_INFO = {
                        "into 2 fp16 limbs, 3 limb products per f32 MAC accumulated in fp32 (error vs fp64 <= the "
                        "f32 MFMA's, tools/h3_accuracy.py)",
                   unit="TFLOP/s (f32-equivalent; peak = f16 dense 2516.6 / 3 limb products)",
-                  kernel="k_gemm_h3 (ensemble layers: hidden v_mfma_f32_16x16x32_f16, output v_mfma_f32_32x32x16_f16; "
+                  kernel="k_gemm_h3 (ensemble layers: hidden and output layers on v_mfma_f32_16x16x32_f16; "
                          "3 per f32 MAC)"),
     "bf16x6": dict(peak=X6_PEAK_TFLOPS, products=6,
                    desc="bf16x6: fp32 operands split exactly into 3 bf16 limbs, 6 limb products per f32 MAC "
