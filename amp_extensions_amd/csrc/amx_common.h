@@ -29,6 +29,7 @@ struct amx_termination {
 
 struct amx_ctx {
   int device;
+  int n_cus;               // compute units of the device (tile selection: workgroups resident at once)
   int S, A, M, H, L, F;
   int k0_pad, ldk, n_out_pad, k_rff_pad;
   // device copies of the normalizers: mu_s, sd_s (S), mu_a, sd_a (A), mu_d, sd_d (S)

@@ -36,6 +36,9 @@ extern "C" amx_ctx* amx_create(int device, int S, int A, int n_models, int hidde
     return nullptr;
   }
   c->device = device;
+  hipDeviceProp_t prop;
+  c->n_cus = (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+                 ? prop.multiProcessorCount : 256;
   c->S = S;
   c->A = A;
   c->M = n_models;

@@ -32,20 +32,14 @@ constexpr int LDS_LD = BK + 4;  // floats per LDS row
 
 enum { EPI_BIAS_ACT = 0, EPI_UNNORM = 1, EPI_RFF = 2 };
 
-template <int WM_, int WN_, int TM_, int TN_, int STAGES_ = 2, int OCC_ = 2, bool PIPE_ = false>
+template <int WM_, int WN_, int TM_, int TN_>
 struct Tile {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_;
-  // PIPE: one wave per SIMD, software-pipelined: fragments of step v+1 are read while the
-  // MFMAs of step v run, and the next K-tile's LDS publish + barrier + first fragment read
-  // sit under the last MFMA group of the current tile.
-  static constexpr bool PIPE = PIPE_;
-  static constexpr int STAGES = STAGES_;  // 2: double-buffered LDS, 1 barrier / K-tile;
-                                          // 1: single buffer, 2 barriers / K-tile, half the LDS
-  static constexpr int OCC = OCC_;        // __launch_bounds__ waves-per-SIMD target
+  static constexpr int OCC = 2;                             // __launch_bounds__ waves-per-SIMD target
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   static constexpr int STAGE = (BM + BN) * LDS_LD;          // floats of one stage (A + W)
-  static constexpr size_t LDS = STAGES * STAGE * sizeof(float);
+  static constexpr size_t LDS = 2 * STAGE * sizeof(float);  // double-buffered, 1 barrier / K-tile
   static constexpr int ROW_STEP = NT / 8;                   // staging rows covered per pass
   static constexpr int VA = BM / ROW_STEP, VW = BN / ROW_STEP;
   static_assert(BM % ROW_STEP == 0 && BN % ROW_STEP == 0, "staging map");
@@ -66,11 +60,8 @@ struct GemmArgs {
   double* col_partials;    // EPI_RFF: [rows/128][N]
   const uint8_t* row_mask; // EPI_RFF: nullable
   int tiles_m, tiles_n, groups;
-  long long* clock_probe;  // internal diagnostics: per-WG {s_memtime, s_memrealtime} at start / end
   const uint16_t* W3;      // bf16x6 path: 3-limb weight image [g][N][K/16][3][16] (amx_split_bf16x3)
   long long strideW3;      //   elements between groups; a row is 3*K elements
-  const uint16_t* A3;      // bf16x6 path, pre-split activations: [g][rows][lda/16][3][16]
-  long long strideA3;
   // f16x3 path (see the section below)
   const uint16_t* W2;      // 2-limb scaled weight image [g][N][K/16][2][16] (amx_split_f16x2)
   long long strideW2;
@@ -82,11 +73,7 @@ struct GemmArgs {
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
   int k_shared;            // leading K columns of A read from group 0's rows for every group
                            //   (the ensemble's x0 slice, assembled once; multiple of the tile's BK)
-  int abl_nostore;         // timing ablation only (h3 variant 96): skip the hidden-layer stores
-  int prio;                // A/B only: 1 s_setprio(1) around each MFMA block, 2 static priority for waves >= NT/2
 };
-
-long long* g_clock_probe = nullptr;  // amx__set_gemm_clock_probe (diagnostics only)
 
 // Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over
 // the 8 XCDs, so block ids congruent mod 8 share an L2.  We hand each XCD a contiguous
@@ -207,12 +194,6 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int orig) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   int g, tm, tn;
   map_tile(a, orig, g, tm, tn);
-  long long clk0 = 0, rt0 = 0;
-  if (a.clock_probe) {
-    clk0 = (long long)__builtin_amdgcn_s_memtime();
-    rt0 = (long long)__builtin_amdgcn_s_memrealtime();
-  }
-
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const float* __restrict__ Wg = a.W + (long long)g * a.strideW + (long long)tn * BN * a.ldw;
 
@@ -254,75 +235,8 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int orig) {
 
   const int a_off = (wm * TM * 32 + li) * LDS_LD + lh * 16;
   const int w_off = BM * LDS_LD + (wn * TN * 32 + li) * LDS_LD + lh * 16;
-  if constexpr (TL::PIPE) {
-    static_assert(TL::STAGES == 2, "PIPE needs the double buffer");
-    f32x4 fa[2][TM], fb[2][TN];
-    auto mfma_e = [&](int p, int e) {
-#pragma unroll
-      for (int m = 0; m < TM; ++m)
-#pragma unroll
-        for (int n = 0; n < TN; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[p][m][e], fb[p][n][e], acc[m][n], 0, 0, 0);
-    };
-#pragma unroll
-    for (int m = 0; m < TM; ++m) fa[0][m] = *reinterpret_cast<const f32x4*>(smem + a_off + m * 32 * LDS_LD);
-#pragma unroll
-    for (int n = 0; n < TN; ++n) fb[0][n] = *reinterpret_cast<const f32x4*>(smem + w_off + n * 32 * LDS_LD);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
-#pragma unroll
-      for (int j = 0; j < VA; ++j) ra[j] = *reinterpret_cast<const f32x4*>(a_src + j * a_step + kn);
-#pragma unroll
-      for (int j = 0; j < VW; ++j) rw[j] = *reinterpret_cast<const f32x4*>(w_src + j * w_step + kn);
-      __builtin_amdgcn_sched_barrier(0);
-      const float* As = smem + cur * STAGE + a_off;
-      const float* Ws = smem + cur * STAGE + w_off;
-#pragma unroll
-      for (int v = 0; v < 3; ++v) {
-        const int p = v & 1;
-#pragma unroll
-        for (int m = 0; m < TM; ++m) fa[p ^ 1][m] = *reinterpret_cast<const f32x4*>(As + m * 32 * LDS_LD + (v + 1) * 4);
-#pragma unroll
-        for (int n = 0; n < TN; ++n) fb[p ^ 1][n] = *reinterpret_cast<const f32x4*>(Ws + n * 32 * LDS_LD + (v + 1) * 4);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) mfma_e(p, e);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      // step 3 (fragments in set 1): three MFMA groups, then publish the prefetched tile,
-      // barrier, read step 0 of the next tile into set 0, last MFMA group
-#pragma unroll
-      for (int e = 0; e < 3; ++e) mfma_e(1, e);
-      __builtin_amdgcn_sched_barrier(0);
-      const int nb = (cur ^ 1) * STAGE;
-#pragma unroll
-      for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + nb + j * RS * LDS_LD) = ra[j];
-#pragma unroll
-      for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + nb + j * RS * LDS_LD) = rw[j];
-      __syncthreads();
-#pragma unroll
-      for (int m = 0; m < TM; ++m) fa[0][m] = *reinterpret_cast<const f32x4*>(smem + nb + a_off + m * 32 * LDS_LD);
-#pragma unroll
-      for (int n = 0; n < TN; ++n) fb[0][n] = *reinterpret_cast<const f32x4*>(smem + nb + w_off + n * 32 * LDS_LD);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_e(1, 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = (TL::STAGES == 2) ? (kt & 1) : 0;
-    if constexpr (TL::STAGES == 1) {
-      // single buffer: tile kt is in registers; publish it, then prefetch kt+1 behind the MFMAs
-      if (kt > 0) {
-        __syncthreads();  // everyone finished reading tile kt-1
-#pragma unroll
-        for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + j * RS * LDS_LD) = ra[j];
-#pragma unroll
-        for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + j * RS * LDS_LD) = rw[j];
-        __syncthreads();
-      }
-    }
+    const int cur = kt & 1;
     // prefetch the next K-tile (the last iteration re-reads its own tile: branch-free loop)
     const int kn = (kt + 1 < nk ? kt + 1 : kt) * BK;
 #pragma unroll
@@ -350,37 +264,20 @@ __device__ __forceinline__ void gemm_tile(const GemmArgs& a, int orig) {
           for (int n = 0; n < TN; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[m][e], fb[n][e], acc[m][n], 0, 0, 0);
     }
-    if constexpr (TL::STAGES == 2) {
-      const int nb = (cur ^ 1) * STAGE;
+    const int nb = (cur ^ 1) * STAGE;
 #pragma unroll
-      for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + nb + j * RS * LDS_LD) = ra[j];
+    for (int j = 0; j < VA; ++j) *reinterpret_cast<f32x4*>(a_dst0 + nb + j * RS * LDS_LD) = ra[j];
 #pragma unroll
-      for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + nb + j * RS * LDS_LD) = rw[j];
-      __syncthreads();
-    }
-  }
-  }
-  if constexpr (TL::STAGES == 1) __syncthreads();  // epilogues reuse the LDS
-
-  if (a.clock_probe && threadIdx.x == 0) {
-    long long* p = a.clock_probe + 4LL * orig;
-    p[0] = clk0; p[1] = rt0;
-    p[2] = (long long)__builtin_amdgcn_s_memtime();
-    p[3] = (long long)__builtin_amdgcn_s_memrealtime();
+    for (int j = 0; j < VW; ++j) *reinterpret_cast<f32x4*>(w_dst0 + nb + j * RS * LDS_LD) = rw[j];
+    __syncthreads();
   }
   epilogue<EPI, TL>(a, acc, g, tm, tn);
 }
 
-// Grid = one workgroup per tile, or (persistent) fewer workgroups that each loop over tiles
-// id = blockIdx.x + j * gridDim.x (gridDim.x a multiple of 8 keeps every id on the XCD that
-// map_tile assigns it to): the epilogue stores of one tile then overlap the next tile's loads.
+// Grid = one workgroup per tile.
 template <int EPI, class TL>
 __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_nt(GemmArgs a) {
-  const int nwg = a.tiles_m * a.tiles_n * a.groups;
-  for (int id = blockIdx.x; id < nwg; id += gridDim.x) {
-    if (id != (int)blockIdx.x) __syncthreads();  // previous tile's last LDS reads are done
-    gemm_tile<EPI, TL>(a, id);
-  }
+  gemm_tile<EPI, TL>(a, blockIdx.x);
 }
 
 // ==== bf16x6: the same fp32 GEMM on the bf16 matrix pipe ==================================
@@ -406,32 +303,22 @@ typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int XBK = 16;  // granule of the weight image: 16 fp32 k per [limb][16] chunk
 
-// NSUB 16-k granules per K-tile (BK = 16*NSUB); LDS row = NSUB x [limb0 16 | limb1 | limb2]
-// + 8 bf16 pad (56 bf16 = 28 dwords at NSUB 1, 104 = 52 dwords at NSUB 2: both put the 16
-// rows of a ds_read_b128 lane group on distinct 4-bank slots).  STAGES 2: double-buffered
-// LDS, one barrier per K-tile; 1: single buffer, two barriers.  PF: K-tiles held in
-// registers ahead of the one being published (1 or 2).
-template <int WM_, int WN_, int TM_, int TN_, int NSUB_ = 1, int STAGES_ = 2, int PF_ = 1, int OCC_ = 2,
-          bool ALIMB_ = false, bool LATE_ = false>
+// LDS row = [limb0 16 | limb1 | limb2] + 8 bf16 pad (56 bf16 = 28 dwords: the 16 rows of a
+// ds_read_b128 lane group land on distinct 4-bank slots); BK = 16, double-buffered LDS, one
+// barrier per K-tile.
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2>
 struct TileX6 {
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_;
-  // LATE: barrier -> publish tile t+1 -> issue the loads of t+2 -> compute t (the LDS writes
-  // drain under the MFMAs and the global loads get a whole K-tile to land) instead of
-  // loads(t+1) -> compute t -> publish t+1 -> barrier
-  static constexpr bool LATE = LATE_;
-  // ALIMB: A arrives pre-split as a limb image like W3 (GemmArgs::A3), staged by plain copies
-  static constexpr bool ALIMB = ALIMB_;
-  static constexpr int NSUB = NSUB_, BK = 16 * NSUB_, STAGES = STAGES_, PF = PF_;
-  static constexpr int LD = NSUB * 48 + 8;                     // bf16 per LDS row
+  static constexpr int BK = 16;
+  static constexpr int LD = 48 + 8;                            // bf16 per LDS row
   static constexpr int NT = WM * WN * 64;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
   static constexpr int STAGE = (BM + BN) * LD;                 // bf16 of one stage (A + W)
-  static constexpr size_t LDS = STAGES * STAGE * sizeof(uint16_t);
-  static constexpr int NA = ALIMB ? BM * NSUB * 6 : BM * (BK / 4);  // 16-B chunks of the A tile
-  static constexpr int NW = BN * NSUB * 6;                     // 16-B chunks of the W tile
+  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t);
+  static constexpr int NA = BM * (BK / 4);                     // 16-B chunks of the A tile (fp32)
+  static constexpr int NW = BN * 6;                            // 16-B chunks of the W tile
   static constexpr int VA = (NA + NT - 1) / NT, VW = (NW + NT - 1) / NT;
   static_assert(LDS <= 160 * 1024, "LDS");
-  static_assert(PF == 1 || (PF == 2 && STAGES == 2), "two register sets need the double buffer");
 };
 
 // x (4 consecutive k of one row) -> limbs packed as 4 bf16 each
@@ -446,21 +333,14 @@ __device__ __forceinline__ void split3(f32x4 x, u32x2& l0, u32x2& l1, u32x2& l2)
   l2 = __builtin_bit_cast(u32x2, h2);
 }
 
-template <int V> using IC = std::integral_constant<int, V>;
-
 template <int EPI, class TL>
 __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
   constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
-  constexpr int NT = TL::NT, STAGE = TL::STAGE, NSUB = TL::NSUB, BK = TL::BK, CPR = BK / 4;
+  constexpr int NT = TL::NT, STAGE = TL::STAGE, BK = TL::BK, CPR = BK / 4;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
   int g, tm, tn;
   map_tile(a, orig, g, tm, tn);
-  long long clk0 = 0, rt0 = 0;
-  if (a.clock_probe) {
-    clk0 = (long long)__builtin_amdgcn_s_memtime();
-    rt0 = (long long)__builtin_amdgcn_s_memrealtime();
-  }
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const long long ldw3 = 3LL * a.K;
   const uint16_t* __restrict__ Wg = a.W3 + (long long)g * a.strideW3 + (long long)tn * TL::BN * ldw3;
@@ -471,26 +351,18 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
   const int wm = wave / TL::WN, wn = wave % TL::WN;
   const int li = lane & 31, lh = lane >> 5;
 
-  // staging maps: A chunk q = t + NT*j -> row q / CPR, k 4*(q % CPR) (granule (q%CPR)/4);
-  // W chunk q -> row q / (6*NSUB), 16-B piece p = q % (6*NSUB), stored in the image's order
-  using AP = std::conditional_t<TL::ALIMB, const uint16_t*, const float*>;
-  using AR = std::conditional_t<TL::ALIMB, u32x4, f32x4>;
-  AP a_src[VA];
+  // staging maps: A chunk q = t + NT*j -> row q / CPR, k 4*(q % CPR);
+  // W chunk q -> row q / 6, 16-B piece p = q % 6, stored in the image's order
+  const float* a_src[VA];
   int a_dst[VA];
   bool a_ok[VA];
 #pragma unroll
   for (int j = 0; j < VA; ++j) {
     const int q = t + NT * j;
     a_ok[j] = (TL::NA % NT == 0 || j + 1 < VA) ? true : q < TL::NA;  // compile-time true but for a ragged last pass
-    if constexpr (TL::ALIMB) {
-      const int r = a_ok[j] ? q / (6 * NSUB) : 0, p = q % (6 * NSUB);
-      a_src[j] = a.A3 + (long long)g * a.strideA3 + ((long long)tm * BM + r) * 3LL * a.lda + p * 8;
-      a_dst[j] = r * LD + p * 8;
-    } else {
-      const int r = a_ok[j] ? q / CPR : 0, c = q % CPR;
-      a_src[j] = Ag + (long long)r * a.lda + 4 * c;
-      a_dst[j] = r * LD + (c >> 2) * 48 + (c & 3) * 4;
-    }
+    const int r = a_ok[j] ? q / CPR : 0, c = q % CPR;
+    a_src[j] = Ag + (long long)r * a.lda + 4 * c;
+    a_dst[j] = r * LD + c * 4;
   }
   const uint16_t* w_src[VW];
   int w_dst[VW];
@@ -499,13 +371,13 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
   for (int j = 0; j < VW; ++j) {
     const int q = t + NT * j;
     w_ok[j] = (TL::NW % NT == 0 || j + 1 < VW) ? true : q < TL::NW;
-    const int r = w_ok[j] ? q / (6 * NSUB) : 0, p = q % (6 * NSUB);
+    const int r = w_ok[j] ? q / 6 : 0, p = q % 6;
     w_src[j] = Wg + (long long)r * ldw3 + p * 8;
     w_dst[j] = BM * LD + r * LD + p * 8;
   }
 
-  AR ra[TL::PF][VA];
-  u32x4 rw[TL::PF][VW];
+  f32x4 ra[VA];
+  u32x4 rw[VW];
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -515,132 +387,66 @@ __device__ __forceinline__ void gemm_tile_x6(const GemmArgs& a, int orig) {
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   const int nk = a.K / BK;
-  auto load = [&](auto set, int kt) {
-    constexpr int S = decltype(set)::value;
+  auto load = [&](int kt) {
     kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
 #pragma unroll
     for (int j = 0; j < VA; ++j)
-      if (a_ok[j]) {
-        if constexpr (TL::ALIMB) ra[S][j] = *reinterpret_cast<const u32x4*>(a_src[j] + kt * 48 * NSUB);
-        else ra[S][j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
-      }
+      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(a_src[j] + kt * BK);
 #pragma unroll
     for (int j = 0; j < VW; ++j)
-      if (w_ok[j]) rw[S][j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 48 * NSUB);
+      if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 48);
   };
-  auto publish = [&](auto set, int base) {
-    constexpr int S = decltype(set)::value;
+  auto publish = [&](int base) {
 #pragma unroll
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) {
-        if constexpr (TL::ALIMB) {
-          *reinterpret_cast<u32x4*>(sm + base + a_dst[j]) = ra[S][j];
-        } else {
-          u32x2 l0, l1, l2;
-          split3(ra[S][j], l0, l1, l2);
-          *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
-          *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
-          *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 32) = l2;
-        }
+        u32x2 l0, l1, l2;
+        split3(ra[j], l0, l1, l2);
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 32) = l2;
       }
 #pragma unroll
     for (int j = 0; j < VW; ++j)
-      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[S][j];
+      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
   };
   const int a_off = (wm * TM * 32 + li) * LD + lh * 8;
   const int w_off = BM * LD + (wn * TN * 32 + li) * LD + lh * 8;
   auto compute = [&](int base) {
     const uint16_t* As = sm + base + a_off;
     const uint16_t* Ws = sm + base + w_off;
+    bf16x8 fa[TM][3], fb[TN][3];
 #pragma unroll
-    for (int sub = 0; sub < NSUB; ++sub) {
-      bf16x8 fa[TM][3], fb[TN][3];
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int l = 0; l < 3; ++l) fa[m][l] = *reinterpret_cast<const bf16x8*>(As + m * 32 * LD + l * 16);
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+#pragma unroll
+      for (int l = 0; l < 3; ++l) fb[n][l] = *reinterpret_cast<const bf16x8*>(Ws + n * 32 * LD + l * 16);
+    // small terms first: (a2,b0) (a0,b2) (a1,b1) (a1,b0) (a0,b1) (a0,b0)
+    constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
 #pragma unroll
       for (int m = 0; m < TM; ++m)
 #pragma unroll
-        for (int l = 0; l < 3; ++l)
-          fa[m][l] = *reinterpret_cast<const bf16x8*>(As + m * 32 * LD + sub * 48 + l * 16);
-#pragma unroll
-      for (int n = 0; n < TN; ++n)
-#pragma unroll
-        for (int l = 0; l < 3; ++l)
-          fb[n][l] = *reinterpret_cast<const bf16x8*>(Ws + n * 32 * LD + sub * 48 + l * 16);
-      // small terms first: (a2,b0) (a0,b2) (a1,b1) (a1,b0) (a0,b1) (a0,b0)
-      constexpr int PA[6] = {2, 0, 1, 1, 0, 0}, PB[6] = {0, 2, 1, 0, 1, 0};
-#pragma unroll
-      for (int p = 0; p < 6; ++p)
-#pragma unroll
-        for (int m = 0; m < TM; ++m)
-#pragma unroll
-          for (int n = 0; n < TN; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
-    }
+        for (int n = 0; n < TN; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[m][PA[p]], fb[n][PB[p]], acc[m][n], 0, 0, 0);
   };
 
-  if constexpr (TL::STAGES == 1) {
-    load(IC<0>{}, 0);
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt > 0) __syncthreads();  // everyone finished reading tile kt-1
-      publish(IC<0>{}, 0);
-      __syncthreads();
-      load(IC<0>{}, kt + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(0);
-    }
-    __syncthreads();  // the epilogue may reuse the LDS
-  } else if constexpr (TL::LATE) {
-    load(IC<0>{}, 0);
-    publish(IC<0>{}, 0);
-    load(IC<0>{}, 1);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      __syncthreads();  // tile kt visible in buffer cur; everyone is done reading buffer cur^1
-      publish(IC<0>{}, (cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
-      load(IC<0>{}, kt + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cur * STAGE);
-    }
-    __syncthreads();  // the epilogue may reuse the LDS
-  } else if constexpr (TL::PF == 1) {
-    load(IC<0>{}, 0);
-    publish(IC<0>{}, 0);
+  load(0);
+  publish(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    load(kt + 1);
+    // keep the prefetch ahead of the MFMA block (hipcc otherwise sinks the loads to their
+    // consumer, the LDS store after the MFMAs)
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cur * STAGE);
+    publish((cur ^ 1) * STAGE);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      load(IC<0>{}, kt + 1);
-      // keep the prefetch ahead of the MFMA block (hipcc otherwise sinks the loads to
-      // their consumer, the LDS store after the MFMAs)
-      __builtin_amdgcn_sched_barrier(0);
-      compute(cur * STAGE);
-      publish(IC<0>{}, (cur ^ 1) * STAGE);
-      __syncthreads();
-    }
-  } else {
-    // two register sets: tile kt+2 is in flight while kt+1 is published and kt computed
-    load(IC<0>{}, 0);
-    publish(IC<0>{}, 0);
-    load(IC<1>{}, 1);
-    __syncthreads();
-    auto iter = [&](auto ldset, auto pubset, int kt) {
-      load(ldset, kt + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      compute((kt & 1) * STAGE);
-      publish(pubset, ((kt & 1) ^ 1) * STAGE);
-      __syncthreads();
-    };
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-      iter(IC<0>{}, IC<1>{}, kt);
-      iter(IC<1>{}, IC<0>{}, kt + 1);
-    }
-    if (kt < nk) iter(IC<0>{}, IC<1>{}, kt);
-  }
-
-  if (a.clock_probe && threadIdx.x == 0) {
-    long long* p = a.clock_probe + 4LL * orig;
-    p[0] = clk0; p[1] = rt0;
-    p[2] = (long long)__builtin_amdgcn_s_memtime();
-    p[3] = (long long)__builtin_amdgcn_s_memrealtime();
   }
   epilogue<EPI, TL>(a, acc, g, tm, tn);
 }
@@ -847,7 +653,7 @@ __device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc
           const int row = row0 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
           float v = __builtin_amdgcn_ldexpf(acc[m][n][e], er[e] + ec[n]) + bv[n];
           if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
-          if (!a.abl_nostore || v == 1234.5f) Cg[(long long)row * a.ldc + a.col_off + col] = v;
+          Cg[(long long)row * a.ldc + a.col_off + col] = v;
           const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
           mx[e] = mx[e] > b ? mx[e] : b;
         }
@@ -982,7 +788,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
           const int row = row0 + m * 16 + 4 * lq + j;
           float v = __builtin_amdgcn_ldexpf(acc[m][n][j], er[j] + ec[n]) + bv[n];
           if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
-          if (!a.abl_nostore || v == 1234.5f) Cg[(long long)row * a.ldc + a.col_off + col] = v;
+          Cg[(long long)row * a.ldc + a.col_off + col] = v;
           const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
           mx[m * 4 + j] = mx[m * 4 + j] > b ? mx[m * 4 + j] : b;
         }
@@ -1028,11 +834,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
   }
 }
 
-// ABL != 0: ablations for the timing study only (tools/h3_variants.py, variants 91..95; wrong
-// results by design): 1 every K-tile loads tile 0 (L2-hot operands), 2 no barrier in the
-// loop, 3 A staged without the split (limb1 = limb0), 4 no loads / LDS writes in the loop,
-// 5 = 4 without the barrier (the bare fragment-read + MFMA loop)
-template <int EPI, class TL, int ABL = 0>
+template <int EPI, class TL>
 __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
   constexpr int NT = TL::NT, STAGE = TL::STAGE;
@@ -1041,11 +843,6 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   int* sExp = reinterpret_cast<int*>(sm + TL::SEXP);
   int g, tm, tn;
   map_tile(a, blockIdx.x, g, tm, tn);
-  long long clk0 = 0, rt0 = 0, rt1 = 0, clk1 = 0;  // clock probe (diagnostics: tools/h3_clock.py)
-  if (a.clock_probe) {
-    clk0 = (long long)__builtin_amdgcn_s_memtime();
-    rt0 = (long long)__builtin_amdgcn_s_memrealtime();
-  }
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const float* __restrict__ Ag0 = a.A + (long long)tm * BM * a.lda;  // group 0: the shared K slice
   const long long ldw2 = 2LL * a.K;
@@ -1125,7 +922,6 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   const int nk = a.K / BK;
   auto load = [&](int kt) {
     kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
-    if constexpr (ABL == 1) kt = 0;
     const float* Ab = kt < nks ? Ag0 : Ag;
 #pragma unroll
     for (int j = 0; j < VA; ++j)
@@ -1139,14 +935,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) {
         f32x4 x = ra[j];
-        u32x2 l0, l1;
-        if constexpr (ABL == 3) {
-          l0 = l1 = __builtin_bit_cast(u32x2, __builtin_convertvector(x, f16x4));
-        } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
-          split2(x, l0, l1);
-        }
+        for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
+        u32x2 l0, l1;
+        split2(x, l0, l1);
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
       }
@@ -1298,7 +1090,6 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     load(0);
     publish(0);
     load(1);
-    if (a.prio == 2 && __builtin_amdgcn_readfirstlane(threadIdx.x) >= NT / 2) __builtin_amdgcn_s_setprio(1);
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       __syncthreads();  // tile kt visible in buffer cur; buffer cur^1 (tile kt-1) fully read
@@ -1315,23 +1106,9 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       publish((cur ^ 1) * STAGE);  // tile kt+1 (past the end: a harmless re-publish)
       load(kt + 2);
       __builtin_amdgcn_sched_barrier(0);
-      if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
       compute(cur * STAGE);
-      if (a.prio == 1) __builtin_amdgcn_s_setprio(0);
-    }
-    if (a.clock_probe) {
-      clk1 = (long long)__builtin_amdgcn_s_memtime();
-      rt1 = (long long)__builtin_amdgcn_s_memrealtime();
     }
     finish(acc);
-    if (a.clock_probe) {  // per WG: start, main-loop end, epilogue end (stores drained), loop clocks
-      __builtin_amdgcn_s_waitcnt(0);
-      const long long rt2 = (long long)__builtin_amdgcn_s_memrealtime();
-      if (threadIdx.x == 0) {
-        long long* p = a.clock_probe + 4LL * blockIdx.x;
-        p[0] = rt0; p[1] = rt1; p[2] = rt2; p[3] = clk1 - clk0;
-      }
-    }
     return;
   }
   load(0);
@@ -1339,11 +1116,11 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if constexpr (ABL != 4 && ABL != 5) load(kt + 1);
+    load(kt + 1);
     __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the MFMA block
     compute(cur * STAGE);
-    if constexpr (ABL != 4 && ABL != 5) publish((cur ^ 1) * STAGE);
-    if constexpr (ABL != 2 && ABL != 5) __syncthreads();
+    publish((cur ^ 1) * STAGE);
+    __syncthreads();
   }
   finish(acc);
 }
@@ -1410,81 +1187,52 @@ __global__ __launch_bounds__(256) void k_row_exp(const float* __restrict__ A, in
   if (lane < n_slots) re[(long long)lane * rows] = lane == 0 ? exp_of_bits(mx) : -100;
 }
 
-using H256w8 = TileH3<2, 4, 4, 2>;      // 256x256, 8 waves of 128x64 (83 KB): 1 WG / CU
-using H128 = TileH3<2, 2, 2, 2>;        // 128x128, 4 waves of 64x64 (41 KB): 2+ WGs / CU
-using H128x224w14 = TileH3<2, 7, 2, 1, 4>;  // 128x224 output layer, 14 waves of 64x32
-using H256w8k32 = TileH3<2, 4, 4, 2, 2, 2>;  // 256x256, BK 32 (148 KB)
-using H256w16 = TileH3<4, 4, 2, 2, 4>;       // 256x256, 16 waves of 64x64
-using H256x128 = TileH3<2, 2, 4, 2, 2>;      // 256x128, 4 waves of 128x64 (62 KB): 2 WGs / CU
-using H128x256 = TileH3<2, 2, 2, 4, 2>;      // 128x256, 4 waves of 64x128
-using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;    // 128x128, BK 32 (74 KB): 2 WGs / CU
-using H256x128k32 = TileH3<2, 2, 4, 2, 1, 2>;  // 256x128, BK 32 (111 KB): 1 WG / CU
-using H128x224k32 = TileH3<2, 7, 2, 1, 4, 2>;  // output layer, BK 32
-using H128x224w4k32 = TileH3<4, 1, 1, 7, 1, 2>;  // output layer, 4 waves of 32x224, BK 32
-using H128x224w4 = TileH3<4, 1, 1, 7, 2, 1>;     // output layer, 4 waves of 32x224, BK 16 (56 KB)
-using H128x224w7k32 = TileH3<1, 7, 4, 1, 2, 2>;  // output layer, 7 waves of 128x32, BK 32
-using H128x256w8k32 = TileH3<2, 4, 2, 2, 2, 2>;  // output layer on N padded to 256: 8 waves of 64x64, BK 32
-using H128x256w8 = TileH3<2, 4, 2, 2, 4, 1>;     //   same, BK 16 (61 KB: 2 WGs / CU)
-using H128x256w4k32 = TileH3<2, 2, 2, 4, 2, 2>;  //   4 waves of 64x128, BK 32
-using H128x256w8k32late = TileH3<2, 4, 2, 2, 2, 2, true>;
-using H128x224k32late = TileH3<2, 7, 2, 1, 4, 2, true>;  // output layer, 14 waves, BK 32, write-after-barrier
-using H128x256w16k32late = TileH3<4, 4, 1, 2, 4, 2, true>;  // N padded to 256: 16 waves of 32x64
-using H256w16k32 = TileH3<4, 4, 2, 2, 4, 2>;     // 256x256, 16 waves of 64x64, BK 32
-using H256w8k32late = TileH3<2, 4, 4, 2, 2, 2, true>;  // H256w8k32, write-after-barrier schedule
-using H256w16k32late = TileH3<4, 4, 2, 2, 4, 2, true>;  // H256w16k32, write-after-barrier schedule
-using H256w16k32lateM = TileH3<4, 4, 2, 2, 4, 2, true, true, true>;  // same on 16x16x32 MFMAs
-using H128x224k32lateM = TileH3<2, 7, 2, 1, 4, 2, true, true, true>;
-using H256w8k32lateM = TileH3<2, 4, 4, 2, 2, 2, true, true, true>;  // 8 waves of 128x64, 16x16x32
-using H256w8k32lateMP = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true>;  // + pinned fragment reads
-using H256w8k32lateMPE = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true>;  // + early first reads
-using H256w8k32lateMPES = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;  // + split staging
-using H128x224k32lateMPE = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true>;  // output, 16x16x32
-using H128x224k32lateMPES = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true>;
-using H128x256w8k32lateMPES = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
-using H128x256w8k32lateMPE = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true>;  // S = 226 output
-using H128x224k32lateP = TileH3<2, 7, 2, 1, 4, 2, true, true, false, 0, 0, true>;
-using H128k32late = TileH3<2, 2, 2, 2, 2, 2, true>;
-using H128k32lateP = TileH3<2, 2, 2, 2, 2, 2, true, true, false, 0, 0, true>;
-using H128k32lateMPES = TileH3<2, 2, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;  // RFF, 16x16x32
-using H128k32P = TileH3<2, 2, 2, 2, 2, 2, false, true, false, 0, 0, true>;
-using H128x256w8k32lateM = TileH3<2, 4, 2, 2, 2, 2, true, true, true>;  // output on N padded to 256, 16x16x32
-using H128x224w8k32lateM = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 2, 7>;  // output: 8 waves of 32x112, 16x16x32
+// The tiles the launchers pick (chosen by same-process A/B runs in round 1: DESIGN.md §3.0,
+// profiles/r01_h3_*.txt):
+//   hidden layers, grid >= one WG per CU: 256x256, BK 32, 8 waves of 128x64 on 16x16x32,
+//     write-after-barrier with pinned / early fragment reads and split staging (160 KB LDS)
+//   otherwise (and the RFF features): 128x128, BK 32, 4 waves of 64x64 on 32x32x16
+//   output layer S <= 224: 128x224, 14 waves of 64x32 on 16x16x32 (same schedule);
+//     S in (224, 256]: 128x256, 8 waves of 64x64
+using H256 = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
+using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;
+using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
+using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true>;
+using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
+using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 
-using X128 = TileX6<2, 2, 2, 2>;          // 128x128, 4 waves of 64x64, BK 16, 57 KB LDS: 2 WGs / CU
-using X128x224 = TileX6<1, 7, 4, 1>;       // 128x224 output layer (S <= 224), 7 waves of 128x32
-using X128x224o4 = TileX6<1, 7, 4, 1, 1, 2, 1, 4>;  // same, <= 128 VGPRs: two WGs (14 waves) per CU
-using X128x224w14 = TileX6<2, 7, 2, 1, 1, 2, 1, 4>; // 128x224, 14 waves of 64x32
-using X128pf2 = TileX6<2, 2, 2, 2, 1, 2, 2>;  // two K-tiles in registers ahead
-using X128k32s1 = TileX6<2, 2, 2, 2, 2, 1>;   // BK 32, single LDS buffer (53 KB), 2 barriers / K-tile
-using X128k32 = TileX6<2, 2, 2, 2, 2, 2, 1, 1>;  // BK 32 double-buffered (106 KB): 1 WG / CU
-using X128x256w8 = TileX6<2, 4, 2, 2, 1, 2, 1, 2>;  // 128x256, 8 waves of 64x64 (86 KB): 1 WG / CU
-using X256x128w8 = TileX6<4, 2, 2, 2, 1, 2, 1, 2>;  // 256x128, 8 waves of 64x64
-using X128x256 = TileX6<2, 2, 2, 4, 1, 2, 1, 1>;    // 128x256, 4 waves of 64x128
-using X128a = TileX6<2, 2, 2, 2, 1, 2, 1, 2, true>;  // X128 on pre-split activations
-using X128x256w8a = TileX6<2, 4, 2, 2, 1, 2, 1, 2, true>;
-using X256w8 = TileX6<2, 4, 4, 2, 1, 2, 1, 2>;    // 256x256, 8 waves of 128x64 (115 KB): 1 WG / CU
-using X256w16 = TileX6<4, 4, 2, 2, 1, 2, 1, 4>;   // 256x256, 16 waves of 64x64
-using X256x128 = TileX6<2, 2, 4, 2, 1, 2, 1, 1>;  // 256x128, 4 waves of 128x64
-using X256w8pf2 = TileX6<2, 4, 4, 2, 1, 2, 2, 2>;  // + two K-tiles in registers
-using X256w8k32 = TileX6<2, 4, 4, 2, 2, 1, 1, 2>;  // BK 32, single LDS buffer (106 KB)
-using X256w8late = TileX6<2, 4, 4, 2, 1, 2, 1, 2, false, true>;
-using X128late = TileX6<2, 2, 2, 2, 1, 2, 1, 2, false, true>;
-const uint16_t* g_x6_a3 = nullptr;  // amx__set_x6_a3: pre-split activation image (A/B only)
-long long g_x6_a3_stride = 0;
+using X128 = TileX6<2, 2, 2, 2>;        // 128x128, 4 waves of 64x64 (57 KB): 2 WGs / CU
+using X256 = TileX6<2, 4, 4, 2>;        // 256x256, 8 waves of 128x64 (115 KB): 1 WG / CU
+using X128x224 = TileX6<2, 7, 2, 1, 4>; // output layer (S <= 224), 14 waves of 64x32
 
-int g_x6_variant = -1;      // amx__set_x6_variant: hidden-layer tile (-1 automatic)
-int g_x6_out_variant = -1;  // amx__set_x6_out_variant: output-layer tile (-1 automatic)
+using T128 = Tile<2, 2, 2, 2>;          // 128x128, 256 threads, 2 WGs / CU
+using T128x224 = Tile<4, 1, 1, 7>;      // 128x224, 256 threads, wave 32x224 (output layer, S <= 224)
 
-int resident_wgs(size_t lds, int nt, int occ);
+// workgroups of a tile shape resident on the context's device at once
+int resident_wgs(const amx_ctx* ctx, size_t lds, int nt, int occ) {
+  const int by_lds = (int)((160 * 1024) / lds);
+  const int by_waves = (occ * 4) / (nt / 64);
+  const int per_cu = by_lds < by_waves ? by_lds : by_waves;
+  return (per_cu < 1 ? 1 : per_cu) * ctx->n_cus;
+}
+
+template <int EPI, class TL>
+int launch_nt(GemmArgs& a, hipStream_t stream) {
+  a.tiles_m = a.rows / TL::BM;
+  a.tiles_n = a.N / TL::BN;
+  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+  if (nwg == 0) return AMX_OK;
+  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
 
 template <int EPI, class TL>
 int launch_x6(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
   a.tiles_n = a.N / TL::BN;
-  a.clock_probe = g_clock_probe;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  a.clock_probe = g_clock_probe;
   // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
   constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
   hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
@@ -1492,122 +1240,16 @@ int launch_x6(GemmArgs& a, hipStream_t stream) {
   return AMX_OK;
 }
 
-template <int EPI>
-int launch_x6_variant(int v, GemmArgs& a, hipStream_t s) {
-  const bool m256 = a.rows % 256 == 0, n256 = a.N % 256 == 0;
-  switch (v) {
-    case 1: return launch_x6<EPI, X128pf2>(a, s);
-    case 2: return launch_x6<EPI, X128k32s1>(a, s);
-    case 3: return launch_x6<EPI, X128k32>(a, s);
-    case 4: if (n256) return launch_x6<EPI, X128x256w8>(a, s); break;
-    case 5: if (m256) return launch_x6<EPI, X256x128w8>(a, s); break;
-    case 6: if (n256) return launch_x6<EPI, X128x256>(a, s); break;
-    case 9: if (m256 && n256) return launch_x6<EPI, X256w8>(a, s); break;
-    case 10: if (m256 && n256) return launch_x6<EPI, X256w16>(a, s); break;
-    case 11: if (m256) return launch_x6<EPI, X256x128>(a, s); break;
-    case 12: if (m256 && n256) return launch_x6<EPI, X256w8pf2>(a, s); break;
-    case 13: if (m256 && n256) return launch_x6<EPI, X256w8k32>(a, s); break;
-    case 14: if (m256 && n256) return launch_x6<EPI, X256w8late>(a, s); break;
-    case 15: return launch_x6<EPI, X128late>(a, s);
-    case 7: if (g_x6_a3) { a.A3 = g_x6_a3; a.strideA3 = g_x6_a3_stride; return launch_x6<EPI, X128a>(a, s); } break;
-    case 8: if (g_x6_a3 && n256) { a.A3 = g_x6_a3; a.strideA3 = g_x6_a3_stride; return launch_x6<EPI, X128x256w8a>(a, s); } break;
-    case 0: return launch_x6<EPI, X128>(a, s);
-    default: break;
-  }
-  // automatic: the 256x256 tile (8 waves of 128x64, one WG per CU) halves the operand bytes
-  // staged per MFMA against 128x128 and is 10-14% faster per hidden layer when its grid
-  // still fills the chip (tools/x6_variants.py); otherwise 128x128 (2 WGs per CU).
-  if (m256 && n256 && (long long)(a.rows / 256) * (a.N / 256) * a.groups >= resident_wgs(X256w8::LDS, X256w8::NT, 2))
-    return launch_x6<EPI, X256w8>(a, s);
-  return launch_x6<EPI, X128>(a, s);
-}
-
-// ---- tile selection -------------------------------------------------------------------------
-using T128 = Tile<2, 2, 2, 2>;        // 128x128, 256 threads, 2 WGs / CU
-using T128x256 = Tile<2, 2, 2, 4>;    // 128x256, 256 threads, wave 64x128
-using T128x256w8 = Tile<2, 4, 2, 2>;  // 128x256, 512 threads, wave 64x64
-using T256 = Tile<4, 2, 2, 4>;        // 256x256, 512 threads, wave 64x128
-using T256x128 = Tile<4, 2, 2, 2>;    // 256x128, 512 threads, wave 64x64
-using T128x224 = Tile<4, 1, 1, 7>;    // 128x224, 256 threads, wave 32x224 (output layer, S <= 224)
-using T128s1 = Tile<2, 2, 2, 2, 1, 4>;    // 128x128, single-buffered LDS (37 KB): 4 WGs / CU
-using T128x256s1 = Tile<2, 4, 2, 2, 1, 2>;  // 128x256, 8 waves, single-buffered (55 KB): 2 WGs / CU
-using T256x128p = Tile<2, 2, 4, 2, 2, 1, true>;  // 256x128, 4 waves of 128x64, pipelined, 1 wave/SIMD
-
-int g_variant = -1;  // -1: automatic; >= 0 forces a tile for A/B tests (amx__set_gemm_variant)
-int g_persistent = 0;  // amx__set_gemm_persistent: loop workgroups over tiles (A/B)
-int g_cus = 0;         // compute units of the current device (queried once)
-
-int resident_wgs(size_t lds, int nt, int occ) {
-  if (g_cus == 0) {
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      g_cus = prop.multiProcessorCount;
-    if (g_cus <= 0) g_cus = 256;
-  }
-  const int by_lds = (int)((160 * 1024) / lds);
-  const int by_waves = (occ * 4) / (nt / 64);
-  const int per_cu = by_lds < by_waves ? by_lds : by_waves;
-  return (per_cu < 1 ? 1 : per_cu) * g_cus;
-}
-
 template <int EPI, class TL>
-int launch_tile(GemmArgs& a, hipStream_t stream) {
+int launch_h3(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
   a.tiles_n = a.N / TL::BN;
-  a.clock_probe = g_clock_probe;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  int grid = nwg;
-  if (g_persistent && EPI != EPI_RFF) {
-    const int slots = resident_wgs(TL::LDS, TL::NT, TL::OCC) / 8 * 8;
-    if (slots >= 8 && slots < nwg) grid = slots;
-  }
-  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(grid), dim3(TL::NT), TL::LDS, stream, a);
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
+  hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
-}
-
-template <int EPI>
-int launch_variant(int v, GemmArgs& a, hipStream_t s) {
-  switch (v) {
-    case 1: return launch_tile<EPI, T128x256>(a, s);
-    case 2: return launch_tile<EPI, T128x256w8>(a, s);
-    case 3: return launch_tile<EPI, T256>(a, s);
-    case 4: return launch_tile<EPI, T256x128>(a, s);
-    case 5: return launch_tile<EPI, T128s1>(a, s);
-    case 6: return launch_tile<EPI, T128x256s1>(a, s);
-    case 9: return launch_tile<EPI, T256x128p>(a, s);
-    default: return launch_tile<EPI, T128>(a, s);
-  }
-}
-
-bool variant_fits(int v, const GemmArgs& a) {
-  const int bm = (v == 3 || v == 4 || v == 9) ? 256 : 128;
-  const int bn = (v == 1 || v == 2 || v == 3 || v == 6) ? 256 : 128;
-  return a.rows % bm == 0 && a.N % bn == 0;
-}
-
-int launch_gemm(int epi, GemmArgs& a, hipStream_t stream) {
-  if (epi == EPI_RFF) return launch_tile<EPI_RFF, T128>(a, stream);
-  if (epi == EPI_UNNORM) {
-    const int n32 = amx::round_up(a.n_valid, 32);
-    if (g_variant < 0 && n32 > 128 && n32 <= 224) {  // one 224-wide tile instead of two 128s
-      a.N = 224;
-      return launch_tile<EPI_UNNORM, T128x224>(a, stream);
-    }
-    a.N = amx::round_up(a.n_valid, 128);
-    const int v = (g_variant >= 0 && variant_fits(g_variant, a)) ? g_variant : 0;
-    return launch_variant<EPI_UNNORM>(v, a, stream);
-  }
-  // automatic: 128x128, 4 waves of 64x64, two WGs per CU.  Its main loop keeps the MFMA
-  // pipe busy 93-95% of cycles (tools/gemm_clock.py) and is then power-limited (the chip
-  // holds 2.1-2.3 GHz under it); the 1-WG/CU tiles (256x128, 128x256, 256x256, pipelined
-  // one-wave-per-SIMD) run at 2.38 GHz but only 82-87% busy.  Net, across four boxes:
-  // 128x128 ahead by 4% on two, behind by 1.5% on two (tools/gemm_variants.py, same process).
-  int v = g_variant < 0 ? 0 : g_variant;
-  if (!variant_fits(v, a)) v = 0;
-  return launch_variant<EPI_BIAS_ACT>(v, a, stream);
 }
 
 int check_common(const char* fn, int groups, int rows, int K, const float* A, int lda, const float* W,
@@ -1623,28 +1265,36 @@ int check_common(const char* fn, int groups, int rows, int K, const float* A, in
   return AMX_OK;
 }
 
+int check_x6(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W3,
+             long long strideW3) {
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
+  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
+                AMX_ROW_TILE);
+  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, XBK);
+  AMX_CHECK_ARG(A && W3 && amx::aligned16(A) && amx::aligned16(W3), "%s: null/unaligned operand", fn);
+  AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
+  AMX_CHECK_ARG(strideW3 % 8 == 0, "%s: strideW3=%lld must be a multiple of 8", fn, strideW3);
+  return AMX_OK;
+}
+
+int check_h3(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W2,
+             long long strideW2, const int* w_exp, const int* row_exp, int rexp_slots, int k_shared = 0) {
+  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
+  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
+                AMX_ROW_TILE);
+  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, XBK);
+  AMX_CHECK_ARG(A && W2 && amx::aligned16(A) && amx::aligned16(W2), "%s: null/unaligned operand", fn);
+  AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
+  AMX_CHECK_ARG(strideW2 % 8 == 0, "%s: strideW2=%lld must be a multiple of 8", fn, strideW2);
+  AMX_CHECK_ARG(w_exp && row_exp && rexp_slots >= 1, "%s: null exponents or rexp_slots=%d", fn, rexp_slots);
+  AMX_CHECK_ARG(k_shared >= 0 && k_shared <= K && k_shared % 32 == 0,
+                "%s: k_shared=%d must be a multiple of 32 in [0, K=%d]", fn, k_shared, K);
+  return AMX_OK;
+}
+
 }  // namespace
 
-// Internal (not in the public header): force a tile variant for A/B measurements.
-extern "C" int amx__set_gemm_variant(int v) {
-  g_variant = v;
-  return AMX_OK;
-}
-
-// Internal: persistent workgroups (1) or one workgroup per tile (0), for A/B measurements.
-extern "C" int amx__set_gemm_persistent(int on) {
-  g_persistent = on;
-  return AMX_OK;
-}
-
-// Internal: device buffer of >= 4 * n_tiles int64 receiving each workgroup's
-// {s_memtime, s_memrealtime} at start and at the end of its main loop (shader clock =
-// cycles / (realtime ticks / 100 MHz)); nullptr disables.
-extern "C" int amx__set_gemm_clock_probe(long long* buf) {
-  g_clock_probe = buf;
-  return AMX_OK;
-}
-
+// ---- f32 MFMA entry points ------------------------------------------------------------------
 extern "C" int amx_gemm_bias_act(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
                                  long long strideA, const float* W, int ldw, long long strideW,
                                  const float* bias, long long strideBias, float* C, int ldc, long long strideC,
@@ -1662,7 +1312,9 @@ extern "C" int amx_gemm_bias_act(amx_ctx* ctx, int groups, int rows, int N, int 
   a.bias = bias; a.strideBias = strideBias;
   a.C = C; a.strideC = strideC; a.ldc = ldc; a.col_off = col_off;
   a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
-  return launch_gemm(EPI_BIAS_ACT, a, (hipStream_t)stream);
+  // 128x128, 4 waves of 64x64, two WGs per CU: the main loop keeps the MFMA pipe busy 93-95%
+  // of cycles and is then power-limited
+  return launch_nt<EPI_BIAS_ACT, T128>(a, (hipStream_t)stream);
 }
 
 extern "C" int amx_gemm_out_unnorm(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
@@ -1684,7 +1336,13 @@ extern "C" int amx_gemm_out_unnorm(amx_ctx* ctx, int groups, int rows, int n_val
   const int S = ctx->S, Ad = ctx->A;
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
-  return launch_gemm(EPI_UNNORM, a, (hipStream_t)stream);
+  const int n32 = amx::round_up(a.n_valid, 32);
+  if (n32 > 128 && n32 <= 224) {  // one 224-wide tile instead of two 128s
+    a.N = 224;
+    return launch_nt<EPI_UNNORM, T128x224>(a, (hipStream_t)stream);
+  }
+  a.N = amx::round_up(a.n_valid, 128);
+  return launch_nt<EPI_UNNORM, T128>(a, (hipStream_t)stream);
 }
 
 extern "C" int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
@@ -1703,27 +1361,10 @@ extern "C" int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int 
   a.C = phi; a.ldc = ldphi;
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
-  return launch_gemm(EPI_RFF, a, (hipStream_t)stream);
+  return launch_nt<EPI_RFF, T128>(a, (hipStream_t)stream);
 }
 
 // ---- bf16x6 entry points ----------------------------------------------------------------
-// Internal (not in the public header): force the x6 tile of the hidden layers / of the
-// output layer (0: 128x224 where S fits, k >= 1: hidden-layer variant k-1 on N padded to
-// 128) for A/B measurements.
-extern "C" int amx__set_x6_variant(int v) {
-  g_x6_variant = v;
-  return AMX_OK;
-}
-extern "C" int amx__set_x6_a3(const uint16_t* a3, long long stride) {
-  g_x6_a3 = a3;
-  g_x6_a3_stride = stride;
-  return AMX_OK;
-}
-extern "C" int amx__set_x6_out_variant(int v) {
-  g_x6_out_variant = v;
-  return AMX_OK;
-}
-
 extern "C" int amx_split_bf16x3(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw,
                                 long long strideW, uint16_t* W3, long long strideW3, void* stream) {
   AMX_CHECK_ARG(ctx, "amx_split_bf16x3: null ctx");
@@ -1737,18 +1378,6 @@ extern "C" int amx_split_bf16x3(amx_ctx* ctx, int groups, int rows, int K, const
   hipLaunchKernelGGL(k_split_bf16x3, dim3((unsigned)((n + 255) / 256), groups), dim3(256), 0, (hipStream_t)stream, W,
                      ldw, strideW, rows, K, W3, strideW3);
   AMX_CHECK_LAUNCH();
-  return AMX_OK;
-}
-
-static int check_x6(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W3,
-                    long long strideW3) {
-  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
-  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
-                AMX_ROW_TILE);
-  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, XBK);
-  AMX_CHECK_ARG(A && W3 && amx::aligned16(A) && amx::aligned16(W3), "%s: null/unaligned operand", fn);
-  AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
-  AMX_CHECK_ARG(strideW3 % 8 == 0, "%s: strideW3=%lld must be a multiple of 8", fn, strideW3);
   return AMX_OK;
 }
 
@@ -1770,7 +1399,13 @@ extern "C" int amx_gemm_bias_act_x6(amx_ctx* ctx, int groups, int rows, int N, i
   a.bias = bias; a.strideBias = strideBias;
   a.C = C; a.strideC = strideC; a.ldc = ldc; a.col_off = col_off;
   a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
-  return launch_x6_variant<EPI_BIAS_ACT>(g_x6_variant, a, (hipStream_t)stream);
+  const hipStream_t s = (hipStream_t)stream;
+  // the 256x256 tile halves the operand bytes staged per MFMA against 128x128 (10-14% per
+  // hidden layer) when its grid still fills the chip; otherwise 128x128 (2 WGs per CU)
+  if (rows % 256 == 0 && N % 256 == 0 &&
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(ctx, X256::LDS, X256::NT, 2))
+    return launch_x6<EPI_BIAS_ACT, X256>(a, s);
+  return launch_x6<EPI_BIAS_ACT, X128>(a, s);
 }
 
 extern "C" int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
@@ -1792,19 +1427,16 @@ extern "C" int amx_gemm_out_unnorm_x6(amx_ctx* ctx, int groups, int rows, int n_
   const int S = ctx->S, Ad = ctx->A;
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
-  // weight rows are padded to round_up(S, 128) (the f32 path's layout, amx_layout n_out_pad)
+  // weight rows are padded to round_up(S, 128) (amx_layout n_out_pad)
   const int n32 = amx::round_up(n_valid, 32);
-  if ((g_x6_out_variant < 0 || g_x6_out_variant == 0 || g_x6_out_variant >= 100) && n32 > 128 && n32 <= 224) {
+  if (n32 > 128 && n32 <= 224) {
     a.N = 224;
     AMX_CHECK_ARG(strideW3 >= 3LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
-    if (g_x6_out_variant == 100) return launch_x6<EPI_UNNORM, X128x224o4>(a, (hipStream_t)stream);
-    if (g_x6_out_variant == 0) return launch_x6<EPI_UNNORM, X128x224>(a, (hipStream_t)stream);
-    // automatic: 14 waves of 64x32 (88 VGPRs), 3% ahead of 7 waves of 128x32 (tools/x6_variants.py)
-    return launch_x6<EPI_UNNORM, X128x224w14>(a, (hipStream_t)stream);
+    return launch_x6<EPI_UNNORM, X128x224>(a, (hipStream_t)stream);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW3 >= 3LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_x6: strideW3=%lld", strideW3);
-  return launch_x6_variant<EPI_UNNORM>(g_x6_out_variant > 0 ? g_x6_out_variant - 1 : 0, a, (hipStream_t)stream);
+  return launch_x6<EPI_UNNORM, X128>(a, (hipStream_t)stream);
 }
 
 extern "C" int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
@@ -1827,50 +1459,6 @@ extern "C" int amx_rff_features_x6(amx_ctx* ctx, int rows, int n_valid, int F, i
 }
 
 // ---- f16x3 entry points -------------------------------------------------------------------
-namespace {
-int g_h3_variant = -1;      // amx__set_h3_variant: hidden-layer tile (-1 automatic; see the switch)
-int g_h3_out_variant = -1;  // amx__set_h3_out_variant: output-layer tile (-1 automatic, 1 BK 32)
-int g_h3_rff_variant = -1;  // amx__set_h3_rff_variant: RFF tile (-1 automatic, 1 late, 2 late+pinned, 3 pinned)
-
-template <int EPI, class TL, int ABL = 0>
-int launch_h3(GemmArgs& a, hipStream_t stream) {
-  a.tiles_m = a.rows / TL::BM;
-  a.tiles_n = a.N / TL::BN;
-  const int nwg = a.tiles_m * a.tiles_n * a.groups;
-  if (nwg == 0) return AMX_OK;
-  a.clock_probe = g_clock_probe;
-  // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
-  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
-  hipLaunchKernelGGL((k_gemm_h3<EPI, TL, ABL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
-  AMX_CHECK_LAUNCH();
-  return AMX_OK;
-}
-
-int check_h3(const char* fn, int groups, int rows, int K, const float* A, int lda, const uint16_t* W2,
-             long long strideW2, const int* w_exp, const int* row_exp, int rexp_slots, int k_shared = 0) {
-  AMX_CHECK_ARG(groups >= 1 && groups <= AMX_MAX_MODELS, "%s: groups=%d", fn, groups);
-  AMX_CHECK_ARG(rows >= 0 && rows % AMX_ROW_TILE == 0, "%s: rows=%d must be a multiple of %d", fn, rows,
-                AMX_ROW_TILE);
-  AMX_CHECK_ARG(K > 0 && K % XBK == 0, "%s: K=%d must be a positive multiple of %d", fn, K, XBK);
-  AMX_CHECK_ARG(A && W2 && amx::aligned16(A) && amx::aligned16(W2), "%s: null/unaligned operand", fn);
-  AMX_CHECK_ARG(lda >= K && lda % 4 == 0, "%s: lda=%d (K=%d) must be >= K and a multiple of 4", fn, lda, K);
-  AMX_CHECK_ARG(strideW2 % 8 == 0, "%s: strideW2=%lld must be a multiple of 8", fn, strideW2);
-  AMX_CHECK_ARG(w_exp && row_exp && rexp_slots >= 1, "%s: null exponents or rexp_slots=%d", fn, rexp_slots);
-  AMX_CHECK_ARG(k_shared >= 0 && k_shared <= K && k_shared % 32 == 0,
-                "%s: k_shared=%d must be a multiple of 32 in [0, K=%d]", fn, k_shared, K);
-  return AMX_OK;
-}
-}  // namespace
-
-extern "C" int amx__set_h3_variant(int v) {
-  g_h3_variant = v;
-  return AMX_OK;
-}
-extern "C" int amx__set_h3_out_variant(int v) {
-  g_h3_out_variant = v;
-  return AMX_OK;
-}
-
 extern "C" int amx_split_f16x2(amx_ctx* ctx, int groups, int rows, int K, const float* W, int ldw, long long strideW,
                                uint16_t* W2, long long strideW2, int* w_exp, long long strideWexp, void* stream) {
   AMX_CHECK_ARG(ctx, "amx_split_f16x2: null ctx");
@@ -1928,48 +1516,9 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots; a.row_exp_out = row_exp_out;
   a.k_shared = k_shared;
   const hipStream_t s = (hipStream_t)stream;
-  const bool fit256 = rows % 256 == 0 && N % 256 == 0;
-  const bool m256 = rows % 256 == 0, n256 = N % 256 == 0;
-  switch (g_h3_variant) {
-    case 0: return launch_h3<EPI_BIAS_ACT, H128>(a, s);
-    case 1: if (fit256) return launch_h3<EPI_BIAS_ACT, H256w8>(a, s); break;
-    case 2: if (fit256) return launch_h3<EPI_BIAS_ACT, H256w8k32>(a, s); break;
-    case 3: if (fit256) return launch_h3<EPI_BIAS_ACT, H256w16>(a, s); break;
-    case 4: if (m256) return launch_h3<EPI_BIAS_ACT, H256x128>(a, s); break;
-    case 5: if (n256) return launch_h3<EPI_BIAS_ACT, H128x256>(a, s); break;
-    case 6: if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s); break;
-    case 7: if (m256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256x128k32>(a, s); break;
-    case 8: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32>(a, s); break;
-    case 9: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32late>(a, s); break;
-    case 11: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s); break;
-    case 13: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w16k32lateM>(a, s); break;
-    case 14: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
-    case 15: a.prio = 1; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
-    case 16: a.prio = 2; if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateM>(a, s); break;
-    case 17: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32lateM>(a, s); break;
-    case 19: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMP>(a, s); break;
-    case 20: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPE>(a, s); break;
-    case 21: if (fit256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPES>(a, s); break;
-    case 18: if (n256 && K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128x256w8k32late>(a, s); break;
-    case 91: return launch_h3<EPI_BIAS_ACT, H256w8k32, 1>(a, s);
-    case 92: return launch_h3<EPI_BIAS_ACT, H256w8k32, 2>(a, s);
-    case 93: return launch_h3<EPI_BIAS_ACT, H256w8k32, 3>(a, s);
-    case 94: return launch_h3<EPI_BIAS_ACT, H256w8k32, 4>(a, s);
-    case 95: return launch_h3<EPI_BIAS_ACT, H256w8k32, 5>(a, s);
-    case 96: a.abl_nostore = 1; return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
-    case 97: a.row_exp_out = nullptr; return launch_h3<EPI_BIAS_ACT, H256w16k32late>(a, s);
-    default: break;
-  }
-  // automatic: 256x256 with BK 32 on 16x16x32 MFMAs (8 waves of 128x64, one WG per CU),
-  // write-after-barrier schedule, fragment reads pinned one MFMA group ahead (5% per rollout)
-  // and the K-tile's first reads issued ahead of the next tile's LDS writes (+0.7%), the
-  // staging of the next tiles cut into one piece per m-block behind its MFMAs (+3.1%),
-  // when its grid fills the chip -- 7% ahead of the same tile
-  // on 32x32x16 MFMAs with 16 waves (itself 8-10% ahead of BK 16, 2-3% ahead of the
-  // write-before-barrier schedule; tools/h3_variants.py); otherwise 128x128 (BK 32 when K allows)
-  if (fit256 && K % 32 == 0 &&
-      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(H256w8k32lateMPES::LDS, H256w8k32lateMPES::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256w8k32lateMPES>(a, s);
+  if (rows % 256 == 0 && N % 256 == 0 && K % 32 == 0 &&
+      (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(ctx, H256::LDS, H256::NT, 2))
+    return launch_h3<EPI_BIAS_ACT, H256>(a, s);
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1996,57 +1545,19 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   const int S = ctx->S, Ad = ctx->A;
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
+  const hipStream_t s = (hipStream_t)stream;
   // weight rows padded to round_up(S, 128) (amx_layout n_out_pad); S <= 224 runs one 224-wide tile
   const int n32 = amx::round_up(n_valid, 32);
   if (n32 > 128 && n32 <= 224) {
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
-    if (g_h3_out_variant == 0 || K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224w14>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 1) return launch_h3<EPI_UNNORM, H128x224k32>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 12) return launch_h3<EPI_UNNORM, H128x224k32lateM>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 14) return launch_h3<EPI_UNNORM, H128x224w8k32lateM>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 15) return launch_h3<EPI_UNNORM, H128x224k32lateP>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 16) return launch_h3<EPI_UNNORM, H128x224k32lateMPE>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 2) return launch_h3<EPI_UNNORM, H128x224w4k32>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 3) return launch_h3<EPI_UNNORM, H128x224w4>(a, (hipStream_t)stream);
-    if (g_h3_out_variant == 4) return launch_h3<EPI_UNNORM, H128x224w7k32>(a, (hipStream_t)stream);
-
-    if (g_h3_out_variant == 13 && strideW2 >= 2LL * K * 256) {
-      a.N = 256;
-      return launch_h3<EPI_UNNORM, H128x256w8k32lateM>(a, (hipStream_t)stream);
-    }
-    if (g_h3_out_variant == 10 && strideW2 >= 2LL * K * 256) {
-      a.N = 256;
-      return launch_h3<EPI_UNNORM, H128x256w16k32late>(a, (hipStream_t)stream);
-    }
-    if (g_h3_out_variant >= 5 && g_h3_out_variant <= 8 && strideW2 >= 2LL * K * 256) {
-      a.N = 256;  // the weight image has round_up(S, 128) = 256 rows (zero beyond S)
-      switch (g_h3_out_variant) {
-        case 5: return launch_h3<EPI_UNNORM, H128x256w8k32>(a, (hipStream_t)stream);
-        case 6: return launch_h3<EPI_UNNORM, H128x256w8>(a, (hipStream_t)stream);
-        case 7: return launch_h3<EPI_UNNORM, H128x256w4k32>(a, (hipStream_t)stream);
-        default: return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, (hipStream_t)stream);
-      }
-    }
-    if (g_h3_out_variant == 9) return launch_h3<EPI_UNNORM, H128x224k32late>(a, (hipStream_t)stream);
-    // automatic: BK 32, write-after-barrier, 14 waves of 64x32 on 16x16x32 MFMAs with pinned /
-    // early fragment reads: 13% ahead of write-before-barrier, 3% ahead of 8 waves on N padded
-    // to 256 and 1.4% per rollout ahead of the same tile on 32x32x16 (tools/h3_variants.py,
-    // tools/rollout_ab.py)
-    return launch_h3<EPI_UNNORM, H128x224k32lateMPES>(a, (hipStream_t)stream);  // + split staging: -9%
+    if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
+    return launch_h3<EPI_UNNORM, H128x224>(a, s);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
-  const hipStream_t s = (hipStream_t)stream;
   if (K % 32 == 0) {
-    // the reference scene's S = 226 (and any N that is a multiple of 256): 128x256 tiles,
-    // 8 waves of 64x64, BK 32, write-after-barrier; other N: 128x128, BK 32
-    if (a.N % 256 == 0) {
-      if (g_h3_out_variant == 13) return launch_h3<EPI_UNNORM, H128x256w8k32lateM>(a, s);
-      if (g_h3_out_variant == 18) return launch_h3<EPI_UNNORM, H128x256w8k32late>(a, s);
-      if (g_h3_out_variant == 17) return launch_h3<EPI_UNNORM, H128x256w8k32lateMPE>(a, s);
-      return launch_h3<EPI_UNNORM, H128x256w8k32lateMPES>(a, s);  // 16x16x32 pinned/early/split: 17% ahead
-    }
+    if (a.N % 256 == 0) return launch_h3<EPI_UNNORM, H128x256>(a, s);  // the reference scene's S = 226
     return launch_h3<EPI_UNNORM, H128k32>(a, s);
   }
   return launch_h3<EPI_UNNORM, H128>(a, s);
@@ -2070,19 +1581,6 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.C = phi; a.ldc = ldphi;
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
-  if (K % 32 == 0) {
-    switch (g_h3_rff_variant) {
-      case 1: return launch_h3<EPI_RFF, H128k32late>(a, (hipStream_t)stream);
-      case 2: return launch_h3<EPI_RFF, H128k32lateP>(a, (hipStream_t)stream);
-      case 3: return launch_h3<EPI_RFF, H128k32P>(a, (hipStream_t)stream);
-      case 4: return launch_h3<EPI_RFF, H128k32lateMPES>(a, (hipStream_t)stream);
-      default: return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
-    }
-  }
+  if (K % 32 == 0) return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
   return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);
-}
-
-extern "C" int amx__set_h3_rff_variant(int v) {
-  g_h3_rff_variant = v;
-  return AMX_OK;
 }

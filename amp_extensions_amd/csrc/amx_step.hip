@@ -757,13 +757,6 @@ extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, i
   return AMX_OK;
 }
 
-static int g_pol_tpl = 0;  // amx__set_policy_tpl: 0 automatic (16), 32 threads per lane (A/B)
-
-extern "C" int amx__set_policy_tpl(int tpl) {
-  g_pol_tpl = tpl;
-  return AMX_OK;
-}
-
 static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                       const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                       const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
@@ -778,11 +771,10 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
                             (ctx->M == 1 || stride_m >= (long long)ldk * B)),
                 "amx_policy_act: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B");
   if (B == 0) return AMX_OK;
-  // threads per lane: 16 (16 lanes per workgroup).  amx__set_policy_tpl(32) selects 8 lanes
-  // of 32 threads (twice the waves, one output per thread) when H <= 32, A <= 64 -- measured
-  // 1.3 % slower per rollout (tools/rollout_ab.py p16,p32), so not the default
+  // 16 threads per lane, 16 lanes per workgroup (32 threads per lane measured 1.3 % slower
+  // per rollout in round 1, profiles/r01_policy_tpl.txt)
   const int hmax = H1 > H2 ? H1 : H2;
-  const int tpl = (g_pol_tpl == 32 && hmax <= 32 && ctx->A <= 64) ? 32 : 16;
+  constexpr int tpl = 16;
   const int lanes = 256 / tpl;
   const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A, lanes);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S/H too large for LDS staging (%zu B)", lds);
@@ -799,8 +791,7 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
   const int qh = (hmax + tpl - 1) / tpl;
   const int qa = (ctx->A + tpl - 1) / tpl;
   hipStream_t st = (hipStream_t)stream;
-  if (tpl == 32) hipLaunchKernelGGL((k_policy<32, 1, 2>), grid, dim3(256), lds, st, p);
-  else if (qh <= 2 && qa <= 2) hipLaunchKernelGGL((k_policy<16, 2, 2>), grid, dim3(256), lds, st, p);
+  if (qh <= 2 && qa <= 2) hipLaunchKernelGGL((k_policy<16, 2, 2>), grid, dim3(256), lds, st, p);
   else if (qh <= 2 && qa <= 3) hipLaunchKernelGGL((k_policy<16, 2, 3>), grid, dim3(256), lds, st, p);
   else if (qh <= 4 && qa <= 4) hipLaunchKernelGGL((k_policy<16, 4, 4>), grid, dim3(256), lds, st, p);
   else hipLaunchKernelGGL((k_policy<16, 16, 16>), grid, dim3(256), lds, st, p);

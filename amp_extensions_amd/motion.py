@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 
 import numpy as np
 import torch
@@ -158,6 +159,17 @@ class ReferenceMotion:
         N.check(ctx.lib.amx_set_motion(ctx.h, self.blob.ctypes.data, self.blob.size), "amx_set_motion")
         self.duration = float(times[-1])
         self.S = ctx.S
+
+    DEFAULT_BUNDLE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "humanoid3d_spinkick.npz")
+
+    @classmethod
+    def from_bundle(cls, ctx: AmxContext, path: str | None = None, **flags) -> "ReferenceMotion":
+        """Load a character + clip bundle written by tools/pack_motion.py (default: humanoid3d
+        with the spinkick clip, the reference's run_amp_humanoid3d_spinkick_args.txt data)."""
+        with np.load(path or cls.DEFAULT_BUNDLE, allow_pickle=False) as z:
+            character = json.loads(str(z["character_json"]))
+            motion = {"Loop": str(z["loop"]), "Frames": z["frames"].tolist()}
+        return cls(ctx, character, motion, **flags)
 
     @property
     def amp_obs_size(self) -> int:

@@ -35,8 +35,8 @@ def _work(i):
 
 def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers: int | None = None,
         samples: int = 20000, horizon: int = 300, expert_rows: int = 50000, feature_dim: int = 512,
-        lambda_b: float = 0.0025, seed: int = 100) -> dict:
-    """Returns env-steps/s of the CPU sampler alone and of sampler + relabel."""
+        lambda_b: float = 0.0025, seed: int = 100, relabel: bool = True) -> dict:
+    """Returns env-steps/s of the CPU sampler alone and (relabel=True) of sampler + relabel."""
     from amp_extensions_amd import synthetic as syn
 
     torch.set_num_threads(1)
@@ -55,6 +55,8 @@ def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers:
         t1 = time.perf_counter()
     paths = [p for r in results for p in r]
     n = sum(len(p["rewards"]) for p in paths)
+    if not relabel:
+        return dict(samples=n, paths=len(paths), workers=workers, sampler_s=t1 - t0, sampler_steps_per_s=n / (t1 - t0))
     # host relabel with the reference's batching (thread count restored for the relabel)
     torch.set_num_threads(workers)
     expert = torch.from_numpy(syn.expert(expert_rows, S, 3))

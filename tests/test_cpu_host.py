@@ -173,3 +173,36 @@ def test_npg_pack_unpack_roundtrip():
     for (W, b), (W2, b2) in zip(layers, l2):
         assert torch.equal(W, W2) and torch.equal(b, b2)
     assert torch.equal(ls, ls2)
+
+
+# ---- a1: the product's normalizers (amp_extensions_amd.datasets) vs the reference (G7) -----
+def test_product_transformations_match_reference(golden):
+    """AmpDataset.get_transformations (milo/milo/datasets.py:23-43) as the product computes it
+    (the normalizers DeviceEnsemble uploads) equals the reference's own output bit for bit."""
+    from amp_extensions_amd.datasets import AmpDataset, get_transformations
+    g = golden("g7_transformations.npz")
+    torch.set_num_threads(1)  # the fixture was generated single-threaded
+    rs = np.random.RandomState(int(g["seed"]))
+    n = int(g["n"])
+    s = 0.5 * rs.randn(n, 226)
+    s[:, 0] = rs.uniform(0.8, 0.95, n)
+    a = rs.randn(n, 28)
+    s2 = s + 0.01 * rs.randn(n, 226)
+    st, at, s2t = (torch.from_numpy(x).float() for x in (s, a, s2))
+    keys = ["mu_s", "sd_s", "mu_a", "sd_a", "mu_d", "sd_d"]
+    for out in (get_transformations(st, at, s2t), AmpDataset(st, at, s2t).get_transformations()):
+        for k, v in zip(keys, out):
+            assert v.dtype == torch.float32
+            np.testing.assert_array_equal(v.numpy(), g[k], err_msg=k)
+
+
+def test_motion_bundle_matches_reference_data(golden):
+    """The packaged character + spinkick clip (amp_extensions_amd/data, tools/pack_motion.py)
+    holds the reference's data files (the G12 fixture was read from them)."""
+    import json
+    from amp_extensions_amd.motion import ReferenceMotion
+    g = golden("g12_motion.npz")
+    with np.load(ReferenceMotion.DEFAULT_BUNDLE, allow_pickle=False) as z:
+        assert json.loads(str(z["character_json"])) == json.loads(str(g["character_json"]))
+        np.testing.assert_array_equal(z["frames"], g["frames"])
+        assert str(z["loop"]) == str(g["loop"])
