@@ -65,11 +65,10 @@ def test_fused_step_reset_matches_step_then_reset(cost_kind):
 
 
 @pytest.mark.parametrize("hidden", [(32, 32), (64, 48)])
-def test_policy_threads_per_lane_bit_identical(hidden):
-    """k_policy with 32 threads per lane (8 lanes per workgroup, amx__set_policy_tpl(32) for
-    H <= 32) and with 16 (automatic) gives the same actions, means and fused x0 rows bit for bit (each
-    output unit keeps its sequential fma order); wider layers always run the 16-thread form."""
-    import ctypes
+def test_policy_fused_assembly_bit_identical(hidden):
+    """k_policy writing the ensemble's x0 rows itself (fused assembly) gives the same actions and
+    means as without, and the same x0 rows as the separate assembly kernel, bit for bit; the
+    means follow the oracle's float32 MLP (gaussian_mlp.py:95-104)."""
     import amp_extensions_amd as amx
     S, A, B = 197, 36, 1000
     rs = np.random.RandomState(4)
@@ -80,20 +79,21 @@ def test_policy_threads_per_lane_bit_identical(hidden):
     ctx.set_normalizers(norms)
     pw, log_std = R.init_policy_weights(S, A, hidden, seed=100)
     pol = amx.DevicePolicy(ctx, pw, log_std, seed=1)
-    ctx.lib.amx__set_policy_tpl.argtypes = [ctypes.c_int]
     ob = torch.from_numpy(0.5 * rs.randn(B, S)).to(DEV)
     outs = []
-    for tpl in (16, 32):
-        ctx.lib.amx__set_policy_tpl(tpl)
+    for fused in (False, True):
         act = torch.empty(B, A, dtype=torch.float64, device=DEV)
         mean = torch.empty(B, A, dtype=torch.float32, device=DEV)
         x0 = torch.zeros(4, 1024, ctx.ldk, dtype=torch.float32, device=DEV)
-        pol.act(ob, B, act, 7, mean_out=mean, x0=x0)
+        pol.act(ob, B, act, 7, mean_out=mean, x0=x0 if fused else None)
         outs.append((act, mean, x0))
-    ctx.lib.amx__set_policy_tpl(0)
+    x0_sep = torch.zeros(4, 1024, ctx.ldk, dtype=torch.float32, device=DEV)
+    from amp_extensions_amd import _native as N
+    N.check(ctx.lib.amx_assemble_input(ctx.h, ob.data_ptr(), outs[0][0].data_ptr(), N.AMX_IN_F64, x0_sep.data_ptr(),
+                                       1024 * ctx.ldk, ctx.ldk, B, ctx.stream), "amx_assemble_input")
     torch.cuda.synchronize()
-    for x, y in zip(*outs):
-        assert torch.equal(x, y)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert torch.equal(outs[1][2][:, :B, :ctx.k0_pad], x0_sep[:, :B, :ctx.k0_pad])
     obn = ob.cpu().numpy()
     ref = np.stack([R.policy_mean(pw, obn[i]) for i in range(0, B, 37)])  # the oracle's float32 MLP
     np.testing.assert_allclose(outs[1][1].cpu().numpy()[::37], ref, rtol=1e-5, atol=1e-6)
