@@ -62,7 +62,7 @@ def test_rbf_input_types_vs_oracle(amx, norms, typ, cost_range):
     assert cost.bw == ref.bw
     ps, pa, ps2 = synthetic_offline(300, 4)
     x = R.cost_input(typ, t32(ps), t32(pa), t32(ps2))
-    close(cost.fit_cost(x.to(DEV)), ref.fit_cost(x), rtol=1e-3)
+    close(cost.fit_cost(x.to(DEV)), ref.fit_cost(x), rtol=1e-4)
     close(cost.get_costs(x.to(DEV)).cpu().numpy(), ref.get_costs(x).numpy())
     s, a, _ = synthetic_offline(2048, 0)
     thr = ens.compute_threshold(t32(s).to(DEV), t32(a).to(DEV))
@@ -76,7 +76,7 @@ def test_rbf_input_types_vs_oracle(amx, norms, typ, cost_range):
         with pytest.raises(AttributeError):
             cost.get_expert_cost()
     else:
-        close(float(cost.get_expert_cost()), float(ref.get_expert_cost()), rtol=1e-3)
+        close(float(cost.get_expert_cost()), float(ref.get_expert_cost()), rtol=1e-4)
 
 
 @pytest.mark.parametrize("loss", ["least_squares", "logistic"])
@@ -126,7 +126,7 @@ def test_rollout_cost_rows_and_relabel(amx, norms, typ):
     assert torch.equal(rows[:, :x.shape[1]], x) and (rows[:, x.shape[1]:] == 0).all()
     assert (eng.cost_in[:, B:] == 0).all()
     ref = R.RBFLinearCostRef(expert, feature_dim=512, input_type=typ, lambda_b=0.0025, seed=100)
-    close(float(info["mb_mmd"]), ref.fit_cost(x), rtol=1e-3)
+    close(float(info["mb_mmd"]), ref.fit_cost(x), rtol=1e-4)
     disc_fn = lambda st, ac: R.compute_discrepancy(ens_w, norms, st, ac)
     cst, _ = ref.get_bonus_costs(t32(obs), t32(acts), disc_fn, thr, next_states=t32(nxt))
     close(eng.rewards[:K, :B].cpu().numpy().reshape(-1), -cst.numpy()[:, 0])
