@@ -12,6 +12,9 @@
 // bit-exact by construction.
 #include "amx_common.h"
 
+#include <utility>
+#include <stdlib.h>
+
 namespace {
 
 __device__ inline double wave_sum(double v) {
@@ -417,31 +420,75 @@ __device__ inline void pol_stage_all(float* __restrict__ img, const float* __res
   }
 }
 
+// One dense layer for the lanes of a workgroup: thread (lane l, u0) computes units
+// u = u0 + 16q of lane l.  The lane's input row x is needed by all 16 threads of its DPP row
+// (16 consecutive threads): each thread reads its own float4 chunks c = u0 + 16j of the row
+// from LDS and the chunks are broadcast across the row with DPP row_newbcast.  Reading the
+// same 16 bytes from LDS with all 16 threads of a row (a broadcast ds_read_b128) returned
+// wrong data in wave lanes 48-63 on gfx950 whenever another workgroup on the CU ran
+// v_mfma_f32_16x16x32_f16 (reproduced with tools/victim.hip + tools/corunner.hip, DESIGN.md
+// §5.6), so no LDS read here is a broadcast: the weight rows of the 16 threads are distinct
+// (rows past H wrap around, their results are dropped) and the input comes through DPP.  The
+// summation order per unit is the chunk order k = 0 .. n4-1, as before.
+template <int XS>
+__device__ inline void pol_load_row(const float* __restrict__ x, int n4, int u0, pf4 (&xr)[XS]) {
+#pragma unroll
+  for (int j = 0; j < XS; ++j) {
+    const int c = u0 + 16 * j;
+    xr[j] = c < n4 ? *reinterpret_cast<const pf4*>(x + 4 * c) : pf4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <int N>
+__device__ __forceinline__ float pol_bcast(float v) {  // lane N of each 16-lane DPP row to the whole row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + N, 0xf, 0xf,
+                                                               false));
+}
+
+template <int Q, int N>
+__device__ __forceinline__ void pol_chunk(const pf4& xk, const float* const (&wr)[Q], int k, float (&acc)[Q]) {
+  pf4 v;
+  v.x = pol_bcast<N>(xk.x);
+  v.y = pol_bcast<N>(xk.y);
+  v.z = pol_bcast<N>(xk.z);
+  v.w = pol_bcast<N>(xk.w);
+  pf4 a[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) a[q] = *reinterpret_cast<const pf4*>(wr[q] + 4 * k);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    acc[q] = fmaf(a[q].x, v.x, acc[q]);
+    acc[q] = fmaf(a[q].y, v.y, acc[q]);
+    acc[q] = fmaf(a[q].z, v.z, acc[q]);
+    acc[q] = fmaf(a[q].w, v.w, acc[q]);
+  }
+}
+
+template <int Q, int... N>
+__device__ __forceinline__ void pol_slot(const pf4& xk, const float* const (&wr)[Q], int k0, int n4, float (&acc)[Q],
+                                         std::integer_sequence<int, N...>) {
+  // chunks k0 .. k0+15 (the slot's owners are lanes 0..15 of the row); n4 is uniform
+  ((k0 + N < n4 ? pol_chunk<Q, N>(xk, wr, k0 + N, acc) : (void)0), ...);
+}
+
 template <int TPL, int Q>
 __device__ inline void pol_layer(const float* __restrict__ w, int ws, const float* __restrict__ x, int n4,
                                  const float* __restrict__ bias, int H, int u0, float (&out)[Q], bool tanh_act) {
+  static_assert(TPL == 16, "one lane per 16-thread DPP row");
+  constexpr int XS = (POL_MAXH / 4 + 15) / 16;  // chunk slots per thread (rows up to POL_MAXH floats)
   float acc[Q];
   const float* wr[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     acc[q] = 0.f;
     const int u = u0 + TPL * q;
-    wr[q] = w + (u < H ? u : H - 1) * ws;
+    wr[q] = w + (u < H ? u : u % H) * ws;  // distinct rows within the 16 threads (H >= 16)
   }
-#pragma unroll 2
-  for (int k = 0; k < n4; ++k) {
-    const pf4 v = *reinterpret_cast<const pf4*>(x + 4 * k);
-    pf4 a[Q];
+  pf4 xr[XS];
+  pol_load_row<XS>(x, n4, u0, xr);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) a[q] = *reinterpret_cast<const pf4*>(wr[q] + 4 * k);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      acc[q] = fmaf(a[q].x, v.x, acc[q]);
-      acc[q] = fmaf(a[q].y, v.y, acc[q]);
-      acc[q] = fmaf(a[q].z, v.z, acc[q]);
-      acc[q] = fmaf(a[q].w, v.w, acc[q]);
-    }
-  }
+  for (int j = 0; j < XS; ++j)
+    if (16 * j < n4) pol_slot<Q>(xr[j], wr, 16 * j, n4, acc, std::make_integer_sequence<int, 16>{});
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int u = u0 + TPL * q;
@@ -764,8 +811,8 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
   AMX_CHECK_ARG(ctx && ob && blob && act, "amx_policy_act: null pointer");
   AMX_CHECK_ARG(amx::aligned16(blob), "amx_policy_act: blob must be 16-byte aligned");
   AMX_CHECK_ARG(eval_mode || noise_scale, "amx_policy_act: noise_scale required unless eval_mode");
-  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH,
-                "amx_policy_act: H1=%d H2=%d A=%d (max %d)", H1, H2, ctx->A, POL_MAXH);
+  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH && ctx->S <= POL_MAXH,
+                "amx_policy_act: S=%d H1=%d H2=%d A=%d (max %d)", ctx->S, H1, H2, ctx->A, POL_MAXH);
   AMX_CHECK_ARG(B >= 0, "amx_policy_act: B=%d", B);
   AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
                             (ctx->M == 1 || stride_m >= (long long)ldk * B)),

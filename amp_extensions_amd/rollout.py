@@ -52,11 +52,6 @@ class RolloutEngine:
         self.eval_mode = eval_mode
         self.auto_reset = auto_reset
         self.fuse_reset = True  # table resets run inside the step kernel (amx_step_reset)
-        # score each step on a side stream as soon as its cost rows exist, overlapping the
-        # next step's latency-bound kernels (policy, assembly, step); joined by score()
-        self.overlap_score = False
-        self._side = None
-        self._side_pending = False
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
         from .motion import ReferenceMotion
@@ -238,19 +233,7 @@ class RolloutEngine:
             self.obs[t + 1].copy_(ob_next)
         self.t += 1
         self.step_counter += 1
-        if self.overlap_score and self.cost is not None and not self._capturing:
-            self._score_async()
         return t
-
-    def _score_async(self) -> None:
-        dev = self.ctx.device
-        main = torch.cuda.current_stream(dev)
-        if self._side is None:
-            self._side = torch.cuda.Stream(dev)
-        self._side.wait_stream(main)
-        with torch.cuda.stream(self._side):
-            self.score()
-        self._side_pending = True
 
     def _record_cost_input(self, t: int) -> None:
         """Cost-input rows of step t for the non-'ss' input types (linear_cost.py:115-127)."""
@@ -285,9 +268,6 @@ class RolloutEngine:
     def score(self) -> None:
         """Features (MMD) or discriminator rewards (GAIL) of the steps recorded since the last
         call, in one launch over their T*B_pad cost-input rows."""
-        if self._side_pending and torch.cuda.current_stream(self.ctx.device) != self._side:
-            torch.cuda.current_stream(self.ctx.device).wait_stream(self._side)  # join the side scoring
-            self._side_pending = False
         c, cost, t0, t1, Bp = self.ctx, self.cost, self._scored, self.t, self.Bp
         if t1 <= t0 or cost is None:
             self._scored = t1

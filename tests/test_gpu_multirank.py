@@ -1,0 +1,76 @@
+"""The engine's multi-rank path on the GPU (BASELINE configs[3]: the rollout's lanes sharded
+over ranks, one all-reduce of [sum phi, count] per rollout, milo/milo/linear_cost.py:84-94):
+two ranks (fresh processes, gloo, sharing the card) vs one process over the union of their
+lanes with the same injected reset rows and policy noise, plus the two-graph HIP-graph replay
+(RolloutEngine.graph_rollout with the all-reduce between the graphs) vs eager rollouts.
+
+Per-lane results (next states, done flags, rewards) must be bit-identical (rows are
+independent in every kernel); the global witness comes from per-rank fp64 sums added in a
+different order, so mb_mmd and the rewards that depend on it agree to 1e-6 relative."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(rank, world, port, out, env=None):
+    e = dict(os.environ, **(env or {}))
+    return subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py"), str(rank), str(world),
+                             str(port), out], env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+
+
+def _wait(procs, timeout=240):
+    outs = []
+    try:
+        for p in procs:
+            o, _ = p.communicate(timeout=timeout)
+            outs.append(o.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-4000:]
+
+
+def test_two_ranks_match_one_process_over_the_union(tmp_path):
+    port = _free_port()
+    outs = [str(tmp_path / f"rank{r}.npz") for r in range(2)]
+    _wait([_run(r, 2, port, outs[r]) for r in range(2)])
+    single = str(tmp_path / "single.npz")
+    _wait([_run(0, 1, 0, single)])
+    ranks = [np.load(o) for o in outs]
+    one = np.load(single)
+    assert int(ranks[0]["hi"]) == int(ranks[1]["lo"]) and int(ranks[1]["hi"]) == one["rewards"].shape[1]
+    for r in ranks:
+        lo, hi = int(r["lo"]), int(r["hi"])
+        np.testing.assert_array_equal(r["next_obs"], one["next_obs"][:, lo:hi])
+        np.testing.assert_array_equal(r["done"], one["done"][:, lo:hi])
+        np.testing.assert_allclose(r["rewards"], one["rewards"][:, lo:hi], rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(float(r["mb_mmd"]), float(one["mb_mmd"]), rtol=1e-6)
+        np.testing.assert_allclose(r["phi_sum"], one["phi_sum"], rtol=1e-12)  # the all-reduced fp64 sums
+        np.testing.assert_allclose(float(r["expert_cost"]), float(one["expert_cost"]), rtol=1e-6)
+    assert ranks[0]["done"].any()  # the horizon-3 lanes reset inside the rollout
+    # every rank holds the same global witness
+    assert float(ranks[0]["mb_mmd"]) == float(ranks[1]["mb_mmd"])
+    # two-graph replay with the all-reduce between the graphs == eager rollout + relabel(allreduce)
+    for r in ranks:
+        np.testing.assert_array_equal(r["graph_obs"], r["eager_obs"])
+        np.testing.assert_array_equal(r["graph_rewards"], r["eager_rewards"])
+        assert float(r["graph_mmd"]) == float(r["eager_mmd"])
+        assert float(r["graph_expert"]) == float(r["eager_expert"])
+    assert float(ranks[0]["graph_mmd"]) == float(ranks[1]["graph_mmd"])

@@ -3,8 +3,7 @@ interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 
 usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
 variants: "base" (defaults); "s0": one x0 copy per member (DeviceEnsemble.shared_x0 off);
-"r0": separate step + reset launches (RolloutEngine.fuse_reset off); "o1": per-step
-side-stream scoring (RolloutEngine.overlap_score); "f0"/"f1": layer-by-layer GEMM launches /
+"r0": separate step + reset launches (RolloutEngine.fuse_reset off); "f0"/"f1": layer-by-layer GEMM launches /
 the fused ensemble forward (DeviceEnsemble.fused).
 """
 import math
@@ -44,7 +43,6 @@ def setv(v):
     s = str(v)
     ens.shared_x0 = s != "s0"
     eng.fuse_reset = s != "r0"
-    eng.overlap_score = s == "o1"
     if hasattr(ens, "fused"):
         ens.fused = s == "f1" or (s != "f0" and ens.fused_default)
 
