@@ -764,7 +764,6 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
     return;
   }
   if constexpr (EPI == EPI_BIAS_ACT) {
-    static_assert(MB * 4 == 16 || MB * 4 == 32, "row-exponent reduce-scatter: 16 or 32 rows per lane");
     float bv[NB];
     int ec[NB];
 #pragma unroll
@@ -795,18 +794,35 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
       }
     }
     if (a.row_exp_out) {
-      // reduce-scatter over the 16 column lanes (bits 3..0 of lc): lane lc keeps the PER
-      // values of flat indices PER*lc .. PER*lc+PER-1 (flat index = m*4 + j)
-      constexpr int NV = MB * 4, PER = NV / 16;
-      rs_step<8, NV / 2>(mx, lc);
-      rs_step<4, NV / 4>(mx, lc);
-      rs_step<2, NV / 8>(mx, lc);
-      rs_step<1, NV / 16>(mx, lc);
       int* out = a.row_exp_out + (long long)g * a.strideRexp;
+      if constexpr (MB * 4 == 16 || MB * 4 == 32) {
+        // reduce-scatter over the 16 column lanes (bits 3..0 of lc): lane lc keeps the PER
+        // values of flat indices PER*lc .. PER*lc+PER-1 (flat index = m*4 + j)
+        constexpr int NV = MB * 4, PER = NV / 16;
+        rs_step<8, NV / 2>(mx, lc);
+        rs_step<4, NV / 4>(mx, lc);
+        rs_step<2, NV / 8>(mx, lc);
+        rs_step<1, NV / 16>(mx, lc);
 #pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int i = PER * lc + u, m = i >> 2, j = i & 3;
-        atomicMax(out + row0 + m * 16 + 4 * lq + j, exp_of_bits(mx[u]));
+        for (int u = 0; u < PER; ++u) {
+          const int i = PER * lc + u, m = i >> 2, j = i & 3;
+          atomicMax(out + row0 + m * 16 + 4 * lq + j, exp_of_bits(mx[u]));
+        }
+      } else {
+        // any MB: per 16-row block, reduce-scatter the lane's 4 row values over lc bits 3, 2
+        // (value j = 2 bit3 + bit2 remains), then a full max over bits 1, 0
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          uint32_t q4[4] = {mx[m * 4], mx[m * 4 + 1], mx[m * 4 + 2], mx[m * 4 + 3]};
+          rs_step<8, 2>(q4, lc);
+          rs_step<4, 1>(q4, lc);
+          uint32_t o = (uint32_t)__builtin_amdgcn_ds_swizzle((int)q4[0], 0x1f | (2 << 10));
+          q4[0] = q4[0] > o ? q4[0] : o;
+          o = (uint32_t)__builtin_amdgcn_ds_swizzle((int)q4[0], 0x1f | (1 << 10));
+          q4[0] = q4[0] > o ? q4[0] : o;
+          if ((lc & 3) == 0)
+            atomicMax(out + row0 + m * 16 + 4 * lq + ((lc >> 3) & 1) * 2 + ((lc >> 2) & 1), exp_of_bits(q4[0]));
+        }
       }
     }
   } else {  // EPI_UNNORM
@@ -1195,6 +1211,11 @@ __global__ __launch_bounds__(256) void k_row_exp(const float* __restrict__ A, in
 //   output layer S <= 224: 128x224, 14 waves of 64x32 on 16x16x32 (same schedule);
 //     S in (224, 256]: 128x256, 8 waves of 64x64
 using H256 = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
+// row-block tiles for the strong-scaling lane counts (rows = 32 RB, 4 members: a 256-workgroup
+// grid for every RB): hidden RB x 256 (8 waves of RB/2 x 64), output RB x 112 / RB x 128
+// (RB/32 waves of 32 x 112 or 32 x 128), same schedule as H256
+template <int MB> using HRow = TileH3<2, 4, 1, 1, 2, 2, true, true, true, MB, 4, true, true, true>;
+template <int RW, int NBO> using HOut = TileH3<RW, 1, 1, 1, 2, 2, true, true, true, 2, NBO, true, true, true>;
 using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;
 using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
 using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true>;
@@ -1519,6 +1540,19 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   if (rows % 256 == 0 && N % 256 == 0 && K % 32 == 0 &&
       (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(ctx, H256::LDS, H256::NT, 2))
     return launch_h3<EPI_BIAS_ACT, H256>(a, s);
+  // one wave of row-block tiles: rows = RB * n_cus / (groups * N/256), RB in {128..224}
+  if (N % 256 == 0 && K % 32 == 0) {
+    const long long per = (long long)groups * (N / 256);
+    if (per > 0 && (long long)ctx->n_cus % per == 0 && rows % (ctx->n_cus / per) == 0) {
+      switch (rows / (ctx->n_cus / per)) {
+        case 128: return launch_h3<EPI_BIAS_ACT, HRow<4>>(a, s);
+        case 160: return launch_h3<EPI_BIAS_ACT, HRow<5>>(a, s);
+        case 192: return launch_h3<EPI_BIAS_ACT, HRow<6>>(a, s);
+        case 224: return launch_h3<EPI_BIAS_ACT, HRow<7>>(a, s);
+        default: break;
+      }
+    }
+  }
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
@@ -1548,15 +1582,35 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   const hipStream_t s = (hipStream_t)stream;
   // weight rows padded to round_up(S, 128) (amx_layout n_out_pad); S <= 224 runs one 224-wide tile
   const int n32 = amx::round_up(n_valid, 32);
+  // one wave of row-block tiles RB x (N/2) when rows = RB * n_cus / (2 groups), RB in {128..224}
+  const int nrb = (2 * groups > 0 && ctx->n_cus % (2 * groups) == 0) ? ctx->n_cus / (2 * groups) : 0;
+  const int rb = (nrb > 0 && rows % nrb == 0) ? rows / nrb : 0;
+  const bool row_tiles = K % 32 == 0 && (rb == 128 || rb == 160 || rb == 192 || rb == 224);
   if (n32 > 128 && n32 <= 224) {
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
+    if (row_tiles) {
+      switch (rb) {
+        case 128: return launch_h3<EPI_UNNORM, HOut<4, 7>>(a, s);
+        case 160: return launch_h3<EPI_UNNORM, HOut<5, 7>>(a, s);
+        case 192: return launch_h3<EPI_UNNORM, HOut<6, 7>>(a, s);
+        default: return launch_h3<EPI_UNNORM, HOut<7, 7>>(a, s);
+      }
+    }
     return launch_h3<EPI_UNNORM, H128x224>(a, s);
   }
   a.N = amx::round_up(n_valid, 128);
   AMX_CHECK_ARG(strideW2 >= 2LL * K * a.N || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
   if (K % 32 == 0) {
+    if (a.N == 256 && row_tiles) {
+      switch (rb) {
+        case 128: return launch_h3<EPI_UNNORM, HOut<4, 8>>(a, s);
+        case 160: return launch_h3<EPI_UNNORM, HOut<5, 8>>(a, s);
+        case 192: return launch_h3<EPI_UNNORM, HOut<6, 8>>(a, s);
+        default: return launch_h3<EPI_UNNORM, HOut<7, 8>>(a, s);
+      }
+    }
     if (a.N % 256 == 0) return launch_h3<EPI_UNNORM, H128x256>(a, s);  // the reference scene's S = 226
     return launch_h3<EPI_UNNORM, H128k32>(a, s);
   }

@@ -156,12 +156,22 @@ def cpu_baseline_leg(S, A, args):
 
 
 def plan_lanes(samples: int, max_lanes: int, lanes: int = 0):
-    """(lanes, sync steps) of one rank's rollout: the fewest synchronous steps that keep the
-    lanes <= max_lanes, lanes rounded up to the 256-row GEMM tile."""
+    """(lanes, sync steps) of one rank's rollout.  Lane counts are multiples of 1024 in
+    [4096, max_lanes]: with 4 members they give the ensemble GEMMs one full 256-workgroup wave
+    (256 x 256 tiles at 8192 lanes, the row-block tiles RB x 256 at 32 RB lanes otherwise).
+    Among the step counts T = ceil(samples / max_lanes) and T + 1 the one with the smaller
+    modelled time T * (60 us + 53 ns * lanes) wins (per-step fixed cost + per-lane GEMM cost,
+    measured at 8192 lanes)."""
     if lanes:
         return lanes, math.ceil(samples / lanes)
-    T = max(1, math.ceil(samples / max_lanes))
-    return min(max_lanes, (math.ceil(samples / T) + 255) // 256 * 256), T
+    best = None
+    T0 = max(1, math.ceil(samples / max_lanes))
+    for T in (T0, T0 + 1):
+        L = min(max_lanes, max(4096, (math.ceil(samples / T) + 1023) // 1024 * 1024))
+        t = T * (60e-6 + 53e-9 * L)
+        if L * T >= samples and (best is None or t < best[0]):
+            best = (t, L, T)
+    return best[1], best[2]
 
 
 def main():

@@ -40,11 +40,15 @@ def row_err(p, ref):
 
 @pytest.mark.parametrize("S,A,hidden,B", [(197, 36, [512] * 4, 8192), (197, 36, [512] * 4, 640),
                                           (100, 20, [256] * 3, 640), (300, 40, [128] * 2, 384),
-                                          (226, 28, [100] * 2, 200)])
+                                          (226, 28, [100] * 2, 200), (197, 36, [512] * 4, 4096),
+                                          (197, 36, [512] * 4, 5120), (197, 36, [512] * 4, 6144),
+                                          (197, 36, [512] * 4, 7168), (226, 28, [512] * 4, 5120)])
 def test_f16x3_ensemble_matches_oracle_and_f32(S, A, hidden, B):
-    """Tile paths: 8192 lanes -> 256x256 BK32 hidden tiles, smaller grids -> 128x128; S=197 ->
-    the 128x224 output tile, S=100 -> 128, S=300 -> three 128 tiles; hidden 100 -> padded
-    columns.  Same tolerance as the f32 path (2e-5 of max(1, |ref|)) and within 1e-6 of it."""
+    """Tile paths: 8192 lanes -> 256x256 BK32 hidden tiles; 4096 / 5120 / 6144 / 7168 lanes ->
+    the row-block tiles (RB x 256 hidden, RB x 112 / RB x 128 output, RB = 128 .. 224: one
+    256-workgroup wave); other grids -> 128x128; S=197 -> the 128x224 output tile, S=100 ->
+    128, S=300 -> three 128 tiles; hidden 100 -> padded columns.  Same tolerance as the f32
+    path (2e-5 of max(1, |ref|)) and within 1e-6 of it."""
     amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, hidden)
     rs = np.random.RandomState(1)
     ob = 0.5 * rs.randn(B, S)
@@ -96,12 +100,15 @@ def _f64_forward(ens_w, norms, ob, ac):
     return np.stack(out)
 
 
-def test_f16x3_extreme_and_zero_rows():
+@pytest.mark.parametrize("B", [512, 5120])
+def test_f16x3_extreme_and_zero_rows(B):
     """Rows 1e4x and 1e-4x the offline scale, rows exactly at the normalizer mean (x0 = 0) and
     ordinary rows in one batch: each row is scaled by its own power of two, so every row's
     error vs fp64 stays at fp32 level relative to that row, no worse than the f32 MFMA path's,
-    and the ordinary rows are bit-identical to a batch without the extreme ones."""
-    S, A, B = 197, 36, 512
+    and the ordinary rows are bit-identical to a batch without the extreme ones (B = 5120: the
+    row-block tiles, RB = 160, and their per-block row-exponent reduction; fp64 check on the
+    first 512 rows)."""
+    S, A = 197, 36
     amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, [512] * 4)
     rs = np.random.RandomState(2)
     ob = 0.5 * rs.randn(B, S)
@@ -115,15 +122,16 @@ def test_f16x3_extreme_and_zero_rows():
     ac2[64:128] = mu_a + (ac[64:128] - mu_a) * 1e-4
     ob2[128:136] = mu_s.astype(np.float32)
     ac2[128:136] = mu_a.astype(np.float32)
-    ref = _f64_forward(ens_w, norms, ob2, ac2)
+    ref = _f64_forward(ens_w, norms, ob2[:512], ac2[:512])
     e3 = ens["f16x3"]
-    p3 = e3.forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :B].cpu().numpy()
-    p32 = ens["f32"].forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :B].cpu().numpy()
+    p3 = e3.forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :512].cpu().numpy()
+    p32 = ens["f32"].forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :512].cpu().numpy()
     r3, r32 = row_err(p3.astype(np.float64), ref), row_err(p32.astype(np.float64), ref)
     assert r3.max() <= 2e-5, r3.max()
     assert (r3 <= 2.0 * r32 + 1e-6).all()
+    full = e3.forward_preds(torch.from_numpy(ob2).to(DEV), torch.from_numpy(ac2).to(DEV), B)[:, :B].cpu().numpy()
     clean = e3.forward_preds(torch.from_numpy(ob).to(DEV), torch.from_numpy(ac).to(DEV), B)[:, :B].cpu().numpy()
-    np.testing.assert_array_equal(p3[:, 136:], clean[:, 136:])
+    np.testing.assert_array_equal(full[:, 136:], clean[:, 136:])
 
 
 def test_f16x3_nonfinite_rows_stay_local_and_deterministic():
