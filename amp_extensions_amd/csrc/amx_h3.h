@@ -1,0 +1,165 @@
+// Internal building blocks shared by the GEMM launches (amx_gemm.hip) and the fused ensemble
+// forward (amx_ens.hip): vector types, GemmArgs, the XCD-aware tile map, and the f16x3 tile
+// family (fp32 as two scaled fp16 limbs, three MFMA products).
+#pragma once
+
+#include "amx_common.h"
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// native vector (HIP's float4 is a wrapper struct: arrays of it were not promoted to registers)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum { EPI_BIAS_ACT = 0, EPI_UNNORM = 1, EPI_RFF = 2 };
+
+struct GemmArgs {
+  const float* A; long long strideA; int lda;
+  const float* W; long long strideW; int ldw;
+  const float* bias; long long strideBias;
+  float* C; long long strideC; int ldc; int col_off;
+  int rows, N, K;
+  int act;                 // EPI_BIAS_ACT: AMX_ACT_*
+  int n_valid;             // EPI_UNNORM: valid output columns; EPI_RFF: valid rows
+  const float* scale;      // EPI_UNNORM: sd_d
+  const float* shift;      // EPI_UNNORM: mu_d
+  float rff_scale;         // EPI_RFF: sqrt(2/F)
+  double* col_partials;    // EPI_RFF: [rows/128][N]
+  const uint8_t* row_mask; // EPI_RFF: nullable
+  int tiles_m, tiles_n, groups;
+  const uint16_t* W3;      // bf16x6 path: 3-limb weight image [g][N][K/16][3][16] (amx_split_bf16x3)
+  long long strideW3;      //   elements between groups; a row is 3*K elements
+  // f16x3 path (see the section below)
+  const uint16_t* W2;      // 2-limb scaled weight image [g][N][K/16][2][16] (amx_split_f16x2)
+  long long strideW2;
+  const int* w_exp;        // [g][N] column exponents of W2 (strideWexp between groups)
+  long long strideWexp;
+  const int* row_exp;      // [g][slots][rows]: row exponents of A's column slices
+  long long strideRexp;    //   between groups
+  int rexp_slots;          //   slices of A read by this launch (exponent = max over them)
+  int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
+  int k_shared;            // leading K columns of A read from group 0's rows for every group
+                           //   (the ensemble's x0 slice, assembled once; multiple of the tile's BK)
+};
+
+// Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over
+// the 8 XCDs, so block ids congruent mod 8 share an L2.  We hand each XCD a contiguous
+// run of logical tiles (tile_n fastest: consecutive tiles reuse the same A row panel;
+// then tile_m: they reuse the same weight panels of one ensemble member).  Bijective for
+// any tile count (cdna_hip_programming.md T1).
+__device__ inline void map_tile(const GemmArgs& a, int orig, int& g, int& tm, int& tn) {
+  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+  const int xcd = orig & 7;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int logical = base + (orig >> 3);
+  tn = logical % a.tiles_n;
+  const int rest = logical / a.tiles_n;
+  tm = rest % a.tiles_m;
+  g = rest / a.tiles_m;
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// ==== f16x3: fp32 as two scaled fp16 limbs, three products ==================================
+// x = 2^-s (x0 + x1) with x0 = RN_f16(2^s x) and x1 = RN_f16(2^s x - x0): 11 + 11 significant
+// bits, |2^s x - x0 - x1| <= 2^-22 |2^s x| (or, below fp16's normal range, 2^-25 absolute
+// against a row maximum scaled to [2^13, 2^14)).  a*b is then a0b0 + a0b1 + a1b0 on the f16
+// matrix pipe with fp32 accumulation; the dropped a1b1 <= 2^-22 |ab|.  Over a K-long dot
+// product these per-term errors add up like sqrt(K) * 2^-23 while the fp32 accumulation of
+// the same sum rounds like K * 2^-24, so for K >= ~64 the result carries the same error as an
+// fp32 GEMM (measured against fp64: tools/x6_accuracy.py) -- at 3 MFMA per 32x32x16 block
+// instead of bf16x6's 6.
+//
+// The scales are powers of two, so they factor out of the contraction exactly:
+//   * weights: per output column c, exponent E_c with max_k |W[c][k]| < 2^E_c, stored
+//     scaled by 2^(14 - E_c) (amx_split_f16x2);
+//   * activations: per row r, exponent E_r with max_k |A[r][k]| < 2^E_r, scaled by
+//     2^(14 - E_r) while staged into LDS.  E_r = max over the row's column slices
+//     (row_exp[g][slot][r]); the dense-concat rows are built slice by slice (x0, h0, h1, ...),
+//     so the assembly writes slot 0 and each hidden layer's epilogue atomically max-es the
+//     exponents of the slice it writes into its own slot (no slot is read and written by the
+//     same launch: deterministic).
+//   * epilogue: acc * 2^(E_r + E_c - 28) (one exact v_ldexp), then the fp32 bias etc. exactly
+//     as the other paths.
+// Exponents are clamped to [-100, 100] (zero rows, inf/NaN rows keep propagating as in fp32).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+constexpr int HSC = 14;  // scaled operands stay below 2^14 (fp16 max 65504)
+
+__device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
+  // E with v < 2^E for v = |x| (bits of a non-negative float); clamped to [-100, 100]
+  int e = (int)(absbits >> 23) - 126;
+  e = e < -100 ? -100 : e;
+  return e > 100 ? 100 : e;
+}
+
+// NSUB 16-k granules per K-tile (BK = 16 NSUB); LDS row = NSUB x [limb0 16 | limb1 16] + 8 pad
+// (20 dwords at NSUB 1, 36 at NSUB 2: the 16 rows of a ds_read_b128 lane group land on
+// distinct 4-bank slots)
+template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
+          bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false, bool EARLY_ = false,
+          bool SPLIT_ = false>
+struct TileH3 {
+  static constexpr bool EARLY = EARLY_ && M16_ && LATE_;  // first fragment reads before the publish
+  // SPLIT: the publish of tile t+1 and the loads of t+2 are cut into one piece per m-block and
+  // placed behind that block's MFMAs (the guide's split write-after-barrier schedule)
+  static constexpr bool SPLIT = SPLIT_ && EARLY;
+  // PIN: sched_barriers keep each block's fragment reads one MFMA group ahead of their use
+  static constexpr bool PIN = PIN_;
+  static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;
+  // M16: v_mfma_f32_16x16x32_f16 on 16x16 blocks (BK 32; 4 fp32 accumulators per lane and
+  // block) instead of 32x32x16 -- the same cycles per FLOP at lower power per FLOP
+  // (MI355X_MICROARCH.md); LDS rows of 40 dwords (conflict-free for its lane->k map and for
+  // the plain A staging map), the row exponents live in the stage area (160 KB LDS)
+  static constexpr bool M16 = M16_;
+  static_assert(!M16 || NSUB == 2, "the 16x16x32 MFMA consumes a 32-deep K-tile");
+  // AMAP (BK 32): the 16 lanes of a ds_write_b64 group stage rows r and r+2 (36-dword rows:
+  // 72 = 8 mod 32 banks apart, so their 2 x 8 dwords interleave) instead of r and r+1 (2-way
+  // bank conflict on every A limb store): 2% per layer (tools/h3_variants.py)
+  static constexpr bool AMAP = AMAP_ && !M16_;
+  // LATE: barrier -> publish tile t+1 -> issue the loads of t+2 -> compute t (write after
+  // the barrier: the LDS writes drain under the MFMAs, the loads get a whole K-tile)
+  static constexpr bool LATE = LATE_;
+  static constexpr int LD = NSUB * 32 + (M16 ? 16 : 8);       // f16 per LDS row
+  static constexpr int NT = WM * WN * 64;
+  // M16: MB x NB blocks of 16x16 per wave (default 2TM x 2TN; MB16_/NB16_ override, e.g. 7
+  // column blocks = 112 columns); 32x32 form: TM x TN blocks of 32x32
+  static constexpr int MB = (M16 && MB16_) ? MB16_ : 2 * TM, NB = (M16 && NB16_) ? NB16_ : 2 * TN;
+  static constexpr int WROWS = M16 ? MB * 16 : TM * 32, WCOLS = M16 ? NB * 16 : TN * 32;
+  static constexpr int BM = WM * WROWS, BN = WN * WCOLS;
+  static constexpr int STAGE = (BM + BN) * LD;                 // f16 of one stage (A + W)
+  static constexpr size_t LDS = 2 * STAGE * sizeof(uint16_t) + (M16 ? 0 : BM * sizeof(int));
+  static constexpr int SEXP = M16 ? STAGE : 2 * STAGE;         // f16 offset of the row exponents
+  static constexpr int CPR = 4 * NSUB;                         // 16-B chunks per row and K-tile (A f32 and W)
+  static constexpr int NA = BM * CPR, NW = BN * CPR;
+  static constexpr int VA = (NA + NT - 1) / NT, VW = (NW + NT - 1) / NT;
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+// 4 consecutive k of one row, pre-scaled -> two f16 limbs packed as 4 f16 each
+__device__ __forceinline__ void split2(f32x4 x, u32x2& l0, u32x2& l1) {
+  const f16x4 h0 = __builtin_convertvector(x, f16x4);
+  const f32x4 r1 = x - __builtin_convertvector(h0, f32x4);  // exact
+  const f16x4 h1 = __builtin_convertvector(r1, f16x4);
+  l0 = __builtin_bit_cast(u32x2, h0);
+  l1 = __builtin_bit_cast(u32x2, h1);
+}
+
+// One reduce-scatter step of a max over the 32 lanes li: lanes with bit MASK set keep the upper
+// HALF values, their partners the lower; each receives the other half (ds_swizzle bitmask
+// mode: and 0x1f, xor MASK within 32-lane groups) and keeps the max.
+template <int MASK, int HALF>
+__device__ __forceinline__ void rs_step(uint32_t* v, int li) {
+  const bool up = (li & MASK) != 0;
+#pragma unroll
+  for (int i = 0; i < HALF; ++i) {
+    const uint32_t keep = up ? v[HALF + i] : v[i];
+    const uint32_t send = up ? v[i] : v[HALF + i];
+    const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send, 0x1f | (MASK << 10));
+    v[i] = keep > recv ? keep : recv;
+  }
+}
+
+}  // namespace

@@ -82,7 +82,9 @@ def parse():
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
-    p.add_argument("--cpu-samples", type=int, default=0)
+    p.add_argument("--cpu-samples", type=int, default=0, help="env-steps per worker at each sweep point (default 1500)")
+    p.add_argument("--cpu-final-samples", type=int, default=200000,
+                   help="env-steps of the timed best-W run (five 40 000-sample rollouts: 10-30 s of CPU work)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the whole rollout as captured HIP graph(s); auto: when a rank's rollout is "
@@ -116,7 +118,8 @@ def cpu_baseline_leg(S, A, args):
     """The oracle's restated reference sampler + host relabel, timed on this host's cores
     (BASELINE.md §3): a sweep over the worker count W (powers of two up to the CPU share this
     process has, plus the share itself), each point a bounded sample (about 1 500 env-steps per
-    worker); the relabel is timed on the best point's trajectories.  Runs before anything
+    worker); the best W is then timed end to end (sampler + relabel) on --cpu-final-samples
+    env-steps (default 200 000 = five 40 000-sample rollouts, 10-30 s of CPU work).  Runs before anything
     touches the GPU (the worker pools fork)."""
     from oracle import cpu_baseline as cb
     share = cpu_share()
@@ -130,7 +133,8 @@ def cpu_baseline_leg(S, A, args):
         r = cb.run(S, A, workers=w, samples=per_worker * w, expert_rows=args.expert_rows, relabel=False)
         sweep.append((w, r))
     best_w, best = max(sweep, key=lambda x: x[1]["sampler_steps_per_s"])
-    best = cb.run(S, A, workers=best_w, samples=per_worker * best_w, expert_rows=args.expert_rows, relabel=True)
+    best = cb.run(S, A, workers=best_w, samples=max(per_worker * best_w, args.cpu_final_samples),
+                  expert_rows=args.expert_rows, relabel=True)
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -314,7 +318,8 @@ def main():
         st = all_stamps.cpu().numpy()
         gemm_ms = float((st[..., 1] - st[..., 0]).sum()) / 1e5  # 100 MHz ticks -> ms
         n_fwd = args.steps * T
-    launches = n_fwd * (ctx.L + 1)
+    per_fwd = ctx.L + 1  # GEMM launches per forward
+    launches = n_fwd * per_fwd
     flops_per_fwd = ens.mlp_flops_per_sample() * B
     achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
     ens.gemm_events = None
@@ -381,7 +386,7 @@ def main():
                 "timing": ("HIP events around the GEMM launches" if graph is None else
                            "device realtime stamps (amx_timestamp, 100 MHz) around the GEMM launches, captured in "
                            "the graph (ROCm has no timing events in graphs)"),
-                "flops_per_launch": flops_per_fwd / (ctx.L + 1),
+                "flops_per_launch": flops_per_fwd / per_fwd,
             },
             "step_flops_frac": round(value / world * step_flops / (peak * 1e12), 4),
             "cpu_baseline": cpu_base,
