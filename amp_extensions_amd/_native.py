@@ -70,7 +70,7 @@ SIGNATURES = {
     "amx_policy_act_dev": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, vp, c_u64, c_int, vp, vp, vp,
                                    c_ll, c_int, vp]),
     "amx_counter_add": (c_int, [vp, vp, c_ll, vp]),
-    "amx_timestamp": (c_int, [vp, vp, vp]),
+    "amx_set_gemm_timer": (c_int, [vp, vp]),
     "amx_policy_blob_floats": (c_ll, [vp, c_int, c_int]),
     "amx_policy_pack": (c_int, [vp, vp, vp, c_int, vp, vp, c_int, vp, vp, vp, vp]),
     "amx_rff_features": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_flt, vp, c_int,
@@ -80,6 +80,9 @@ SIGNATURES = {
     "amx_mmd_reward": (c_int, [vp, vp, c_int, vp, c_int, vp, c_flt, c_dbl, c_flt, c_flt, vp, vp, vp, c_int, vp]),
     "amx_mmd_reward_raw": (c_int, [vp, vp, c_int, vp, c_int, vp, c_dbl, vp, vp, vp, c_int, vp]),
     "amx_expert_cost": (c_int, [vp, vp, c_int, vp, c_int, c_int, c_flt, c_flt, vp, vp, c_dbl, vp]),
+    "amx_feature_message": (c_int, [vp, vp, c_int, c_int, c_dbl, vp, vp]),
+    "amx_mmd_relabel": (c_int, [vp, vp, c_dbl, vp, c_int, vp, vp, vp, c_int, vp, c_flt, c_dbl, c_int, c_flt, c_flt,
+                                vp, vp, vp, c_int, vp, c_int, c_int, vp, vp, vp, vp]),
     "amx_amp_reward": (c_int, [vp, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
     "amx_disc_reward": (c_int, [vp, c_int, vp, c_int, c_int, vp, c_flt, vp, c_dbl, vp, vp, c_int, vp]),
     "amx_cost_rows": (c_int, [vp, vp, c_ll, c_int, vp, c_ll, c_int, vp, c_ll, c_int, c_int, vp, c_int, vp]),

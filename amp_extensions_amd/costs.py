@@ -104,6 +104,9 @@ class RBFLinearCost:
         self.phi_e = (tot / self.n_expert).float()
         self._expert_out = torch.empty(1 + 1024, dtype=torch.float64, device=ctx.device)
         self._expert_mean = None  # fp32 [1]: get_expert_cost's result (amx_expert_cost mean_out)
+        # set when the last relabel_device launch also computed the expert cost for the current w
+        self._expert_fresh = False
+        self._counter = torch.zeros(4, dtype=torch.int32, device=ctx.device)  # amx_mmd_relabel's arrivals
 
     # linear_cost.py:73-82
     def fit_bandwidth(self, data: torch.Tensor) -> float:
@@ -121,11 +124,38 @@ class RBFLinearCost:
         """Closed-form witness from an (already all-reduced) fp64 feature sum; returns w.w as
         a 1-element device tensor (no host synchronisation)."""
         c = self.ctx
-        if self.w is None:
-            self.w = torch.empty(self.feature_dim, dtype=torch.float32, device=c.device)
-            self._mmd = torch.empty(1, dtype=torch.float32, device=c.device)
+        self._alloc_w()
+        self._expert_fresh = False
         N.check(c.lib.amx_mmd_fit(c.h, phi_sum.data_ptr(), float(count), self.phi_e.data_ptr(), self.feature_dim,
                                   self.w.data_ptr(), self._mmd.data_ptr(), c.stream), "amx_mmd_fit")
+        return self._mmd
+
+    def _alloc_w(self) -> None:
+        if self.w is None:
+            c = self.ctx
+            self.w = torch.empty(self.feature_dim, dtype=torch.float32, device=c.device)
+            self._mmd = torch.empty(1, dtype=torch.float32, device=c.device)
+
+    def relabel_device(self, msg: torch.Tensor, phi, ldphi: int, disc, thr: float, reward, ipm, wb,
+                       n: int) -> torch.Tensor:
+        """The relabel tail in one launch (amx_mmd_relabel): w and w.w from the (all-reduced)
+        [sum phi | count] message, the rewards of n rollout rows (raw device pointers), and,
+        with a cost range, the expert cost for the new w (get_expert_cost then returns it
+        without another pass).  Returns w.w (device, no host synchronisation)."""
+        c = self.ctx
+        self._alloc_w()
+        expert = self.cost_range is not None
+        if expert and self._expert_mean is None:
+            self._expert_mean = torch.empty(1, dtype=torch.float32, device=c.device)
+        N.check(c.lib.amx_mmd_relabel(c.h, msg.data_ptr(), 0.0, self.phi_e.data_ptr(), self.feature_dim,
+                                      self.w.data_ptr(), self._mmd.data_ptr(), phi, ldphi, disc, float(thr),
+                                      self.lambda_b, 1 if expert else 0, self.c_min if expert else 0.0,
+                                      self.c_max if expert else 0.0, reward, ipm, wb, n,
+                                      self.expert_rep.data_ptr() if expert else None, self.expert_rep.stride(0),
+                                      self.n_expert, self._expert_out.data_ptr(),
+                                      self._expert_mean.data_ptr() if expert else None, self._counter.data_ptr(),
+                                      c.stream), "amx_mmd_relabel")
+        self._expert_fresh = expert
         return self._mmd
 
     def fit_w(self, phi_sum: torch.Tensor, count: float) -> float:
@@ -178,6 +208,8 @@ class RBFLinearCost:
         if self.cost_range is None:   # the reference clamps with c_min/c_max, unset without a range
             raise AttributeError("'RBFLinearCost' object has no attribute 'c_min'")
         c = self.ctx
+        if self._expert_fresh:  # computed for the current w by the relabel launch
+            return self._expert_mean[0]
         if self._expert_mean is None:
             self._expert_mean = torch.empty(1, dtype=torch.float32, device=c.device)
         N.check(c.lib.amx_expert_cost(c.h, self.expert_rep.data_ptr(), self.expert_rep.stride(0), self.w.data_ptr(),

@@ -43,6 +43,7 @@ struct amx_ctx {
   int motion_J, motion_D, motion_F;
   double motion_duration;
   int amp_obs_size;          // AMP observation features per transition (0: no character)
+  uint64_t* gemm_timer;      // amx_set_gemm_timer: [start, arrivals, ticks, forwards] or null
   double* d_npg_scratch;     // amx_npg_reduce's run sums
   size_t npg_scratch_bytes;
 };

@@ -144,6 +144,134 @@ __global__ __launch_bounds__(256) void k_sum_small(const double* __restrict__ pa
   }
 }
 
+// ---- the relabel tail in one launch --------------------------------------------------------
+// k_mmd_relabel = k_mmd_fit + k_mmd_reward + k_expert_cost + k_sum_small: every block derives
+// the witness w from the (all-reduced) [sum phi | count] message into LDS (the same fp64
+// divide and fp32 subtraction as k_mmd_fit, so every block holds identical bits); block 0 also
+// publishes w and w.w; blocks [0, nr) score 4 rollout rows each, blocks [nr, nr + ne) 4 expert
+// rows per grid-stride pass.  The expert partials are handed to the last-arriving expert block
+// (agent-scope counter, cdna_hip_programming.md §5 split-K form: sc1 partial stores drained
+// before the relaxed counter add, one acquire in the reducer), which sums them in index order
+// (deterministic) and resets the counter for the next launch.
+struct RelabelArgs {
+  const double* msg; double count; const float* phi_e; int F;
+  float* w; float* mmd;
+  const float* phi; int ldphi; const float* disc; float thr, one_m_lambda, lambda_b, c_min, c_max;
+  float* reward; float* ipm; float* wb; int n, nr;
+  const float* erows; int lde, ne_rows, ne;  // expert rows (null: no expert cost)
+  double* eout;                               // [0] sum, [1 .. ne] block partials
+  float* emean; float escale; uint32_t* counter;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32c;
+
+template <bool CLAMP>
+__global__ __launch_bounds__(256) void k_mmd_relabel(RelabelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float wsh[];  // [F]
+  __shared__ double red[256];
+  __shared__ int last;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  double count = a.count == 0.0 ? a.msg[a.F] : a.count;
+  double acc = 0.0;
+  for (int f = t; f < a.F; f += 256) {
+    const float mean = (float)(a.msg[f] / count);
+    const float wf = mean - a.phi_e[f];
+    wsh[f] = wf;
+    acc += (double)wf * (double)wf;
+  }
+  if (blockIdx.x == 0) {
+    for (int f = t; f < a.F; f += 256) a.w[f] = wsh[f];
+    acc = wave_sum(acc);
+    if (lane == 0) red[wave] = acc;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && t == 0) *a.mmd = (float)(red[0] + red[1] + red[2] + red[3]);
+  if ((int)blockIdx.x < a.nr) {  // rollout rows
+    const int r = blockIdx.x * 4 + wave;
+    if (r >= a.n) return;
+    const double dot = row_dot(a.phi + (long long)r * a.ldphi, wsh, a.F, lane);
+    if (lane != 0) return;
+    float v, bonus;
+    if constexpr (CLAMP) {
+      v = clampf_ref((float)dot, a.c_min, a.c_max);            // linear_cost.py:102
+      float dh = a.disc[r] / a.thr;                            // :132
+      if (dh > 1.0f) dh = 1.0f;                                // :134
+      bonus = dh * a.c_min;                                    // :136
+    } else {
+      v = (float)dot;                                          // :103
+      bonus = a.disc[r];                                       // :139
+    }
+    const float ipm = a.one_m_lambda * v;                      // :141
+    const float wbv = a.lambda_b * bonus;                      // :144
+    const float cost = ipm - wbv;                              // :147
+    a.reward[r] = -1.0f * cost;                                // batch_reinforce.py:144
+    if (a.ipm) a.ipm[r] = ipm;
+    if (a.wb) a.wb[r] = wbv;
+    return;
+  }
+  if (a.ne == 0) return;
+  // expert rows: sum clamp(phi_E[r].w) (linear_cost.py:105-109)
+  const int b = blockIdx.x - a.nr;
+  double e = 0.0;
+  for (int r = b * 4 + wave; r < a.ne_rows; r += a.ne * 4) {
+    const double dot = row_dot(a.erows + (long long)r * a.lde, wsh, a.F, lane);
+    e += (double)clampf_ref((float)dot, a.c_min, a.c_max);
+  }
+  __syncthreads();  // red[] reuse
+  if (lane == 0) red[wave] = e;
+  __syncthreads();
+  if (t == 0) {
+    const double part = red[0] + red[1] + red[2] + red[3];
+    __hip_atomic_store((gu64*)(a.eout + 1 + b), __double_as_longlong(part), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add((gu32c*)a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (uint32_t)(a.ne - 1);
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+  if (!last) return;
+  double s = 0.0;  // ordered: thread t sums t, t + 256, ...; then the fixed tree of k_sum_small
+  for (int i = t; i < a.ne; i += 256)
+    s += __longlong_as_double(__hip_atomic_load((const gu64*)(a.eout + 1 + i), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT));
+  red[t] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) {
+    a.eout[0] = red[0];
+    if (a.emean) a.emean[0] = a.escale * (float)(red[0] / (double)a.ne_rows);  // fp32 product, as torch
+    __hip_atomic_store((gu32c*)a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// [sum phi | count]: the fp64 column sums of the RFF partials (as k_sum_partials) and the
+// sample count in slot F of the same message, so the all-reduce / fit read one buffer.
+__global__ __launch_bounds__(1024) void k_feature_message(const double* __restrict__ partials, int n_parts, int F,
+                                                          double count, double* __restrict__ out) {
+  __shared__ double red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int f = blockIdx.x * 64 + lane;
+  const int per = (n_parts + 15) / 16;
+  const int p0 = w * per, p1 = min(n_parts, p0 + per);
+  double s = 0.0;
+  if (f < F)
+    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && f < F) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][lane];
+    out[f] = t;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[F] = count;
+}
+
 // LOSS 0: least squares (get_ls_costs, gail_cost.py:231-236); LOSS 1: log-likelihood
 // (get_ll_costs, :238-244: cost = logsigmoid(D)).
 template <int LOSS>
@@ -308,6 +436,46 @@ extern "C" int amx_cost_rows(amx_ctx* ctx, const double* x0, long long ld0, int 
   if (B == 0) return AMX_OK;
   hipLaunchKernelGGL(k_cost_rows, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream, x0, ld0, w0, x1, ld1, w1, x2,
                      ld2, w2, B, out, ldc);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_feature_message(amx_ctx* ctx, const double* partials, int n_parts, int F, double count,
+                                   double* out, void* stream) {
+  AMX_CHECK_ARG(ctx && partials && out && n_parts >= 0 && F > 0 && count >= 0.0, "amx_feature_message: bad argument");
+  hipLaunchKernelGGL(k_feature_message, dim3((F + 63) / 64), dim3(1024), 0, (hipStream_t)stream, partials, n_parts,
+                     F, count, out);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_mmd_relabel(amx_ctx* ctx, const double* msg, double count, const float* phi_e, int F, float* w,
+                               float* mmd, const float* phi, int ldphi, const float* disc, float thr, double lambda_b,
+                               int clamp, float c_min, float c_max, float* reward, float* ipm, float* wbonus, int n,
+                               const float* expert_rows, int ld_e, int n_e, double* expert_out, float* expert_mean,
+                               uint32_t* counter, void* stream) {
+  AMX_CHECK_ARG(ctx && msg && phi_e && w && mmd, "amx_mmd_relabel: null pointer");
+  AMX_CHECK_ARG(F > 0 && F % 256 == 0 && F <= 4096, "amx_mmd_relabel: F=%d (multiple of 256, <= 4096)", F);
+  AMX_CHECK_ARG(count >= 0.0, "amx_mmd_relabel: count=%g (0: read msg[F])", count);
+  AMX_CHECK_ARG(n >= 0 && (n == 0 || (phi && disc && reward && ldphi >= F && ldphi % 4 == 0 && amx::aligned16(phi))),
+                "amx_mmd_relabel: rollout rows n=%d need phi/disc/reward, ldphi=%d", n, ldphi);
+  AMX_CHECK_ARG(expert_rows == nullptr || (clamp && n_e > 0 && ld_e >= F && ld_e % 4 == 0 && expert_out && counter &&
+                                           amx::aligned16(expert_rows)),
+                "amx_mmd_relabel: the expert cost needs clamp, n_e > 0, ld_e >= F, expert_out and counter");
+  RelabelArgs a;
+  a.msg = msg; a.count = count; a.phi_e = phi_e; a.F = F; a.w = w; a.mmd = mmd;
+  a.phi = phi; a.ldphi = ldphi; a.disc = disc; a.thr = thr;
+  a.one_m_lambda = (float)(1.0 - lambda_b); a.lambda_b = (float)lambda_b; a.c_min = c_min; a.c_max = c_max;
+  a.reward = reward; a.ipm = ipm; a.wb = wbonus; a.n = n; a.nr = (n + 3) / 4;
+  a.erows = expert_rows; a.lde = ld_e; a.ne_rows = expert_rows ? n_e : 0;
+  a.ne = expert_rows ? ((n_e + 3) / 4 < 1024 ? (n_e + 3) / 4 : 1024) : 0;
+  a.eout = expert_out; a.emean = expert_mean; a.escale = (float)(1.0 - lambda_b); a.counter = counter;
+  const int blocks = (a.nr + a.ne) > 0 ? a.nr + a.ne : 1;
+  const size_t lds = (size_t)F * sizeof(float);
+  if (clamp)
+    hipLaunchKernelGGL(k_mmd_relabel<true>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(k_mmd_relabel<false>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

@@ -702,11 +702,27 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
   }
 }
 
+// amx_set_gemm_timer: the last workgroup of a forward's output layer adds (now - start) to the
+// tick sum (stamps only in a buffer nothing else reads)
+__device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t nwg = (uint32_t)(a.tiles_m * a.tiles_n * a.groups);
+    if (atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 1), 1ull) == nwg - 1) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 2), (unsigned long long)(now - a.timer[0]));
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 3), 1ull);
+      atomicExch(reinterpret_cast<unsigned long long*>(a.timer + 1), 0ull);
+    }
+  }
+}
+
 template <int EPI, class TL>
 __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
   constexpr int NT = TL::NT, STAGE = TL::STAGE;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (a.timer_role == 1 && blockIdx.x == 0 && threadIdx.x == 0) a.timer[0] = __builtin_amdgcn_s_memrealtime();
   uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
   int* sExp = reinterpret_cast<int*>(sm + TL::SEXP);
   int g, tm, tn;
@@ -977,6 +993,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       compute(cur * STAGE);
     }
     finish(acc);
+    if (a.timer_role == 2) gemm_timer_end(a);
     return;
   }
   load(0);
@@ -991,6 +1008,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     __syncthreads();
   }
   finish(acc);
+  if (a.timer_role == 2) gemm_timer_end(a);
 }
 
 // fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
@@ -1388,6 +1406,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   a.rows = rows; a.N = N; a.K = K; a.act = act; a.groups = groups;
   a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots; a.row_exp_out = row_exp_out;
   a.k_shared = k_shared;
+  if (ctx->gemm_timer && rexp_slots == 1) { a.timer = ctx->gemm_timer; a.timer_role = 1; }
   const hipStream_t s = (hipStream_t)stream;
   if (rows % 256 == 0 && N % 256 == 0 && K % 32 == 0 &&
       (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(ctx, H256::LDS, H256::NT, 2))
@@ -1428,6 +1447,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   a.rows = rows; a.K = K; a.groups = groups;
   a.n_valid = n_valid;
   a.row_exp = row_exp; a.strideRexp = strideRexp; a.rexp_slots = rexp_slots; a.k_shared = k_shared;
+  if (ctx->gemm_timer) { a.timer = ctx->gemm_timer; a.timer_role = 2; }
   const int S = ctx->S, Ad = ctx->A;
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
@@ -1489,4 +1509,10 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
   if (K % 32 == 0) return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
   return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);
+}
+
+extern "C" int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf) {
+  AMX_CHECK_ARG(ctx, "amx_set_gemm_timer: null ctx");
+  ctx->gemm_timer = buf;
+  return AMX_OK;
 }

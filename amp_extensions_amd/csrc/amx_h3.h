@@ -40,6 +40,8 @@ struct GemmArgs {
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
   int k_shared;            // leading K columns of A read from group 0's rows for every group
                            //   (the ensemble's x0 slice, assembled once; multiple of the tile's BK)
+  uint64_t* timer;         // amx_set_gemm_timer buffer (null: off)
+  int timer_role;          //   1: first layer of a forward (block 0 stamps the start), 2: output layer
 };
 
 // Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over

@@ -866,15 +866,6 @@ extern "C" int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const f
 __global__ void k_counter_add(uint64_t* c, long long d) { c[0] += (uint64_t)d; }
 
 // the GPU's constant 100 MHz realtime counter at the point the stream reaches this launch
-__global__ void k_timestamp(uint64_t* dst) { dst[0] = (uint64_t)__builtin_amdgcn_s_memrealtime(); }
-
-extern "C" int amx_timestamp(amx_ctx* ctx, uint64_t* dst, void* stream) {
-  AMX_CHECK_ARG(ctx && dst, "amx_timestamp: null pointer");
-  hipLaunchKernelGGL(k_timestamp, dim3(1), dim3(1), 0, (hipStream_t)stream, dst);
-  AMX_CHECK_LAUNCH();
-  return AMX_OK;
-}
-
 extern "C" int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stream) {
   AMX_CHECK_ARG(ctx && counter, "amx_counter_add: null pointer");
   hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, delta);

@@ -57,6 +57,16 @@ class AmxContext:
         except Exception:
             pass
 
+    def gemm_timer(self, on: bool = True):
+        """In-kernel timing of the f16x3 ensemble forwards (amx_set_gemm_timer): returns the
+        device buffer [start, arrivals, ticks (100 MHz), forwards], zeroed; off with on=False."""
+        if not on:
+            N.check(self.lib.amx_set_gemm_timer(self.h, None), "amx_set_gemm_timer")
+            return None
+        self._timer = torch.zeros(4, dtype=torch.int64, device=self.device)
+        N.check(self.lib.amx_set_gemm_timer(self.h, self._timer.data_ptr()), "amx_set_gemm_timer")
+        return self._timer
+
     @property
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -173,13 +183,10 @@ class DeviceEnsemble:
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
         self._ws = {}
-        # optional timing hooks: when a list, every forward appends a (start, end) pair of
-        # torch.cuda.Events recorded on the launch stream around the L+1 GEMM launches; when a
-        # dict {"buf": int64 [n, 2] device tensor, "i": next row}, every forward writes device
-        # realtime stamps (amx_timestamp, 100 MHz) around them instead -- the form that works
-        # inside a captured HIP graph
+        # optional timing hook: when a list, every forward appends a (start, end) pair of
+        # torch.cuda.Events recorded on the launch stream around the L+1 GEMM launches (inside
+        # captured graphs use the context's in-kernel timer instead: AmxContext.gemm_timer)
         self.gemm_events = None
-        self.gemm_stamps = None
 
     @property
     def num_models(self) -> int:
@@ -249,9 +256,7 @@ class DeviceEnsemble:
         if self.W2 is not None and row_exponents:  # x0 row exponents (slot 0) + reset of the hidden slots
             N.check(c.lib.amx_row_exponents(c.h, c.M, Bp, c.k0_pad, buf.data_ptr(), c.ldk, sA, rexp.data_ptr(),
                                             (c.L + 1) * Bp, c.L + 1, s), "amx_row_exponents")
-        ev, st = self.gemm_events, self.gemm_stamps
-        if st is not None:
-            N.check(c.lib.amx_timestamp(c.h, st["buf"][st["i"], 0:].data_ptr(), s), "amx_timestamp")
+        ev = self.gemm_events
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -260,9 +265,6 @@ class DeviceEnsemble:
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1, Bp))
-            if st is not None:
-                N.check(c.lib.amx_timestamp(c.h, st["buf"][st["i"], 1:].data_ptr(), s), "amx_timestamp")
-                st["i"] += 1
             return
         for i in range(c.L):
             K = c.k0_pad + i * c.Hp
@@ -288,9 +290,6 @@ class DeviceEnsemble:
         if ev is not None:
             e1.record()
             ev.append((e0, e1, Bp))
-        if st is not None:
-            N.check(c.lib.amx_timestamp(c.h, st["buf"][st["i"], 1:].data_ptr(), s), "amx_timestamp")
-            st["i"] += 1
 
     def mlp_flops_per_sample(self) -> int:
         """Algorithmic FLOPs of one sample through all members (unpadded shapes)."""

@@ -122,7 +122,6 @@ class RolloutEngine:
         self._graph_ahead = False  # replays advanced dev_step past the host counter
         # [sum phi (F) | count] of the rollout: the one buffer the cross-rank all-reduce touches
         self._fbuf = z(cost.feature_dim + 1, dt=torch.float64) if isinstance(cost, RBFLinearCost) else None
-        self._fbuf_count = None  # the count the message buffer's last slot holds (None: unknown)
         if self._fbuf is not None:  # feature_sum()'s output is the message's first F slots
             self.phi_sum = self._fbuf[:cost.feature_dim]  # (the global sums once all-reduced)
         self.mb_mmd = None
@@ -292,11 +291,7 @@ class RolloutEngine:
     # ------------------------------------------------------------------------------------
     def feature_sum(self) -> torch.Tensor:
         """Ordered fp64 sum of this rank's RFF column partials over the recorded steps."""
-        self.score()
-        c, cost = self.ctx, self.cost
-        n_parts = self.t * (self.Bp // 128)
-        N.check(c.lib.amx_sum_partials(c.h, self.partials.data_ptr(), n_parts, cost.feature_dim,
-                                       self.phi_sum.data_ptr(), c.stream), "amx_sum_partials")
+        self.relabel_pre()
         return self.phi_sum
 
     def relabel(self, allreduce=None) -> dict:
@@ -311,28 +306,29 @@ class RolloutEngine:
         self.relabel_pre()
         if allreduce is not None:
             allreduce(self._fbuf)  # ONE fused all-reduce of [sum phi, count] across ranks
-            self._fbuf_count = None
         return self.relabel_post()
 
     def relabel_pre(self) -> torch.Tensor:
-        """Rank-local half of the relabel: this rank's [sum phi | count] in the persistent
-        fp64 buffer that the cross-rank all-reduce sums (dist.feature_mean's message)."""
-        F = self.cost.feature_dim
-        self.feature_sum()  # phi_sum is a view of the message's first F slots: no copy
-        n = float(self.t * self.B)
-        if self._capturing or self._fbuf_count != n:  # the count slot changes only with T or an all-reduce
-            self._fbuf[F:].fill_(n)
-            self._fbuf_count = None if self._capturing else n
+        """Rank-local half of the relabel: this rank's [sum phi | count] (amx_feature_message)
+        in the persistent fp64 buffer that the cross-rank all-reduce sums (dist.feature_mean's
+        message); phi_sum is a view of its first F slots."""
+        self.score()
+        c, cost = self.ctx, self.cost
+        n_parts = self.t * (self.Bp // 128)
+        N.check(c.lib.amx_feature_message(c.h, self.partials.data_ptr(), n_parts, cost.feature_dim,
+                                          float(self.t * self.B), self._fbuf.data_ptr(), c.stream),
+                "amx_feature_message")
         return self._fbuf
 
     def relabel_post(self) -> dict:
-        """Global half: mean -> witness w (the fp64 mean is rounded to fp32 inside amx_mmd_fit,
-        which reads the count from the message's last slot) -> per-sample rewards of every recorded transition."""
+        """Global half, one launch (amx_mmd_relabel): mean -> witness w (the fp64 mean rounded
+        to fp32, count from the message's last slot) -> per-sample rewards of every recorded
+        transition, and the expert cost for the new w."""
         cost = self.cost
-        self.mb_mmd = cost.fit_w_device(self._fbuf, 0.0)  # count 0: read from the message; no host sync
         n = self.t * self.Bp
-        cost.reward_launch(self.phi.data_ptr(), cost.feature_dim, self.disc.data_ptr(), float(self.ens.threshold),
-                           self.rewards.data_ptr(), self.ipm.data_ptr(), self.wbonus.data_ptr(), n)
+        self.mb_mmd = cost.relabel_device(self._fbuf, self.phi.data_ptr(), cost.feature_dim, self.disc.data_ptr(),
+                                          float(self.ens.threshold), self.rewards.data_ptr(), self.ipm.data_ptr(),
+                                          self.wbonus.data_ptr(), n)
         return {"mb_mmd": self.mb_mmd}
 
     def graph_rollout(self, T: int | None = None, allreduce=None, tail=None):
@@ -379,7 +375,6 @@ class RolloutEngine:
             graphs[0].replay()
             if two:
                 allreduce(self._fbuf)
-                self._fbuf_count = None
                 graphs[1].replay()
             self._graph_ahead = True
             return T * self.B

@@ -270,19 +270,19 @@ def main():
     # HIP graph: the whole rollout (steps, scoring, relabel, expert cost) is captured once and
     # replayed, so per-kernel host launch overhead leaves the timed region (the RCCL all-reduce
     # of N>1 runs eagerly between two graphs).  ROCm has no timing-event nodes in graphs, so
-    # the ensemble GEMM launches are bracketed by device realtime stamps (amx_timestamp,
-    # 100 MHz) captured with them; each replay's stamps are copied aside on the stream.
+    # the ensemble GEMMs time themselves (amx_set_gemm_timer: start stamp in the first layer,
+    # tick sum in the output layer's last workgroup; no extra launches).
     graph = None
-    use_graph = args.graph == "on" or (args.graph == "auto" and B * T < 16384)
+    use_graph = args.graph == "on" or (args.graph == "auto" and B * T < 16384 and args.gemm == "f16x3")
+    if use_graph and args.gemm != "f16x3":
+        raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
     if use_graph:
         tail = cost.get_expert_cost if args.cost == "mmd" else None
-        stamps = torch.zeros(T, 2, dtype=torch.int64, device=dev)
-        ens.gemm_stamps = {"buf": stamps, "i": 0}
+        timer = ctx.gemm_timer()
         graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail)
-        ens.gemm_stamps = None
         graph()  # warm replay
         torch.cuda.synchronize()
-        all_stamps = torch.zeros(args.steps, T, 2, dtype=torch.int64, device=dev)
+        timer.zero_()
 
     # ---- timed region -----------------------------------------------------------------------
     ens.gemm_events = [] if graph is None else None
@@ -297,7 +297,6 @@ def main():
     else:
         for i in range(args.steps):
             samples += graph()
-            all_stamps[i].copy_(stamps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -315,9 +314,10 @@ def main():
         gemm_ms = sum(e0.elapsed_time(e1) for (e0, e1, _) in ens.gemm_events)
         n_fwd = len(ens.gemm_events)
     else:
-        st = all_stamps.cpu().numpy()
-        gemm_ms = float((st[..., 1] - st[..., 0]).sum()) / 1e5  # 100 MHz ticks -> ms
-        n_fwd = args.steps * T
+        tv = timer.cpu().numpy()
+        gemm_ms = float(tv[2]) / 1e5  # 100 MHz ticks -> ms
+        n_fwd = int(tv[3])
+        ctx.gemm_timer(False)
     per_fwd = ctx.L + 1  # GEMM launches per forward
     launches = n_fwd * per_fwd
     flops_per_fwd = ens.mlp_flops_per_sample() * B
@@ -384,8 +384,8 @@ def main():
                 "matrix_pipe_tflops": round(gi["products"] * achieved_tflops, 1) if gi["products"] else None,
                 "avg_launch_us": round(gemm_ms * 1e3 / max(launches, 1), 2),
                 "timing": ("HIP events around the GEMM launches" if graph is None else
-                           "device realtime stamps (amx_timestamp, 100 MHz) around the GEMM launches, captured in "
-                           "the graph (ROCm has no timing events in graphs)"),
+                           "in-kernel device realtime (amx_set_gemm_timer, 100 MHz): first hidden layer's start to "
+                           "the output layer's last workgroup, per forward (ROCm has no timing events in graphs)"),
                 "flops_per_launch": flops_per_fwd / per_fwd,
             },
             "step_flops_frac": round(value / world * step_flops / (peak * 1e12), 4),

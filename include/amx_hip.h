@@ -335,10 +335,14 @@ int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const float* blob,
                        float* mean, float* x0_buf, long long stride_m, int ldk, void* stream);
 int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stream);
 
-/* dst[0] = the device's 100 MHz realtime counter when the stream reaches this launch (a
- * one-thread kernel): kernel timing inside captured HIP graphs, where ROCm has no timing
- * event nodes (bench.py brackets the ensemble GEMM launches with it). */
-int amx_timestamp(amx_ctx* ctx, uint64_t* dst, void* stream);
+/* GEMM timing that works inside captured HIP graphs (ROCm has no timing-event nodes) and adds
+ * no launches: with buf set (4 uint64 of device memory, zeroed by the caller), every f16x3
+ * ensemble forward on this context records the device's 100 MHz realtime counter when its
+ * first hidden layer starts (amx_gemm_bias_act_h3 with rexp_slots = 1: block 0, buf[0]) and,
+ * when the last workgroup of its output layer (amx_gemm_out_unnorm_h3) finishes, adds the
+ * elapsed ticks to buf[2] and 1 to buf[3] (buf[1]: arrival counter, left zero).  The pointer
+ * is read when a launch is issued (graph capture bakes it in).  null: off. */
+int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf);
 
 /* Floats of the packed policy weight image for hidden widths H1, H2 (host query; -1 on a
  * bad argument). */
@@ -394,6 +398,27 @@ int amx_mmd_reward_raw(amx_ctx* ctx, const float* phi, int ldphi, const float* w
 int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
                     float c_min, float c_max, double* out, float* mean_out, double lambda_b,
                     void* stream);
+
+/* The relabel's feature message (batch_reinforce.py:110-113 -> fit_cost's mean,
+ * linear_cost.py:88): out[0..F) = the ordered fp64 column sums of n_parts rows of RFF
+ * partials (as amx_sum_partials), out[F] = count -- the one buffer the cross-rank all-reduce
+ * sums and amx_mmd_relabel reads. */
+int amx_feature_message(amx_ctx* ctx, const double* partials, int n_parts, int F, double count,
+                        double* out, void* stream);
+
+/* The relabel tail in ONE launch (batch_reinforce.py:110-152 with linear_cost.py:84-109):
+ * w = (float)(msg[f] / count) - phi_e[f] and mmd[0] = w.w exactly as amx_mmd_fit (count 0:
+ * read msg[F]); the per-sample pessimistic reward of rows [0, n) of phi exactly as
+ * amx_mmd_reward (clamp = 1: cost_range (c_min, c_max)) or amx_mmd_reward_raw (clamp = 0);
+ * and, when expert_rows is given (clamp only), the expert cost exactly as amx_expert_cost
+ * (expert_out: 1 + 1024 doubles, expert_mean: (1 - lambda_b) * mean in fp32).  `counter` is
+ * one uint32 of device memory, zero before the first launch; the kernel leaves it zero.
+ * One launch at a time per counter. */
+int amx_mmd_relabel(amx_ctx* ctx, const double* msg, double count, const float* phi_e, int F,
+                    float* w, float* mmd, const float* phi, int ldphi, const float* disc, float thr,
+                    double lambda_b, int clamp, float c_min, float c_max, float* reward, float* ipm,
+                    float* wbonus, int n, const float* expert_rows, int ld_e, int n_e,
+                    double* expert_out, float* expert_mean, uint32_t* counter, void* stream);
 
 /* ---- AMP / GAIL least-squares discriminator reward ---------------------------- */
 

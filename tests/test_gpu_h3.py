@@ -296,3 +296,37 @@ def test_graph_replay_matches_eager_rollouts():
             assert torch.equal(xa, xb)
     # successive replays draw fresh policy noise
     assert not torch.equal(runs[1][0][1], runs[1][1][1])
+
+
+@pytest.mark.parametrize("B", [8192, 5120, 640])
+def test_gemm_timer_counts_every_forward(B):
+    """amx_set_gemm_timer: one start stamp per forward (first hidden layer) and one tick sum per
+    output layer, eager and inside a captured graph; the arrival counter is left zero, the
+    forward's results are unchanged."""
+    amx, ctx, ens, ens_w, norms, (s, a) = make(197, 36, [512] * 4, gemms=("f16x3",))
+    e = ens["f16x3"]
+    rs = np.random.RandomState(2)
+    obd = torch.from_numpy(0.5 * rs.randn(B, 197)).to(DEV)
+    acd = torch.from_numpy(rs.randn(B, 36)).to(DEV)
+    ref = e.forward_preds(obd, acd, B).clone()
+    timer = ctx.gemm_timer()
+    for _ in range(3):
+        out = e.forward_preds(obd, acd, B)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    tv = timer.cpu().numpy()
+    assert tv[3] == 3 and tv[1] == 0 and 0 < tv[2] < 3 * 100000  # < 1 ms per forward at 100 MHz
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        with torch.cuda.graph(g, stream=st):
+            e.forward_preds(obd, acd, B)
+    torch.cuda.synchronize()
+    timer.zero_()
+    for _ in range(4):
+        g.replay()
+    torch.cuda.synchronize()
+    tv = timer.cpu().numpy()
+    assert tv[3] == 4 and tv[1] == 0 and tv[2] > 0
+    ctx.gemm_timer(False)
