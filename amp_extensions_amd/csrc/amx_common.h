@@ -44,6 +44,10 @@ struct amx_ctx {
   double motion_duration;
   int amp_obs_size;          // AMP observation features per transition (0: no character)
   uint64_t* gemm_timer;      // amx_set_gemm_timer: [start, arrivals, ticks, forwards] or null
+  float* split_scratch;      // amx_set_split_workspace: split-K partial tiles of the output layer
+  long long split_floats;
+  uint32_t* split_cnt;       //   and its per-tile arrival counters (zero when idle)
+  int split_ncnt;
   double* d_npg_scratch;     // amx_npg_reduce's run sums
   size_t npg_scratch_bytes;
 };

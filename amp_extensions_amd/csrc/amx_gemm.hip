@@ -707,7 +707,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
 __device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t nwg = (uint32_t)(a.tiles_m * a.tiles_n * a.groups);
+    const uint32_t nwg = (uint32_t)(a.tiles_m * a.tiles_n * a.groups * (a.ksplit > 1 ? a.ksplit : 1));
     if (atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 1), 1ull) == nwg - 1) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 2), (unsigned long long)(now - a.timer[0]));
@@ -715,6 +715,63 @@ __device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
       atomicExch(reinterpret_cast<unsigned long long*>(a.timer + 1), 0ull);
     }
   }
+}
+
+typedef __attribute__((address_space(1))) uint32_t gu32s;
+
+// Split-K combine (the output layer at lane counts whose tiles fill the chip only with K split
+// over ksplit workgroups): every slice stores its raw (scaled) accumulators write-through (sc1,
+// 16-B per lane), drains, and adds to the tile's arrival counter (agent scope); the last arriver
+// acquires, sums the slices in slice order -- P0 + P1 + ... whatever the arrival order, so the
+// result is deterministic -- resets the counter and returns true to run the epilogue
+// (cdna_hip_programming.md §5, in-launch split-K: one release and one acquire per tile).
+template <class TL>
+__device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL::MB][TL::NB], int tile, int ks,
+                                              int* flag) {
+  constexpr int MB = TL::MB, NB = TL::NB, NT = TL::NT;
+  const int t = threadIdx.x;
+  const long long per_slice = (long long)MB * NB * NT;  // f32x4 per slice
+  f32x4* base = reinterpret_cast<f32x4*>(a.split_scratch) + (long long)tile * a.ksplit * per_slice;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m][n]), rs,
+                                             (int)(((ks * MB + m) * NB + n) * NT + t) * 16, 0, 16 /* sc1 */);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add((gu32s*)(a.split_cnt + tile), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(a.ksplit - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store((gu32s*)(a.split_cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  f32x4 mine[MB][NB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) mine[m][n] = acc[m][n];
+  for (int s = 0; s < a.ksplit; ++s) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+        const f32x4 v = s == ks ? mine[m][n]
+                                : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
+        acc[m][n] = s == 0 ? v : acc[m][n] + v;
+      }
+  }
+  return true;
 }
 
 template <int EPI, class TL>
@@ -726,7 +783,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
   int* sExp = reinterpret_cast<int*>(sm + TL::SEXP);
   int g, tm, tn;
-  map_tile(a, blockIdx.x, g, tm, tn);
+  const int n_tiles = a.tiles_m * a.tiles_n * a.groups;
+  const int ks = a.ksplit > 1 ? (int)blockIdx.x / n_tiles : 0;  // K slice of a split tile
+  const int tile = a.ksplit > 1 ? (int)blockIdx.x - ks * n_tiles : (int)blockIdx.x;
+  map_tile(a, tile, g, tm, tn);
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const float* __restrict__ Ag0 = a.A + (long long)tm * BM * a.lda;  // group 0: the shared K slice
   const long long ldw2 = 2LL * a.K;
@@ -971,11 +1031,14 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     }
   };
   if constexpr (TL::LATE) {
-    load(0);
+    // K-tiles [kb, ke) of this workgroup (all of them unless the tile is split)
+    const int kb = a.ksplit > 1 ? (ks * nk) / a.ksplit : 0;
+    const int ke = a.ksplit > 1 ? ((ks + 1) * nk) / a.ksplit : nk;
+    load(kb);
     publish(0);
-    load(1);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
+    load(kb + 1);
+    for (int kt = kb; kt < ke; ++kt) {
+      const int cur = (kt - kb) & 1;
       __syncthreads();  // tile kt visible in buffer cur; buffer cur^1 (tile kt-1) fully read
       if constexpr (TL::EARLY) {
         frag0(cur * STAGE);
@@ -991,6 +1054,15 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       load(kt + 2);
       __builtin_amdgcn_sched_barrier(0);
       compute(cur * STAGE);
+    }
+    if constexpr (TL::M16 && EPI == EPI_UNNORM) {
+      if (a.ksplit > 1) {
+        __syncthreads();  // the stage buffers are free: one int of LDS for the last-arriver flag
+        if (!split_combine<TL>(a, acc, tile, ks, reinterpret_cast<int*>(smem) + BM + 4)) {
+          if (a.timer_role == 2) gemm_timer_end(a);
+          return;
+        }
+      }
     }
     finish(acc);
     if (a.timer_role == 2) gemm_timer_end(a);
@@ -1135,7 +1207,7 @@ template <int EPI, class TL>
 int launch_h3(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
   a.tiles_n = a.N / TL::BN;
-  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+  const int nwg = a.tiles_m * a.tiles_n * a.groups * (a.ksplit > 1 ? a.ksplit : 1);
   if (nwg == 0) return AMX_OK;
   constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
@@ -1462,6 +1534,16 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
+    // lane counts whose 128 x 224 tiles fill less than one wave of CUs and whose row-block
+    // tiles would run an odd number of waves per workgroup (5120 lanes: 160-row blocks, 5 waves
+    // on 4 SIMDs): split K three ways over 128 x 224 tiles (14 waves) -> two balanced rounds
+    const int tiles = rows / 128 * groups, ksplit = 3;
+    if (rows % 128 == 0 && rb == 160 && tiles * ksplit <= 2 * ctx->n_cus && (K / 32) % ksplit == 0 &&
+        ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
+        ctx->split_floats >= (long long)tiles * ksplit * 128 * 224) {
+      a.ksplit = ksplit; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+      return launch_h3<EPI_UNNORM, H128x224>(a, s);
+    }
     if (row_tiles) {
       switch (rb) {
         case 128: return launch_h3<EPI_UNNORM, HOut<4, 7>>(a, s);
@@ -1515,4 +1597,25 @@ extern "C" int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf) {
   AMX_CHECK_ARG(ctx, "amx_set_gemm_timer: null ctx");
   ctx->gemm_timer = buf;
   return AMX_OK;
+}
+
+extern "C" int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
+                                       int n_counters) {
+  AMX_CHECK_ARG(ctx, "amx_set_split_workspace: null ctx");
+  AMX_CHECK_ARG((scratch == nullptr) == (counters == nullptr) && floats >= 0 && n_counters >= 0,
+                "amx_set_split_workspace: scratch and counters must be given together");
+  AMX_CHECK_ARG(scratch == nullptr || amx::aligned16(scratch), "amx_set_split_workspace: scratch must be 16-byte aligned");
+  ctx->split_scratch = scratch; ctx->split_floats = scratch ? floats : 0;
+  ctx->split_cnt = counters; ctx->split_ncnt = counters ? n_counters : 0;
+  return AMX_OK;
+}
+
+extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters) {
+  if (!ctx || groups < 1 || rows <= 0) return -1;
+  const int nrb = (ctx->n_cus % (2 * groups) == 0) ? ctx->n_cus / (2 * groups) : 0;
+  const int rb = (nrb > 0 && rows % nrb == 0) ? rows / nrb : 0;
+  const int tiles = rows % 128 == 0 ? rows / 128 * groups : 0;
+  const bool split = rb == 160 && tiles > 0 && tiles * 3 <= 2 * ctx->n_cus && amx::round_up(ctx->S, 32) <= 224;
+  if (n_counters) *n_counters = split ? tiles : 0;
+  return split ? (long long)tiles * 3 * 128 * 224 : 0;
 }

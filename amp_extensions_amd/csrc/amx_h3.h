@@ -40,6 +40,9 @@ struct GemmArgs {
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
   int k_shared;            // leading K columns of A read from group 0's rows for every group
                            //   (the ensemble's x0 slice, assembled once; multiple of the tile's BK)
+  int ksplit;              // > 1: K split over this many workgroups per tile (output layer, M16 tiles)
+  float* split_scratch;    //   raw partial tiles [tile][slice][MB][NB][NT] f32x4 (amx_set_split_workspace)
+  uint32_t* split_cnt;     //   arrivals per tile (zero between launches: the last arriver resets it)
   uint64_t* timer;         // amx_set_gemm_timer buffer (null: off)
   int timer_role;          //   1: first layer of a forward (block 0 stamps the start), 2: output layer
 };

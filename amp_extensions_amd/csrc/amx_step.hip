@@ -160,7 +160,10 @@ struct StepArgs {
 // NIT = ceil(S/64) state elements per lane, kept in registers: all loads of the row are
 // issued up front, and the fall check reads the few values it needs from the owning lanes
 // with shuffles instead of re-loading them (the kernel is latency-bound, not HBM-bound).
-template <int NIT>
+// MM4: the MILO ensemble (M = 4): all four members' rows are loaded in the first phase and
+// the disagreement is formed from registers (one memory round trip instead of two; the same
+// per-lane j order as lane_disagreement, so the same bits).
+template <int NIT, bool MM4>
 __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
@@ -168,17 +171,32 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   const amx_termination& T = a.term;
   const int S = a.S;
   const int k = a.model_idx[b];
-  const float* pk = a.preds + (long long)k * a.strideP + (long long)b * a.ldp;
   const double* ob = a.ob + (long long)b * S;
   double* on = a.ob_next + (long long)b * S;
 
   double o[NIT], x[NIT];
   float p[NIT];
+  float pm[MM4 ? 4 : 1][NIT];
+  if constexpr (MM4) {
+    const float* pb = a.preds + (long long)b * a.ldp;
 #pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int j = lane + 64 * it;
-    o[it] = j < S ? ob[j] : 0.0;
-    p[it] = j < S ? pk[j] : 0.f;
+    for (int it = 0; it < NIT; ++it) {
+      const int j = lane + 64 * it;
+      o[it] = j < S ? ob[j] : 0.0;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) pm[m][it] = j < S ? pb[m * a.strideP + j] : 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it)
+      p[it] = k == 0 ? pm[0][it] : k == 1 ? pm[1][it] : k == 2 ? pm[2][it] : pm[3][it];
+  } else {
+    const float* pk = a.preds + (long long)k * a.strideP + (long long)b * a.ldp;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int j = lane + 64 * it;
+      o[it] = j < S ? ob[j] : 0.0;
+      p[it] = j < S ? pk[j] : 0.f;
+    }
   }
   // sim_env.py:158  ob += state_diff (float32 -> float64), then the in-place velocity
   // rescale of check_velocity (:264-267) when RecordVelAsPos and the check are enabled.
@@ -254,7 +272,31 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
   const bool nf = __ballot(bad) != 0ull;
 
   float d = 0.f;
-  if (a.disc) d = disagreement_dispatch(a.M, a.preds, a.strideP, a.ldp, b, S, lane);
+  if constexpr (MM4) {
+    if (a.disc) {
+      double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        if (lane + 64 * it < S) {
+          int q = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = i + 1; kk < 4; ++kk) {
+              const float df = pm[i][it] - pm[kk][it];
+              acc[q++] += (double)df * (double)df;
+            }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const float n = (float)sqrt(wave_sum(acc[q]));
+        d = (q == 0 || n > d) ? n : d;
+      }
+    }
+  } else {
+    if (a.disc) d = disagreement_dispatch(a.M, a.preds, a.strideP, a.ldp, b, S, lane);
+  }
 
   const int ns = a.num_steps[b] + 1;  // sim_env.py:153 (every lane: a broadcast load)
   const bool horizon_done = ns >= T.horizon;  // :170
@@ -722,8 +764,11 @@ static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long stride
   }
   const int nit = (ctx->S + 63) / 64;
   switch (nit) {
-#define AMX_STEP_CASE(N) \
-  case N: hipLaunchKernelGGL(k_step<N>, lanes_grid(B), dim3(256), 0, (hipStream_t)stream, a); break;
+#define AMX_STEP_CASE(N)                                                                                 \
+  case N:                                                                                                \
+    if (ctx->M == 4) hipLaunchKernelGGL((k_step<N, true>), lanes_grid(B), dim3(256), 0, (hipStream_t)stream, a); \
+    else hipLaunchKernelGGL((k_step<N, false>), lanes_grid(B), dim3(256), 0, (hipStream_t)stream, a);     \
+    break;
     AMX_STEP_CASE(1) AMX_STEP_CASE(2) AMX_STEP_CASE(3) AMX_STEP_CASE(4)
     AMX_STEP_CASE(5) AMX_STEP_CASE(6) AMX_STEP_CASE(7) AMX_STEP_CASE(8)
 #undef AMX_STEP_CASE

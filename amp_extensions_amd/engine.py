@@ -202,8 +202,27 @@ class DeviceEnsemble:
                       preds=torch.zeros(c.M, Bp, c.S, dtype=torch.float32, device=c.device),
                       # f16x3: row exponents of the activation slices [M][L+1][Bp] (x0, h0..h_{L-1})
                       rexp=torch.zeros(c.M, c.L + 1, Bp, dtype=torch.int32, device=c.device))
+            if self.W2 is not None:
+                self._ensure_split_workspace(Bp)
             self._ws[Bp] = ws
         return ws
+
+    def _ensure_split_workspace(self, Bp: int) -> None:
+        """Register the output layer's split-K scratch with the context when Bp lanes split
+        (amx_split_workspace_floats > 0); the buffer only grows."""
+        c = self.ctx
+        nc = N.C.c_int(0)
+        floats = int(c.lib.amx_split_workspace_floats(c.h, c.M, Bp, N.C.byref(nc)))
+        if floats <= 0:
+            return
+        cur = getattr(c, "_split_ws", None)
+        if cur is not None and cur[0].numel() >= floats and cur[1].numel() >= nc.value:
+            return
+        scratch = torch.empty(floats, dtype=torch.float32, device=c.device)
+        counters = torch.zeros(max(nc.value, 1), dtype=torch.int32, device=c.device)
+        N.check(c.lib.amx_set_split_workspace(c.h, scratch.data_ptr(), floats, counters.data_ptr(), nc.value),
+                "amx_set_split_workspace")
+        c._split_ws = (scratch, counters)
 
     def forward_preds(self, ob: torch.Tensor, act: torch.Tensor, B: int | None = None,
                       assembled: bool = False) -> torch.Tensor:

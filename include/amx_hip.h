@@ -344,6 +344,19 @@ int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stre
  * is read when a launch is issued (graph capture bakes it in).  null: off. */
 int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf);
 
+/* Split-K workspace of the f16x3 output layer (amx_gemm_out_unnorm_h3): at lane counts whose
+ * row-block tiles would leave the output layer with an odd number of waves per workgroup
+ * (5120 lanes x 4 members: 160-row blocks), the layer runs as 128 x 224 tiles with K split over
+ * three workgroups whose raw partials the last arriver sums in slice order (deterministic).
+ * amx_split_workspace_floats: floats of scratch (and *n_counters uint32 counters) a forward of
+ * `rows` padded lanes needs, 0 when that shape does not split.  amx_set_split_workspace
+ * registers caller-owned device memory with the context (counters zeroed by the caller once;
+ * each launch leaves them zero); without it the layer runs unsplit.  One launch at a time per
+ * context. */
+long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters);
+int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
+                            int n_counters);
+
 /* Floats of the packed policy weight image for hidden widths H1, H2 (host query; -1 on a
  * bad argument). */
 long long amx_policy_blob_floats(const amx_ctx* ctx, int H1, int H2);

@@ -330,3 +330,29 @@ def test_gemm_timer_counts_every_forward(B):
     tv = timer.cpu().numpy()
     assert tv[3] == 4 and tv[1] == 0 and tv[2] > 0
     ctx.gemm_timer(False)
+
+
+def test_output_split_k_deterministic_and_close_to_unsplit():
+    """5120 lanes x 4 members: the output layer runs split-K (3 slices of K over 128 x 224 tiles,
+    last arriver sums the raw partials in slice order): repeated forwards give the same bits, the
+    arrival counters are left zero, and the result is within fp32 rounding of the unsplit
+    row-block tiles (amx_set_split_workspace unset)."""
+    amx, ctx, ens, ens_w, norms, (s, a) = make(197, 36, [512] * 4, gemms=("f16x3",))
+    e = ens["f16x3"]
+    B = 5120
+    rs = np.random.RandomState(3)
+    obd = torch.from_numpy(0.5 * rs.randn(B, 197)).to(DEV)
+    acd = torch.from_numpy(rs.randn(B, 36)).to(DEV)
+    p1 = e.forward_preds(obd, acd, B).clone()
+    assert getattr(ctx, "_split_ws", None) is not None, "5120 lanes should register the split-K workspace"
+    p2 = e.forward_preds(obd, acd, B).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(p1, p2)
+    assert int(ctx._split_ws[1].abs().sum().item()) == 0
+    ctx.lib.amx_set_split_workspace(ctx.h, None, 0, None, 0)
+    p0 = e.forward_preds(obd, acd, B).clone()
+    scratch, counters = ctx._split_ws
+    ctx.lib.amx_set_split_workspace(ctx.h, scratch.data_ptr(), scratch.numel(), counters.data_ptr(), counters.numel())
+    torch.cuda.synchronize()
+    d = (p1 - p0).abs().max().item()
+    assert d <= 1e-6 * max(1.0, p0.abs().max().item()), d
