@@ -175,7 +175,8 @@ class RolloutEngine:
         if t >= self.K:
             raise RuntimeError(f"rollout buffer full ({self.K} steps): call begin_rollout()")
         s = c.stream
-        if t == 0:
+        fused = self.auto_reset and self.motion is None and self.fuse_reset
+        if t == 0 and not fused:  # (the fused step kernel records it itself: steps0_out)
             self.steps0.copy_(self.num_steps)
         ob, ob_next, act = self.obs[t], self.next_obs[t], self.acts[t]
         if actions is not None:
@@ -192,7 +193,6 @@ class RolloutEngine:
                             eval_mode=self.eval_mode, mean_out=None if self.means is None else self.means[t],
                             counter_dev=self.dev_step if self._capturing else None)
         preds = self.ens.forward_preds(ob, act, B)
-        fused = self.auto_reset and self.motion is None and self.fuse_reset
         if fused:  # step + table reset in one pass (amx_step_reset)
             ss = self.cost_type == "ss"
             N.check(c.lib.amx_step_reset(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
@@ -203,7 +203,8 @@ class RolloutEngine:
                                          self.nonfinite[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
                                          None if reset_rows is None else reset_rows.data_ptr(), self.seed,
                                          self.obs[t + 1].data_ptr(), self.reset_count.data_ptr(),
-                                         self.reset_rows[t].data_ptr(), B, s), "amx_step_reset")
+                                         self.reset_rows[t].data_ptr(), self.steps0.data_ptr() if t == 0 else None,
+                                         B, s), "amx_step_reset")
         elif self.cost_type == "ss" and self.cost_rexp is not None:
             N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                         ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),

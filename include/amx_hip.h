@@ -284,12 +284,13 @@ int amx_step_rexp(amx_ctx* ctx, const float* preds, int ldp, long long strideP, 
  * ob_src = ob_next) in one pass: done lanes get reset_count/model_idx/num_steps/row_out
  * and ob_out[b] = table[row] exactly as amx_reset_lanes; the others ob_out[b] = ob_next[b]
  * (from registers, no re-read).  ob_out must differ from ob and ob_next; model_idx is
- * read (the member of this step) and, for reset lanes, rewritten. */
+ * read (the member of this step) and, for reset lanes, rewritten.  steps0_out (nullable):
+ * receives num_steps before this step (the trajectory position of a rollout's first slot). */
 int amx_step_reset(amx_ctx* ctx, const float* preds, int ldp, long long strideP, int32_t* model_idx,
                    const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
                    float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, const double* table,
                    int R, const int32_t* rows, uint64_t seed, double* ob_out, int32_t* reset_count,
-                   int32_t* row_out, int B, void* stream);
+                   int32_t* row_out, int32_t* steps0_out, int B, void* stream);
 
 /* Disagreement only (DynamicsEnsemble.get_action_discrepancy / compute_threshold,
  * milo/milo/dynamics.py:145-165). */
