@@ -66,9 +66,9 @@ SIGNATURES = {
     "amx_disagreement": (c_int, [vp, vp, c_int, c_ll, vp, c_int, vp]),
     "amx_reset_lanes": (c_int, [vp, vp, vp, c_int, vp, c_u64, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_policy_act": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, c_u64, c_int, vp, vp, vp, c_ll,
-                               c_int, vp]),
+                               c_int, vp, c_ll, c_ll, c_int, vp]),
     "amx_policy_act_dev": (c_int, [vp, vp, c_int, vp, c_int, c_int, vp, vp, c_u64, vp, c_u64, c_int, vp, vp, vp,
-                                   c_ll, c_int, vp]),
+                                   c_ll, c_int, vp, c_ll, c_ll, c_int, vp]),
     "amx_counter_add": (c_int, [vp, vp, c_ll, vp]),
     "amx_set_gemm_timer": (c_int, [vp, vp]),
     "amx_split_workspace_floats": (c_ll, [vp, c_int, c_int, ip]),

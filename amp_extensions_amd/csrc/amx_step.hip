@@ -413,6 +413,7 @@ struct PolicyArgs {
   const uint64_t* ctr_dev;  // nullable: the counter read from device memory (graph replays)
   double* act; float* mean_out;
   float* x0; long long stride_m; int ldk; int k0_pad; int M; const float* norm;
+  int* row_exp; long long stride_rexp; long long slot_stride; int n_slots;  // nullable (k_assemble's)
   int S, A, B;
 };
 
@@ -624,24 +625,44 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   }
   if (!p.x0) return;
   __syncthreads();
-  // fused amx_assemble_input (dynamics.py:225-227): the block's POL_LANES rows of x0 for every
-  // model, written row-contiguously (consecutive threads -> consecutive columns)
+  // fused amx_assemble_input[_rexp] (dynamics.py:225-227), one wave per row as k_assemble: the
+  // block's POL_LANES rows of x0 (once when stride_m is 0: the f16x3 GEMMs read every model's x0
+  // slice from model 0's rows, else for every model), and with row_exp slot 0 = the exponent of
+  // the row's max |x0| and slots 1..n_slots-1 reset, for every model
   const float* mu_s = p.norm;
   const float* sd_s = p.norm + S;
   const float* mu_a = p.norm + 2 * S;
   const float* sd_a = p.norm + 2 * S + A;
   const int k0 = p.k0_pad;
-  for (int i = t; i < POL_LANES * k0; i += 256) {
-    const int ll = i / k0, j = i - ll * k0;
+  const int lane = t & 63, wave = t >> 6;
+  const int copies = p.stride_m == 0 ? 1 : p.M;
+  for (int ll = wave; ll < POL_LANES; ll += 256 / 64) {
     const int bb = b0 + ll;
-    if (bb >= p.B) continue;
-    float x = 0.f;
-    if (j < S) {
-      x = (so[ll * s1 + j] - mu_s[j]) / sd_s[j];
-    } else if (j < S + A) {
-      x = (xa_s[ll * A + j - S] - mu_a[j - S]) / sd_a[j - S];
+    if (bb >= p.B) break;  // wave-uniform; rows only grow
+    uint32_t mx = 0;
+    for (int j = lane; j < k0; j += 64) {
+      float x = 0.f;
+      if (j < S) {
+        x = (so[ll * s1 + j] - mu_s[j]) / sd_s[j];
+      } else if (j < S + A) {
+        x = (xa_s[ll * A + j - S] - mu_a[j - S]) / sd_a[j - S];
+      }
+      for (int mm = 0; mm < copies; ++mm) p.x0[mm * p.stride_m + (long long)bb * p.ldk + j] = x;
+      const uint32_t bits = __float_as_uint(x) & 0x7fffffffu;
+      mx = mx > bits ? mx : bits;
     }
-    for (int mm = 0; mm < p.M; ++mm) p.x0[mm * p.stride_m + (long long)bb * p.ldk + j] = x;
+    if (p.row_exp == nullptr) continue;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
+      mx = mx > o ? mx : o;
+    }
+    if (lane < p.n_slots) {
+      int e = (int)(mx >> 23) - 126;  // max|x0| < 2^e, clamped as the GEMM's exponents
+      e = e < -100 ? -100 : (e > 100 ? 100 : e);
+      const int v = lane == 0 ? e : -100;
+      for (int mm = 0; mm < p.M; ++mm) p.row_exp[mm * p.stride_rexp + lane * p.slot_stride + bb] = v;
+    }
   }
 }
 
@@ -854,7 +875,8 @@ extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, i
 static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                       const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                       const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
-                      long long stride_m, int ldk, void* stream) {
+                      long long stride_m, int ldk, int* row_exp, long long stride_rexp, long long slot_stride,
+                      int n_slots, void* stream) {
   AMX_CHECK_ARG(ctx && ob && blob && act, "amx_policy_act: null pointer");
   AMX_CHECK_ARG(amx::aligned16(blob), "amx_policy_act: blob must be 16-byte aligned");
   AMX_CHECK_ARG(eval_mode || noise_scale, "amx_policy_act: noise_scale required unless eval_mode");
@@ -862,8 +884,11 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
                 "amx_policy_act: S=%d H1=%d H2=%d A=%d (max %d)", ctx->S, H1, H2, ctx->A, POL_MAXH);
   AMX_CHECK_ARG(B >= 0, "amx_policy_act: B=%d", B);
   AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
-                            (ctx->M == 1 || stride_m >= (long long)ldk * B)),
+                            (ctx->M == 1 || stride_m == 0 || stride_m >= (long long)ldk * B)),
                 "amx_policy_act: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B");
+  AMX_CHECK_ARG(!row_exp || (x0_buf && n_slots >= 1 && n_slots <= 64 && slot_stride >= B &&
+                             (ctx->M == 1 || stride_rexp >= (long long)n_slots * slot_stride)),
+                "amx_policy_act: row_exp needs x0_buf, 1 <= n_slots <= 64, slot_stride >= B, stride_rexp");
   if (B == 0) return AMX_OK;
   // 16 threads per lane, 16 lanes per workgroup (32 threads per lane measured 1.3 % slower
   // per rollout in round 1, profiles/r01_policy_tpl.txt)
@@ -879,6 +904,7 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
   p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode; p.ctr_dev = counter_dev;
   p.act = act; p.mean_out = mean;
   p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
+  p.row_exp = row_exp; p.stride_rexp = stride_rexp; p.slot_stride = slot_stride; p.n_slots = n_slots;
   p.S = ctx->S; p.A = ctx->A; p.B = B;
   dim3 grid((B + lanes - 1) / lanes);
   // outputs per thread, rounded up to a compiled width: hidden layers QH, action layer QA
@@ -896,18 +922,20 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
 extern "C" int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                               const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                               int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
+                              int* row_exp, long long stride_rexp, long long slot_stride, int n_slots,
                               void* stream) {
   return policy_act(ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, counter, nullptr, eval_mode, act, mean,
-                    x0_buf, stride_m, ldk, stream);
+                    x0_buf, stride_m, ldk, row_exp, stride_rexp, slot_stride, n_slots, stream);
 }
 
 extern "C" int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                                   const double* noise_scale, const double* noise, uint64_t seed,
                                   const uint64_t* counter, uint64_t counter_offset, int eval_mode, double* act,
-                                  float* mean, float* x0_buf, long long stride_m, int ldk, void* stream) {
+                                  float* mean, float* x0_buf, long long stride_m, int ldk, int* row_exp,
+                                  long long stride_rexp, long long slot_stride, int n_slots, void* stream) {
   AMX_CHECK_ARG(counter, "amx_policy_act_dev: null counter");
   return policy_act(ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, counter_offset, counter, eval_mode, act,
-                    mean, x0_buf, stride_m, ldk, stream);
+                    mean, x0_buf, stride_m, ldk, row_exp, stride_rexp, slot_stride, n_slots, stream);
 }
 
 __global__ void k_counter_add(uint64_t* c, long long d) { c[0] += (uint64_t)d; }

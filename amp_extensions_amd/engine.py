@@ -225,9 +225,11 @@ class DeviceEnsemble:
         c._split_ws = (scratch, counters)
 
     def forward_preds(self, ob: torch.Tensor, act: torch.Tensor, B: int | None = None,
-                      assembled: bool = False) -> torch.Tensor:
+                      assembled: bool = False, x0_ready: bool = False) -> torch.Tensor:
         """All members' un-normalised deltas for rows [0, B): returns preds [M, Bp, S] (view
-        of the workspace; rows >= B are padding).  ob/act fp64 or fp32 on the device."""
+        of the workspace; rows >= B are padding).  ob/act fp64 or fp32 on the device.
+        `x0_ready` (f16x3): the caller (amx_policy_act's fused assembly) already wrote the shared
+        x0 slice into model 0's rows and the row-exponent slots of the workspace."""
         c = self.ctx
         B = ob.shape[0] if B is None else B
         if ob.dtype != act.dtype or ob.dtype not in (torch.float64, torch.float32):
@@ -242,6 +244,11 @@ class DeviceEnsemble:
         s = c.stream
         rexp = ws["rexp"]
         k_shared = 0
+        if x0_ready:
+            if self.W2 is None:
+                raise ValueError("x0_ready needs the f16x3 GEMM (shared x0 slice + row exponents)")
+            self._mlp(buf, preds, Bp, s, rexp, row_exponents=False, k_shared=c.k0_pad)
+            return preds
         if not assembled and self.W2 is not None:  # x0 + its row exponents in one pass
             # shared_x0: one x0 copy (model 0's rows) that every model's GEMMs read (k_shared)
             k_shared = c.k0_pad if self.shared_x0 else 0

@@ -63,25 +63,32 @@ class DevicePolicy:
 
     def act(self, ob: torch.Tensor, B: int, out: torch.Tensor, counter: int, noise: torch.Tensor | None = None,
             eval_mode: bool = False, mean_out: torch.Tensor | None = None, x0: torch.Tensor | None = None,
-            counter_dev: torch.Tensor | None = None) -> torch.Tensor:
+            counter_dev: torch.Tensor | None = None, row_exp: torch.Tensor | None = None,
+            shared_x0: bool = False) -> torch.Tensor:
         """Actions of B lanes into `out` [B, A] f64.  `x0` (the ensemble workspace's activation
-        buffer [M, B_pad, ldk]) fuses the ensemble's input assembly into the same launch.
-        `counter_dev` (int64 [1] on the device): the Philox counter is counter_dev[0] + `counter`
-        (amx_policy_act_dev: HIP-graph replays draw fresh noise)."""
+        buffer [M, B_pad, ldk]) fuses the ensemble's input assembly into the same launch
+        (`shared_x0`: once, into model 0's rows, for the f16x3 GEMMs' k_shared slice);
+        `row_exp` (the workspace's [M, L+1, B_pad] f16x3 exponent slots) also writes slot 0 and
+        resets the others, as amx_assemble_input_rexp.  `counter_dev` (int64 [1] on the device):
+        the Philox counter is counter_dev[0] + `counter` (amx_policy_act_dev: HIP-graph replays
+        draw fresh noise)."""
         c = self.ctx
+        x0p = None if x0 is None else x0.data_ptr()
+        sm = 0 if (x0 is None or shared_x0) else x0.stride(0)
+        ldk = 0 if x0 is None else x0.stride(1)
+        rx = (None, 0, 0, 0) if row_exp is None else (row_exp.data_ptr(), row_exp.stride(0), row_exp.stride(1),
+                                                      row_exp.shape[1])
         if counter_dev is not None:
             N.check(c.lib.amx_policy_act_dev(
                 c.h, ob.data_ptr(), B, self.blob.data_ptr(), self.H1, self.H2, self.noise_scale.data_ptr(),
                 None if noise is None else noise.data_ptr(), self.seed, counter_dev.data_ptr(),
                 int(counter) & 0xFFFFFFFFFFFFFFFF, int(eval_mode),
-                out.data_ptr(), None if mean_out is None else mean_out.data_ptr(),
-                None if x0 is None else x0.data_ptr(), 0 if x0 is None else x0.stride(0),
-                0 if x0 is None else x0.stride(1), c.stream), "amx_policy_act_dev")
+                out.data_ptr(), None if mean_out is None else mean_out.data_ptr(), x0p, sm, ldk, *rx, c.stream),
+                "amx_policy_act_dev")
             return out
         N.check(c.lib.amx_policy_act(
             c.h, ob.data_ptr(), B, self.blob.data_ptr(), self.H1, self.H2, self.noise_scale.data_ptr(),
             None if noise is None else noise.data_ptr(), self.seed, int(counter) & 0xFFFFFFFFFFFFFFFF,
-            int(eval_mode), out.data_ptr(), None if mean_out is None else mean_out.data_ptr(),
-            None if x0 is None else x0.data_ptr(), 0 if x0 is None else x0.stride(0),
-            0 if x0 is None else x0.stride(1), c.stream), "amx_policy_act")
+            int(eval_mode), out.data_ptr(), None if mean_out is None else mean_out.data_ptr(), x0p, sm, ldk, *rx,
+            c.stream), "amx_policy_act")
         return out

@@ -52,6 +52,10 @@ class RolloutEngine:
         self.eval_mode = eval_mode
         self.auto_reset = auto_reset
         self.fuse_reset = True  # table resets run inside the step kernel (amx_step_reset)
+        # f16x3: the policy launch writes the ensemble's x0 + row exponents (bit-identical, tested;
+        # off: 32.9 us vs 22.2 + 7.3 us for policy + separate assembly at 8192 lanes,
+        # profiles/r02_policy_ab.txt)
+        self.fuse_assembly = False
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
         from .motion import ReferenceMotion
@@ -179,20 +183,26 @@ class RolloutEngine:
         if t == 0 and not fused:  # (the fused step kernel records it itself: steps0_out)
             self.steps0.copy_(self.num_steps)
         ob, ob_next, act = self.obs[t], self.next_obs[t], self.acts[t]
+        x0_ready = False
         if actions is not None:
             act.copy_(actions)
         else:
             if self.policy is None:
                 raise RuntimeError("no policy and no actions given")
-            # (amx_policy_act can also write the ensemble's x0 rows itself, but measured slower
-            # than the separate row-per-wave assembly kernel: 36.5 vs 20.4 + 8.6 us at 8192 lanes)
             if self._graph_ahead and not self._capturing:  # continue after graph replays
                 self.step_counter = int(self.dev_step.item())
                 self._graph_ahead = False
+            # f16x3 with the shared x0 slice: the policy launch also writes x0 (once, model 0's
+            # rows) and its row exponents, as amx_assemble_input_rexp (one launch fewer per step)
+            fuse_x0 = self.fuse_assembly and self.ens.W2 is not None and self.ens.shared_x0
+            ws = self.ens.workspace(B) if fuse_x0 else None
             self.policy.act(ob, B, act, t if self._capturing else self.step_counter, noise=noise,
                             eval_mode=self.eval_mode, mean_out=None if self.means is None else self.means[t],
-                            counter_dev=self.dev_step if self._capturing else None)
-        preds = self.ens.forward_preds(ob, act, B)
+                            counter_dev=self.dev_step if self._capturing else None,
+                            x0=None if ws is None else ws["act"], row_exp=None if ws is None else ws["rexp"],
+                            shared_x0=fuse_x0)
+            x0_ready = fuse_x0
+        preds = self.ens.forward_preds(ob, act, B, x0_ready=x0_ready)
         if fused:  # step + table reset in one pass (amx_step_reset)
             ss = self.cost_type == "ss"
             N.check(c.lib.amx_step_reset(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),

@@ -321,10 +321,13 @@ int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* table, int 
  * noise_scale = exp(log_std) in fp64 (device, [A]).
  * x0_buf (nullable) fuses the ensemble's state assembly (amx_assemble_input with
  * AMX_IN_F64) for the same lanes: x0 = [(float(ob)-mu_s)/sd_s, (float(act)-mu_a)/sd_a, 0]
- * written to every model's activation row (stride_m, ldk as in amx_assemble_input). */
+ * written to every model's activation row (stride_m, ldk as in amx_assemble_input; stride_m
+ * 0: once, model 0's rows, the f16x3 GEMMs' shared x0 slice); row_exp (nullable, needs x0_buf)
+ * additionally writes the f16x3 row-exponent slots exactly as amx_assemble_input_rexp. */
 int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                    const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                    int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,
+                   int* row_exp, long long stride_rexp, long long slot_stride, int n_slots,
                    void* stream);
 
 /* amx_policy_act with the Philox counter = counter[0] (device memory) + counter_offset, so a
@@ -333,7 +336,8 @@ int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int
 int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                        const double* noise_scale, const double* noise, uint64_t seed,
                        const uint64_t* counter, uint64_t counter_offset, int eval_mode, double* act,
-                       float* mean, float* x0_buf, long long stride_m, int ldk, void* stream);
+                       float* mean, float* x0_buf, long long stride_m, int ldk, int* row_exp,
+                       long long stride_rexp, long long slot_stride, int n_slots, void* stream);
 int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stream);
 
 /* GEMM timing that works inside captured HIP graphs (ROCm has no timing-event nodes) and adds

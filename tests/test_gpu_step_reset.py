@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def _engines(cost_kind):
+def _engines(cost_kind, flag="fuse_reset"):
     import amp_extensions_amd as amx
     from amp_extensions_amd.humanoid import TerminationConfig
     S, A, B = 197, 36, 320
@@ -37,7 +37,7 @@ def _engines(cost_kind):
             cost = None
         pol = amx.DevicePolicy(ctx, pw, log_std, seed=1)
         eng = amx.RolloutEngine(ens, s[:97], lanes=B, policy=pol, cost=cost, seed=2, max_steps=8)
-        eng.fuse_reset = fused
+        setattr(eng, flag, fused)
         out.append(eng)
     return out
 
@@ -97,3 +97,26 @@ def test_policy_fused_assembly_bit_identical(hidden):
     obn = ob.cpu().numpy()
     ref = np.stack([R.policy_mean(pw, obn[i]) for i in range(0, B, 37)])  # the oracle's float32 MLP
     np.testing.assert_allclose(outs[1][1].cpu().numpy()[::37], ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("cost_kind", ["mmd", "gail"])
+def test_policy_fused_x0_matches_separate_assembly(cost_kind):
+    """RolloutEngine.fuse_assembly (the policy launch writes the shared x0 slice and its row
+    exponents, amx_policy_act with row_exp) against the separate amx_assemble_input_rexp launch:
+    every lane buffer, the ensemble workspace and the rewards bit-identical over two rollouts."""
+    engs = _engines(cost_kind, flag="fuse_assembly")
+    for eng in engs:
+        eng.reset_all()
+        for _ in range(2):
+            eng.rollout()
+            eng.relabel()
+    torch.cuda.synchronize()
+    ref, got = engs
+    for n in ["obs", "next_obs", "acts", "done", "disc", "num_steps", "model_idx", "cost_in", "cost_rexp",
+              "rewards", "steps0"]:
+        x, y = getattr(ref, n, None), getattr(got, n, None)
+        if x is None:
+            continue
+        torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True, msg=n)  # (padding rows are NaN)
+    wr, wg = ref.ens.workspace(ref.B), got.ens.workspace(got.B)
+    assert torch.equal(wr["preds"], wg["preds"]) and torch.equal(wr["rexp"], wg["rexp"])

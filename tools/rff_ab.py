@@ -7,7 +7,7 @@ res = {}
 for tag in sys.argv[1:]:
     path = _build.LIB_PATH if tag == "base" else _build.LIB_PATH.replace(".so", f"_{tag}.so")
     lib = N.load(path)
-    rows = 40960
+    rows = int(os.environ.get("RFF_ROWS", "40960"))
     S = 197
     ctx_h = lib.amx_create(0, S, 1, 1, 128, 0, 512)
     dev = "cuda"
@@ -30,4 +30,4 @@ for tag in sys.argv[1:]:
     ts = []
     for _ in range(20):
         e0.record(); run(); e1.record(); torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1) * 1e3)
-    print(f"{tag:8s} rff_features_h3 40960 rows: median {np.median(ts):.1f} us, min {min(ts):.1f}", flush=True)
+    print(f"{tag:8s} rff_features_h3 {rows} rows: median {np.median(ts):.1f} us, min {min(ts):.1f}", flush=True)
