@@ -1,8 +1,8 @@
 """Build recipe for libamx_hip.so (the C-ABI HIP library) — in-tree, gfx950 only.
 
 `python -m amp_extensions_amd._build` or `__graft_entry__.build()` compiles every
-`csrc/*.hip` with hipcc into `amp_extensions_amd/libamx_hip.so`.  The build is
-incremental on source/header mtimes.  -ffp-contract=off keeps the scalar state /
+`csrc/*.hip` with hipcc (one object per source, in parallel, under `build/`) and links
+`amp_extensions_amd/libamx_hip.so`.  The build is incremental on source/header mtimes.  -ffp-contract=off keeps the scalar state /
 termination / reward algebra rounding exactly like the reference's separate IEEE ops
 (the GEMM inner loops are MFMA and are unaffected).
 """
@@ -56,16 +56,42 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(p) <= t for p in _deps())
 
 
+def _obj(src: str) -> str:
+    return os.path.join(PKG_DIR, "build", os.path.basename(src)[:-4] + ".o")
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
-    """Compile libamx_hip.so in-tree; returns its path."""
+    """Compile libamx_hip.so in-tree; returns its path.  Each csrc/*.hip is compiled to its
+    own object in parallel (recompiled when it or any header is newer), then linked."""
     if not force and up_to_date():
         return LIB_PATH
-    cmd = [_hipcc(), *HIPCC_FLAGS, "-I", INCLUDE, "-o", LIB_PATH + ".tmp", *sources()]
+    os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
+    hdr_t = max((os.path.getmtime(p) for p in _deps() if not p.endswith(".hip")), default=0.0)
+    cc = [_hipcc(), *[f for f in HIPCC_FLAGS if f != "-shared"], "-I", INCLUDE]
+    procs = []
+    for src in sources():
+        obj = _obj(src)
+        if force or not os.path.exists(obj) or os.path.getmtime(obj) < max(os.path.getmtime(src), hdr_t):
+            cmd = [*cc, "-c", "-o", obj + ".tmp", src]
+            if verbose:
+                print("[amx build]", " ".join(cmd), flush=True)
+            procs.append((obj, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    errs = []
+    for obj, pr in procs:
+        out, _ = pr.communicate()
+        if pr.returncode != 0:
+            errs.append(out)
+        else:
+            os.replace(obj + ".tmp", obj)
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB_PATH + ".tmp",
+           *[_obj(s) for s in sources()]]
     if verbose:
         print("[amx build]", " ".join(cmd), flush=True)
     res = subprocess.run(cmd, capture_output=True, text=True)
     if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+        raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
     return LIB_PATH
 

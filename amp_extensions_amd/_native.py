@@ -60,7 +60,7 @@ SIGNATURES = {
     "amx_step": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_int, vp]),
     "amx_step_rexp": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, c_int, vp]),
     "amx_step_reset": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, vp, c_int, vp,
-                               c_u64, vp, vp, vp, vp, c_int, vp]),
+                               c_u64, vp, vp, vp, vp, vp, c_ll, vp, c_int, vp]),
     "amx_rff_features_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp, vp, c_flt, vp, c_int,
                                     vp, vp, vp]),
     "amx_disagreement": (c_int, [vp, vp, c_int, c_ll, vp, c_int, vp]),

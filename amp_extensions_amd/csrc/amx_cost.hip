@@ -145,14 +145,69 @@ __global__ __launch_bounds__(256) void k_sum_small(const double* __restrict__ pa
 }
 
 // ---- the relabel tail in one launch --------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32c;
+
+// Batched row dots for the relabel: NC = F/256 float4 chunks per lane (lane l reads floats
+// 4l + 256c of a row, exactly row_dot's per-lane order, then the same wave butterfly), R rows
+// loaded per wave before any arithmetic so one memory round trip serves R rows (row_dot waits
+// one trip per row).  The per-row result has row_dot's bits; NC = 0 is the generic-F path.
+template <int NC>
+constexpr int relabel_rows() { return NC == 0 ? 1 : (8 / NC > 0 ? 8 / NC : 1); }
+
+template <int NC, int R>
+__device__ inline void rows_load(const float* __restrict__ base, int ld, int r0, int step, int nrows, int lane,
+                                 float4 (&p)[R][NC > 0 ? NC : 1]) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const int r = r0 + i * step;
+#pragma unroll
+    for (int c = 0; c < (NC > 0 ? NC : 1); ++c)
+      p[i][c] = (NC > 0 && r < nrows) ? *reinterpret_cast<const float4*>(base + (long long)r * ld + lane * 4 + 256 * c)
+                                      : float4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <int NC, int R>
+__device__ inline void rows_dot(const float4 (&p)[R][NC > 0 ? NC : 1], const float* __restrict__ base, int ld,
+                                int r0, int step, int nrows, const float* __restrict__ w, int F, int lane,
+                                double (&d)[R]) {
+  if constexpr (NC == 0) {  // generic F: one row at a time (row_dot)
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int r = r0 + i * step;
+      d[i] = r < nrows ? row_dot(base + (long long)r * ld, w, F, lane) : 0.0;
+    }
+  } else {
+    float4 q[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) q[c] = *reinterpret_cast<const float4*>(w + lane * 4 + 256 * c);
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        s += (double)p[i][c].x * q[c].x + (double)p[i][c].y * q[c].y + (double)p[i][c].z * q[c].z +
+             (double)p[i][c].w * q[c].w;
+      d[i] = s;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int i = 0; i < R; ++i) d[i] += __shfl_xor(d[i], o);
+  }
+}
+
 // k_mmd_relabel = k_mmd_fit + k_mmd_reward + k_expert_cost + k_sum_small: every block derives
 // the witness w from the (all-reduced) [sum phi | count] message into LDS (the same fp64
 // divide and fp32 subtraction as k_mmd_fit, so every block holds identical bits); block 0 also
-// publishes w and w.w; blocks [0, nr) score 4 rollout rows each, blocks [nr, nr + ne) 4 expert
-// rows per grid-stride pass.  The expert partials are handed to the last-arriving expert block
-// (agent-scope counter, cdna_hip_programming.md §5 split-K form: sc1 partial stores drained
-// before the relaxed counter add, one acquire in the reducer), which sums them in index order
-// (deterministic) and resets the counter for the next launch.
+// publishes w and w.w; blocks [0, nr) score R rollout rows per wave, blocks [nr, nr + ne)
+// the expert rows b*4 + wave + k*4ne (k_expert_cost's assignment and per-wave order, R per
+// round trip).  Each wave issues its first rows' loads before the witness prologue.  The
+// expert partials are handed to the last-arriving expert block (agent-scope counter,
+// cdna_hip_programming.md §5 split-K form: sc1 partial stores drained before the relaxed
+// counter add, one acquire in the reducer), which sums them in index order (deterministic)
+// and resets the counter for the next launch.
 struct RelabelArgs {
   const double* msg; double count; const float* phi_e; int F;
   float* w; float* mmd;
@@ -163,15 +218,23 @@ struct RelabelArgs {
   float* emean; float escale; uint32_t* counter;
 };
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) uint32_t gu32c;
-
-template <bool CLAMP>
+template <bool CLAMP, int NC>
 __global__ __launch_bounds__(256) void k_mmd_relabel(RelabelArgs a) {
+  constexpr int R = relabel_rows<NC>();
   extern __shared__ __attribute__((aligned(16))) float wsh[];  // [F]
   __shared__ double red[256];
   __shared__ int last;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool roll = (int)blockIdx.x < a.nr;
+  // this wave's first rows, in flight during the prologue
+  const int eb = blockIdx.x - a.nr;
+  const int r0 = roll ? (blockIdx.x * 4 + wave) * R : eb * 4 + wave;
+  const int step = roll ? 1 : a.ne * 4;
+  const float* base = roll ? a.phi : a.erows;
+  const int ld = roll ? a.ldphi : a.lde;
+  const int nrows = roll ? a.n : a.ne_rows;
+  float4 p[R][NC > 0 ? NC : 1];
+  rows_load<NC, R>(base, ld, r0, step, nrows, lane, p);
   double count = a.count == 0.0 ? a.msg[a.F] : a.count;
   double acc = 0.0;
   for (int f = t; f < a.F; f += 256) {
@@ -187,43 +250,60 @@ __global__ __launch_bounds__(256) void k_mmd_relabel(RelabelArgs a) {
   }
   __syncthreads();
   if (blockIdx.x == 0 && t == 0) *a.mmd = (float)(red[0] + red[1] + red[2] + red[3]);
-  if ((int)blockIdx.x < a.nr) {  // rollout rows
-    const int r = blockIdx.x * 4 + wave;
-    if (r >= a.n) return;
-    const double dot = row_dot(a.phi + (long long)r * a.ldphi, wsh, a.F, lane);
+  if (roll) {  // rollout rows r0 .. r0 + R - 1
+    double d[R];
+    rows_dot<NC, R>(p, base, ld, r0, 1, nrows, wsh, a.F, lane, d);
     if (lane != 0) return;
-    float v, bonus;
-    if constexpr (CLAMP) {
-      v = clampf_ref((float)dot, a.c_min, a.c_max);            // linear_cost.py:102
-      float dh = a.disc[r] / a.thr;                            // :132
-      if (dh > 1.0f) dh = 1.0f;                                // :134
-      bonus = dh * a.c_min;                                    // :136
-    } else {
-      v = (float)dot;                                          // :103
-      bonus = a.disc[r];                                       // :139
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int r = r0 + i;
+      if (r >= a.n) break;
+      float v, bonus;
+      if constexpr (CLAMP) {
+        v = clampf_ref((float)d[i], a.c_min, a.c_max);           // linear_cost.py:102
+        float dh = a.disc[r] / a.thr;                            // :132
+        if (dh > 1.0f) dh = 1.0f;                                // :134
+        bonus = dh * a.c_min;                                    // :136
+      } else {
+        v = (float)d[i];                                         // :103
+        bonus = a.disc[r];                                       // :139
+      }
+      const float ipm = a.one_m_lambda * v;                      // :141
+      const float wbv = a.lambda_b * bonus;                      // :144
+      const float cost = ipm - wbv;                              // :147
+      a.reward[r] = -1.0f * cost;                                // batch_reinforce.py:144
+      if (a.ipm) a.ipm[r] = ipm;
+      if (a.wb) a.wb[r] = wbv;
     }
-    const float ipm = a.one_m_lambda * v;                      // :141
-    const float wbv = a.lambda_b * bonus;                      // :144
-    const float cost = ipm - wbv;                              // :147
-    a.reward[r] = -1.0f * cost;                                // batch_reinforce.py:144
-    if (a.ipm) a.ipm[r] = ipm;
-    if (a.wb) a.wb[r] = wbv;
     return;
   }
   if (a.ne == 0) return;
-  // expert rows: sum clamp(phi_E[r].w) (linear_cost.py:105-109)
-  const int b = blockIdx.x - a.nr;
+  // expert rows: sum clamp(phi_E[r].w) (linear_cost.py:105-109), rows in k_expert_cost's order;
+  // two row batches in flight (the next batch's loads are issued before the current one's dots)
   double e = 0.0;
-  for (int r = b * 4 + wave; r < a.ne_rows; r += a.ne * 4) {
-    const double dot = row_dot(a.erows + (long long)r * a.lde, wsh, a.F, lane);
-    e += (double)clampf_ref((float)dot, a.c_min, a.c_max);
+  float4 p2[R][NC > 0 ? NC : 1];
+  auto consume = [&](const float4 (&pp)[R][NC > 0 ? NC : 1], int rb) {
+    double d[R];
+    rows_dot<NC, R>(pp, base, ld, rb, step, nrows, wsh, a.F, lane, d);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if (rb + i * step < a.ne_rows) e += (double)clampf_ref((float)d[i], a.c_min, a.c_max);
+  };
+  for (int rb = r0; rb < a.ne_rows;) {
+    const int rn = rb + R * step;
+    if (rn < a.ne_rows) rows_load<NC, R>(base, ld, rn, step, nrows, lane, p2);
+    consume(p, rb);
+    if (rn >= a.ne_rows) break;
+    rb = rn + R * step;
+    if (rb < a.ne_rows) rows_load<NC, R>(base, ld, rb, step, nrows, lane, p);
+    consume(p2, rn);
   }
   __syncthreads();  // red[] reuse
   if (lane == 0) red[wave] = e;
   __syncthreads();
   if (t == 0) {
     const double part = red[0] + red[1] + red[2] + red[3];
-    __hip_atomic_store((gu64*)(a.eout + 1 + b), __double_as_longlong(part), __ATOMIC_RELAXED,
+    __hip_atomic_store((gu64*)(a.eout + 1 + eb), __double_as_longlong(part), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     last = __hip_atomic_fetch_add((gu32c*)a.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -466,16 +546,28 @@ extern "C" int amx_mmd_relabel(amx_ctx* ctx, const double* msg, double count, co
   a.msg = msg; a.count = count; a.phi_e = phi_e; a.F = F; a.w = w; a.mmd = mmd;
   a.phi = phi; a.ldphi = ldphi; a.disc = disc; a.thr = thr;
   a.one_m_lambda = (float)(1.0 - lambda_b); a.lambda_b = (float)lambda_b; a.c_min = c_min; a.c_max = c_max;
-  a.reward = reward; a.ipm = ipm; a.wb = wbonus; a.n = n; a.nr = (n + 3) / 4;
+  a.reward = reward; a.ipm = ipm; a.wb = wbonus; a.n = n;
   a.erows = expert_rows; a.lde = ld_e; a.ne_rows = expert_rows ? n_e : 0;
   a.ne = expert_rows ? ((n_e + 3) / 4 < 1024 ? (n_e + 3) / 4 : 1024) : 0;
   a.eout = expert_out; a.emean = expert_mean; a.escale = (float)(1.0 - lambda_b); a.counter = counter;
-  const int blocks = (a.nr + a.ne) > 0 ? a.nr + a.ne : 1;
   const size_t lds = (size_t)F * sizeof(float);
-  if (clamp)
-    hipLaunchKernelGGL(k_mmd_relabel<true>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(k_mmd_relabel<false>, dim3(blocks), dim3(256), lds, (hipStream_t)stream, a);
+  hipStream_t st = (hipStream_t)stream;
+  // NC = F/256 chunks per lane for F <= 1024 (R rows per round trip), else the generic path
+  const int nc = F <= 1024 ? F / 256 : 0;
+#define AMX_RELABEL_CASE(NC)                                                                              \
+  case NC: {                                                                                              \
+    constexpr int R = relabel_rows<NC>();                                                                 \
+    a.nr = (n + 4 * R - 1) / (4 * R);                                                                     \
+    const int blocks = (a.nr + a.ne) > 0 ? a.nr + a.ne : 1;                                               \
+    if (clamp) hipLaunchKernelGGL((k_mmd_relabel<true, NC>), dim3(blocks), dim3(256), lds, st, a);        \
+    else hipLaunchKernelGGL((k_mmd_relabel<false, NC>), dim3(blocks), dim3(256), lds, st, a);             \
+    break;                                                                                                \
+  }
+  switch (nc) {
+    AMX_RELABEL_CASE(0) AMX_RELABEL_CASE(1) AMX_RELABEL_CASE(2) AMX_RELABEL_CASE(3) AMX_RELABEL_CASE(4)
+    default: break;
+  }
+#undef AMX_RELABEL_CASE
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

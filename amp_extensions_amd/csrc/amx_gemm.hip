@@ -707,7 +707,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
 __device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t nwg = (uint32_t)(a.tiles_m * a.tiles_n * a.groups * (a.ksplit > 1 ? a.ksplit : 1));
+    const uint32_t nwg = gridDim.x;
     if (atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 1), 1ull) == nwg - 1) {
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 2), (unsigned long long)(now - a.timer[0]));
@@ -719,18 +719,20 @@ __device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
 
 typedef __attribute__((address_space(1))) uint32_t gu32s;
 
-// Split-K combine (the output layer at lane counts whose tiles fill the chip only with K split
-// over ksplit workgroups): every slice stores its raw (scaled) accumulators write-through (sc1,
-// 16-B per lane), drains, and adds to the tile's arrival counter (agent scope); the last arriver
-// acquires, sums the slices in slice order -- P0 + P1 + ... whatever the arrival order, so the
-// result is deterministic -- resets the counter and returns true to run the epilogue
-// (cdna_hip_programming.md §5, in-launch split-K: one release and one acquire per tile).
+// Stream-K combine (the output layer at lane counts whose 128 x 224 tiles are fewer than the
+// CUs: the tiles' K-tiles are dealt out evenly over one workgroup per CU, so a tile's K range is
+// covered by nseg <= 3 consecutive workgroups): every segment stores its raw (scaled)
+// accumulators write-through (sc1, 16-B per lane) in its slot, drains, and adds to the tile's
+// arrival counter (agent scope); the last arriver acquires, sums the segments in K order --
+// P0 + P1 + ... whatever the arrival order, so the result is deterministic -- resets the
+// counter and returns true to run the epilogue (cdna_hip_programming.md §5, in-launch split-K:
+// one release and one acquire per tile).
 template <class TL>
-__device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL::MB][TL::NB], int tile, int ks,
-                                              int* flag) {
+__device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL::MB][TL::NB], int tile, int seg,
+                                              int nseg, int* flag) {
   constexpr int MB = TL::MB, NB = TL::NB, NT = TL::NT;
   const int t = threadIdx.x;
-  const long long per_slice = (long long)MB * NB * NT;  // f32x4 per slice
+  const long long per_slice = (long long)MB * NB * NT;  // f32x4 per slot
   f32x4* base = reinterpret_cast<f32x4*>(a.split_scratch) + (long long)tile * a.ksplit * per_slice;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
@@ -739,13 +741,13 @@ __device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL
 #pragma unroll
     for (int n = 0; n < NB; ++n)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m][n]), rs,
-                                             (int)(((ks * MB + m) * NB + n) * NT + t) * 16, 0, 16 /* sc1 */);
+                                             (int)(((seg * MB + m) * NB + n) * NT + t) * 16, 0, 16 /* sc1 */);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t == 0) {
     const uint32_t old = __hip_atomic_fetch_add((gu32s*)(a.split_cnt + tile), 1u, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (uint32_t)(a.ksplit - 1);
+    const int last = old == (uint32_t)(nseg - 1);
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -760,33 +762,31 @@ __device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL
   for (int m = 0; m < MB; ++m)
 #pragma unroll
     for (int n = 0; n < NB; ++n) mine[m][n] = acc[m][n];
-  for (int s = 0; s < a.ksplit; ++s) {
+  for (int s = 0; s < nseg; ++s) {
 #pragma unroll
     for (int m = 0; m < MB; ++m)
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
-        const f32x4 v = s == ks ? mine[m][n]
-                                : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
+        const f32x4 v = s == seg ? mine[m][n]
+                                 : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
         acc[m][n] = s == 0 ? v : acc[m][n] + v;
       }
   }
   return true;
 }
 
+// One output tile (logical id `tile`, see map_tile; or, stream-K, the K-tiles [kb, ke) of it:
+// segment seg of nseg) of the f16x3 GEMM; the caller runs the timer hooks.
 template <int EPI, class TL>
-__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
+__device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int ke, int seg, int nseg) {
   constexpr int BM = TL::BM, TM = TL::TM, TN = TL::TN, VA = TL::VA, VW = TL::VW, LD = TL::LD;
   constexpr int NT = TL::NT, STAGE = TL::STAGE;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  if (a.timer_role == 1 && blockIdx.x == 0 && threadIdx.x == 0) a.timer[0] = __builtin_amdgcn_s_memrealtime();
   uint16_t* const sm = reinterpret_cast<uint16_t*>(smem);
   int* sExp = reinterpret_cast<int*>(sm + TL::SEXP);
   int g, tm, tn;
-  const int n_tiles = a.tiles_m * a.tiles_n * a.groups;
-  const int ks = a.ksplit > 1 ? (int)blockIdx.x / n_tiles : 0;  // K slice of a split tile
-  const int tile = a.ksplit > 1 ? (int)blockIdx.x - ks * n_tiles : (int)blockIdx.x;
-  map_tile(a, tile, g, tm, tn);
+  tile_coords(a, tile, g, tm, tn);
   const float* __restrict__ Ag = a.A + (long long)g * a.strideA + (long long)tm * BM * a.lda;
   const float* __restrict__ Ag0 = a.A + (long long)tm * BM * a.lda;  // group 0: the shared K slice
   const long long ldw2 = 2LL * a.K;
@@ -844,7 +844,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     w_dst[j] = BM * LD + r * LD + p * 8;
   }
 
-  f32x4 ra[VA];
+  f32x4 ra[TL::DEEPA ? 2 : 1][VA];  // A stage registers (DEEPA: the sets of tiles t+1 and t+2)
   u32x4 rw[VW];
   constexpr int MB = TL::MB, NB = TL::NB;  // 16x16 blocks of the M16 form
   using AccT = std::conditional_t<TL::M16, f32x4[MB][NB], f32x16[TM][TN]>;
@@ -864,21 +864,28 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   }
 
   const int nk = a.K / BK;
-  auto load = [&](int kt) {
+  auto load_a = [&](auto set, int kt) {
     kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
     const float* Ab = kt < nks ? Ag0 : Ag;
 #pragma unroll
     for (int j = 0; j < VA; ++j)
-      if (a_ok[j]) ra[j] = *reinterpret_cast<const f32x4*>(Ab + a_src[j] + kt * BK);
+      if (a_ok[j]) ra[decltype(set)::value][j] = *reinterpret_cast<const f32x4*>(Ab + a_src[j] + kt * BK);
+  };
+  auto load_w = [&](int kt) {
+    kt = kt < nk ? kt : nk - 1;
 #pragma unroll
     for (int j = 0; j < VW; ++j)
       if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
   };
-  auto publish = [&](int base) {
+  auto load = [&](int kt) {
+    load_a(std::integral_constant<int, 0>{}, kt);
+    load_w(kt);
+  };
+  auto publish = [&](int base) {  // A from set 0
 #pragma unroll
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) {
-        f32x4 x = ra[j];
+        f32x4 x = ra[0][j];
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
         u32x2 l0, l1;
@@ -891,20 +898,23 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
   };
   // one staging piece (SPLIT): publish A/W chunk j of the registered tile, then reload chunk j
-  // of tile kt (clamped as load())
-  auto piece = [&](int q, int base, int kt) {
+  // of tile kt (clamped as load()); DEEPA: A chunk j of register set `set`, reloaded with tile
+  // kt + 1 (two tiles ahead of the W operand's one)
+  auto piece = [&](int q, int base, int kt, auto set) {
+    constexpr int SA = decltype(set)::value;
+    const int kta = TL::DEEPA ? (kt + 1 < nk ? kt + 1 : nk - 1) : (kt < nk ? kt : nk - 1);
     kt = kt < nk ? kt : nk - 1;
     if (q < VA) {
       const int j = q;
       if (a_ok[j]) {
-        f32x4 x = ra[j];
+        f32x4 x = ra[SA][j];
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
         u32x2 l0, l1;
         split2(x, l0, l1);
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
-        ra[j] = *reinterpret_cast<const f32x4*>((kt < nks ? Ag0 : Ag) + a_src[j] + kt * BK);
+        ra[SA][j] = *reinterpret_cast<const f32x4*>((kta < nks ? Ag0 : Ag) + a_src[j] + kta * BK);
       }
     } else if (q < VA + VW) {
       const int j = q - VA;
@@ -936,7 +946,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     }
   };
   int split_base = 0, split_kt = 0;  // SPLIT: where compute16's pieces publish / what they load
-  auto compute16 = [&](int base) {
+  auto compute16 = [&](int base, auto set) {  // set: the A register set its pieces publish (DEEPA)
     if constexpr (TL::M16) {
     const uint16_t* As = sm + base + a_off16;
     if constexpr (!TL::EARLY) frag0(base);
@@ -958,10 +968,10 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga[m & 1][PA[p]], gb[n][PB[p]], acc[m][n], 0, 0, 0);
       if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
       if constexpr (TL::SPLIT) {
-        piece(m, split_base, split_kt);
+        piece(m, split_base, split_kt, set);
         if (m == MB - 1) {
 #pragma unroll
-          for (int q = MB; q < VA + VW; ++q) piece(q, split_base, split_kt);
+          for (int q = MB; q < VA + VW; ++q) piece(q, split_base, split_kt, set);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -970,7 +980,7 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   };
   auto compute = [&](int base) {
     if constexpr (TL::M16) {
-      compute16(base);
+      compute16(base, std::integral_constant<int, 0>{});
       return;
     } else {
     const uint16_t* As = sm + base + a_off;
@@ -1030,10 +1040,37 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       epilogue_h3<EPI, TL>(a, ac, sExp, g, tm, tn);
     }
   };
+  if constexpr (TL::DEEPA) {
+    // K-tiles [kb, ke); tile x's A in register set (x - kb) & 1, loaded two tiles ahead
+    load(kb);
+    publish(0);
+    load_a(std::integral_constant<int, 1>{}, kb + 1);
+    load_w(kb + 1);
+    load_a(std::integral_constant<int, 0>{}, kb + 2);
+    auto kstep = [&](int kt, auto par) {  // buffer par; pieces publish tile kt+1 from set par^1
+      constexpr int P = decltype(par)::value;
+      __syncthreads();  // tile kt visible in buffer P; buffer P^1 (tile kt-1) fully read
+      frag0(P * STAGE);
+      __builtin_amdgcn_sched_barrier(0);
+      split_base = (P ^ 1) * STAGE;
+      split_kt = kt + 2;
+      compute16(P * STAGE, std::integral_constant<int, P ^ 1>{});
+    };
+    for (int kt = kb; kt < ke; kt += 2) {
+      kstep(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < ke) kstep(kt + 1, std::integral_constant<int, 1>{});
+    }
+    if constexpr (EPI == EPI_UNNORM) {
+      if (nseg > 1) {
+        __syncthreads();  // the stage buffers are free: one int of LDS for the last-arriver flag
+        if (!split_combine<TL>(a, acc, tile, seg, nseg, reinterpret_cast<int*>(smem) + BM + 4)) return;
+      }
+    }
+    finish(acc);
+    return;
+  }
   if constexpr (TL::LATE) {
     // K-tiles [kb, ke) of this workgroup (all of them unless the tile is split)
-    const int kb = a.ksplit > 1 ? (ks * nk) / a.ksplit : 0;
-    const int ke = a.ksplit > 1 ? ((ks + 1) * nk) / a.ksplit : nk;
     load(kb);
     publish(0);
     load(kb + 1);
@@ -1056,16 +1093,12 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
       compute(cur * STAGE);
     }
     if constexpr (TL::M16 && EPI == EPI_UNNORM) {
-      if (a.ksplit > 1) {
+      if (nseg > 1) {
         __syncthreads();  // the stage buffers are free: one int of LDS for the last-arriver flag
-        if (!split_combine<TL>(a, acc, tile, ks, reinterpret_cast<int*>(smem) + BM + 4)) {
-          if (a.timer_role == 2) gemm_timer_end(a);
-          return;
-        }
+        if (!split_combine<TL>(a, acc, tile, seg, nseg, reinterpret_cast<int*>(smem) + BM + 4)) return;
       }
     }
     finish(acc);
-    if (a.timer_role == 2) gemm_timer_end(a);
     return;
   }
   load(0);
@@ -1080,6 +1113,35 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
     __syncthreads();
   }
   finish(acc);
+}
+
+// a.streamk (LATE M16 UNNORM tiles): one workgroup per CU; the workgroups of one XCD take
+// consecutive virtual ids v (xcd_logical) and v runs the K-tiles [v U / G, (v + 1) U / G) of
+// the U = tiles x nk units in logical tile order (tile_n fastest, then tile_m: an XCD's
+// workgroups share A row panels and one member's weight panels in its L2) -- one, two or three
+// segments of consecutive tiles -- and the tiles' segments are combined in K order
+// (split_combine).  Otherwise one tile per workgroup (map_tile's XCD-contiguous order).
+template <int EPI, class TL>
+__global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
+  if (a.timer_role == 1 && blockIdx.x == 0 && threadIdx.x == 0) a.timer[0] = __builtin_amdgcn_s_memrealtime();
+  const int nk = a.K / TL::BK;
+  if (a.streamk) {
+    const long long U = (long long)a.tiles_m * a.tiles_n * a.groups * nk, G = gridDim.x;
+    const int v = xcd_logical((int)G, (int)blockIdx.x);
+    long long u = (long long)v * U / G;
+    const long long uend = ((long long)v + 1) * U / G;
+    while (u < uend) {
+      const int tile = (int)(u / nk), kb = (int)(u - (long long)tile * nk);
+      const int ke = (uend - u) < (long long)(nk - kb) ? kb + (int)(uend - u) : nk;
+      const long long u0 = (long long)tile * nk;
+      const int wf = (int)(((u0 + 1) * G - 1) / U), wl = (int)(((u0 + nk) * G - 1) / U);  // its workgroups
+      h3_tile<EPI, TL>(a, tile, kb, ke, v - wf, wl - wf + 1);
+      u += ke - kb;
+      __syncthreads();  // LDS reuse by the next segment
+    }
+  } else {
+    h3_tile<EPI, TL>(a, xcd_logical(a.tiles_m * a.tiles_n * a.groups, (int)blockIdx.x), 0, nk, 0, 1);
+  }
   if (a.timer_role == 2) gemm_timer_end(a);
 }
 
@@ -1160,7 +1222,8 @@ template <int MB> using HRow = TileH3<2, 4, 1, 1, 2, 2, true, true, true, MB, 4,
 template <int RW, int NBO> using HOut = TileH3<RW, 1, 1, 1, 2, 2, true, true, true, 2, NBO, true, true, true>;
 using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;
 using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
-using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true>;
+using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true, true>;  // + DEEPA (-2 %)
+
 using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
 using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 
@@ -1207,8 +1270,9 @@ template <int EPI, class TL>
 int launch_h3(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
   a.tiles_n = a.N / TL::BN;
-  const int nwg = a.tiles_m * a.tiles_n * a.groups * (a.ksplit > 1 ? a.ksplit : 1);
-  if (nwg == 0) return AMX_OK;
+  const int tiles = a.tiles_m * a.tiles_n * a.groups;
+  const int nwg = a.streamk ? a.streamk : tiles;  // stream-K: a.streamk workgroups
+  if (tiles == 0) return AMX_OK;
   constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
@@ -1500,6 +1564,16 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   return launch_h3<EPI_BIAS_ACT, H128>(a, s);
 }
 
+// Output-layer tiles (128 x 224, S <= 224) of a stream-K launch for `rows` padded lanes x
+// `groups` members, 0 when the shape does not use it: fewer tiles than CUs but at least half
+// as many (so a tile's K range spans at most 3 of the evenly dealt workgroup ranges).
+static int streamk_tiles(const amx_ctx* ctx, int groups, int rows) {
+  const int n32 = amx::round_up(ctx->S, 32);
+  if (n32 <= 128 || n32 > 224 || rows % 128 != 0) return 0;
+  const int tiles = rows / 128 * groups;
+  return (tiles < ctx->n_cus && 2 * tiles >= ctx->n_cus) ? tiles : 0;
+}
+
 extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
                                       int lda, long long strideA, const uint16_t* W2, long long strideW2,
                                       const int* w_exp, long long strideWexp, const float* bias, long long strideBias,
@@ -1534,14 +1608,13 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
-    // lane counts whose 128 x 224 tiles fill less than one wave of CUs and whose row-block
-    // tiles would run an odd number of waves per workgroup (5120 lanes: 160-row blocks, 5 waves
-    // on 4 SIMDs): split K three ways over 128 x 224 tiles (14 waves) -> two balanced rounds
-    const int tiles = rows / 128 * groups, ksplit = 3;
-    if (rows % 128 == 0 && rb == 160 && tiles * ksplit <= 2 * ctx->n_cus && (K / 32) % ksplit == 0 &&
-        ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
-        ctx->split_floats >= (long long)tiles * ksplit * 128 * 224) {
-      a.ksplit = ksplit; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+    // lane counts whose 128 x 224 tiles (14 waves) are fewer than the CUs (4096-7168 lanes x 4
+    // members: 128-224 tiles): stream-K over one workgroup per CU (each tile's K range in <= 3
+    // segments), instead of the row-block tiles' 4-7 waves per workgroup
+    const int tiles = streamk_tiles(ctx, groups, rows);
+    if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
+        ctx->split_floats >= (long long)tiles * 3 * 128 * 224) {
+      a.ksplit = 3; a.streamk = ctx->n_cus; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
       return launch_h3<EPI_UNNORM, H128x224>(a, s);
     }
     if (row_tiles) {
@@ -1612,10 +1685,7 @@ extern "C" int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long f
 
 extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters) {
   if (!ctx || groups < 1 || rows <= 0) return -1;
-  const int nrb = (ctx->n_cus % (2 * groups) == 0) ? ctx->n_cus / (2 * groups) : 0;
-  const int rb = (nrb > 0 && rows % nrb == 0) ? rows / nrb : 0;
-  const int tiles = rows % 128 == 0 ? rows / 128 * groups : 0;
-  const bool split = rb == 160 && tiles > 0 && tiles * 3 <= 2 * ctx->n_cus && amx::round_up(ctx->S, 32) <= 224;
-  if (n_counters) *n_counters = split ? tiles : 0;
-  return split ? (long long)tiles * 3 * 128 * 224 : 0;
+  const int tiles = streamk_tiles(ctx, groups, rows);
+  if (n_counters) *n_counters = tiles;
+  return (long long)tiles * 3 * 128 * 224;
 }

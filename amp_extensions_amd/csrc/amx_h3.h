@@ -40,8 +40,9 @@ struct GemmArgs {
   int* row_exp_out;        // nullable: slot receiving the exponents of this launch's output rows
   int k_shared;            // leading K columns of A read from group 0's rows for every group
                            //   (the ensemble's x0 slice, assembled once; multiple of the tile's BK)
-  int ksplit;              // > 1: K split over this many workgroups per tile (output layer, M16 tiles)
-  float* split_scratch;    //   raw partial tiles [tile][slice][MB][NB][NT] f32x4 (amx_set_split_workspace)
+  int ksplit;              // partial-tile slots per tile in split_scratch (stream-K output layer)
+  int streamk;             // > 0: stream-K over this many workgroups (LATE M16 UNNORM tiles)
+  float* split_scratch;    //   raw partial tiles [tile][slot][MB][NB][NT] f32x4 (amx_set_split_workspace)
   uint32_t* split_cnt;     //   arrivals per tile (zero between launches: the last arriver resets it)
   uint64_t* timer;         // amx_set_gemm_timer buffer (null: off)
   int timer_role;          //   1: first layer of a forward (block 0 stamps the start), 2: output layer
@@ -52,16 +53,22 @@ struct GemmArgs {
 // run of logical tiles (tile_n fastest: consecutive tiles reuse the same A row panel;
 // then tile_m: they reuse the same weight panels of one ensemble member).  Bijective for
 // any tile count (cdna_hip_programming.md T1).
-__device__ inline void map_tile(const GemmArgs& a, int orig, int& g, int& tm, int& tn) {
-  const int nwg = a.tiles_m * a.tiles_n * a.groups;
+__device__ inline int xcd_logical(int nwg, int orig) {
   const int xcd = orig & 7;
   const int q = nwg >> 3, r = nwg & 7;
   const int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  const int logical = base + (orig >> 3);
+  return base + (orig >> 3);
+}
+
+__device__ inline void tile_coords(const GemmArgs& a, int logical, int& g, int& tm, int& tn) {
   tn = logical % a.tiles_n;
   const int rest = logical / a.tiles_n;
   tm = rest % a.tiles_m;
   g = rest / a.tiles_m;
+}
+
+__device__ inline void map_tile(const GemmArgs& a, int orig, int& g, int& tm, int& tn) {
+  tile_coords(a, xcd_logical(a.tiles_m * a.tiles_n * a.groups, orig), g, tm, tn);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -105,12 +112,16 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // distinct 4-bank slots)
 template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
           bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false, bool EARLY_ = false,
-          bool SPLIT_ = false>
+          bool SPLIT_ = false, bool DEEPA_ = false>
 struct TileH3 {
   static constexpr bool EARLY = EARLY_ && M16_ && LATE_;  // first fragment reads before the publish
   // SPLIT: the publish of tile t+1 and the loads of t+2 are cut into one piece per m-block and
   // placed behind that block's MFMAs (the guide's split write-after-barrier schedule)
   static constexpr bool SPLIT = SPLIT_ && EARLY;
+  // DEEPA (SPLIT): the A operand's loads run two K-tiles ahead of its publish instead of one (two
+  // register sets; the loop unrolled by two): the output layer's A panel is streamed from HBM
+  // once (N = 224 columns per A row), so its K loop waits on load latency, not on the MFMAs
+  static constexpr bool DEEPA = DEEPA_ && SPLIT;
   // PIN: sched_barriers keep each block's fragment reads one MFMA group ahead of their use
   static constexpr bool PIN = PIN_;
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;

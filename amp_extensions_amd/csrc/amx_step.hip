@@ -156,6 +156,8 @@ struct StepArgs {
   double* ob_out; const double* table; int R; const int32_t* rows; uint32_t k0, k1;
   int32_t* reset_count; int32_t* row_out;
   int32_t* steps0_out;  // nullable: num_steps before this step (a rollout's first slot)
+  uint64_t* counter; long long counter_delta;  // nullable: *counter += delta (graph replays' policy counter)
+  double* ob_rec;  // nullable: a copy of ob (a rollout's slot 0 when the carried state is read in place)
 };
 
 // NIT = ceil(S/64) state elements per lane, kept in registers: all loads of the row are
@@ -212,6 +214,7 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
     x[it] = v;
     if (j < S) {
       on[j] = v;
+      if (a.ob_rec) a.ob_rec[(long long)b * S + j] = o[it];
       if (T.vel_check && j >= T.vel_offset) vel_bad |= fabs(v) > T.vel_thresh;
       bad |= !isfinite(v);
       if (a.cost_in) {
@@ -332,6 +335,7 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
     }
   }
 
+  if (a.counter && b == 0 && lane == 0) a.counter[0] += (uint64_t)a.counter_delta;  // amx_counter_add
   if (lane == 0) {
     if (a.steps0_out) a.steps0_out[b] = ns - 1;
     a.num_steps[b] = reset ? 0 : ns;  // a reset restarts the episode counter (:277)
@@ -755,6 +759,7 @@ extern "C" int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void*
 struct ResetArgs {  // amx_step_reset's reset half (amx_reset_lanes' arguments)
   const double* table; int R; const int32_t* rows; uint64_t seed; double* ob_out; int32_t* model_idx;
   int32_t* reset_count; int32_t* row_out; int32_t* steps0_out;
+  uint64_t* counter; long long counter_delta; double* ob_rec;
 };
 
 static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
@@ -775,15 +780,19 @@ static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long stride
   a.cost_in = cost_in; a.ldc = ldc; a.cost_rexp = cost_rexp; a.nonfinite = nonfinite;
   a.S = ctx->S; a.M = ctx->M; a.B = B; a.term = ctx->term;
   a.model_idx_out = nullptr; a.ob_out = nullptr; a.table = nullptr; a.R = 0; a.rows = nullptr; a.k0 = a.k1 = 0;
-  a.reset_count = nullptr; a.row_out = nullptr; a.steps0_out = nullptr;
+  a.reset_count = nullptr; a.row_out = nullptr; a.steps0_out = nullptr; a.counter = nullptr; a.counter_delta = 0;
+  a.ob_rec = nullptr;
   if (rs) {
     AMX_CHECK_ARG(rs->table && rs->ob_out && rs->model_idx && rs->reset_count && rs->R > 0,
                   "amx_step_reset: null reset pointer or R=%d", rs->R);
-    AMX_CHECK_ARG(rs->ob_out != ob && rs->ob_out != ob_next && (const int32_t*)rs->model_idx == model_idx,
-                  "amx_step_reset: ob_out must be a third buffer and model_idx the step's");
+    AMX_CHECK_ARG(rs->ob_out != ob_next && (const int32_t*)rs->model_idx == model_idx,
+                  "amx_step_reset: ob_out must differ from ob_next and model_idx be the step's");
+    AMX_CHECK_ARG(rs->ob_rec == nullptr || (rs->ob_rec != ob && rs->ob_rec != ob_next && rs->ob_rec != rs->ob_out),
+                  "amx_step_reset: ob_rec must be a fourth buffer");
     a.model_idx_out = rs->model_idx; a.ob_out = rs->ob_out; a.table = rs->table; a.R = rs->R; a.rows = rs->rows;
     a.k0 = (uint32_t)rs->seed; a.k1 = (uint32_t)(rs->seed >> 32);
     a.reset_count = rs->reset_count; a.row_out = rs->row_out; a.steps0_out = rs->steps0_out;
+    a.counter = rs->counter; a.counter_delta = rs->counter_delta; a.ob_rec = rs->ob_rec;
   }
   const int nit = (ctx->S + 63) / 64;
   switch (nit) {
@@ -820,9 +829,11 @@ extern "C" int amx_step_reset(amx_ctx* ctx, const float* preds, int ldp, long lo
                               const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
                               float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, const double* table,
                               int R, const int32_t* rows, uint64_t seed, double* ob_out, int32_t* reset_count,
-                              int32_t* row_out, int32_t* steps0_out, int B, void* stream) {
+                              int32_t* row_out, int32_t* steps0_out, uint64_t* counter, long long counter_delta,
+                              double* ob_rec, int B, void* stream) {
   AMX_CHECK_ARG(!cost_rexp || cost_in, "amx_step_reset: cost_rexp needs cost_in");
-  const ResetArgs rs = {table, R, rows, seed, ob_out, model_idx, reset_count, row_out, steps0_out};
+  const ResetArgs rs = {table, R, rows, seed, ob_out, model_idx, reset_count, row_out, steps0_out, counter,
+                        counter_delta, ob_rec};
   return step_impl(ctx, preds, ldp, strideP, model_idx, ob, ob_next, num_steps, done, disc, cost_in, ldc, cost_rexp,
                    nonfinite, B, stream, &rs);
 }

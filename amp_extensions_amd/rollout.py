@@ -123,6 +123,9 @@ class RolloutEngine:
         # advances dev_step by T at its end, so every replay draws fresh noise
         self.dev_step = torch.zeros(1, dtype=torch.int64, device=dev)
         self._capturing = False
+        self._ctr_delta = 0      # graph capture: steps of the captured rollout (counter advance)
+        self._ctr_folded = False  # the last captured step kernel advanced the counter
+        self._carry = 0           # rollout(): slot holding the carried lane states (0: in slot 0)
         self._graph_ahead = False  # replays advanced dev_step past the host counter
         # [sum phi (F) | count] of the rollout: the one buffer the cross-rank all-reduce touches
         self._fbuf = z(cost.feature_dim + 1, dt=torch.float64) if isinstance(cost, RBFLinearCost) else None
@@ -182,7 +185,11 @@ class RolloutEngine:
         fused = self.auto_reset and self.motion is None and self.fuse_reset
         if t == 0 and not fused:  # (the fused step kernel records it itself: steps0_out)
             self.steps0.copy_(self.num_steps)
-        ob, ob_next, act = self.obs[t], self.next_obs[t], self.acts[t]
+        # rollout(): step 0 reads the carried lane states where the last rollout left them and
+        # the step kernel records them in slot 0 (ob_rec), instead of a separate carry copy
+        src = self._carry if (t == 0 and self._carry) else t
+        self._carry = 0
+        ob, ob_next, act = self.obs[src], self.next_obs[t], self.acts[t]
         x0_ready = False
         if actions is not None:
             act.copy_(actions)
@@ -205,6 +212,10 @@ class RolloutEngine:
         preds = self.ens.forward_preds(ob, act, B, x0_ready=x0_ready)
         if fused:  # step + table reset in one pass (amx_step_reset)
             ss = self.cost_type == "ss"
+            # a captured rollout's last step also advances the device policy counter by T
+            # (amx_counter_add folded into the step kernel: one graph node fewer)
+            last = self._capturing and self._ctr_delta and t == self._ctr_delta - 1
+            ctr, ctr_delta = (self.dev_step, self._ctr_delta) if last else (None, 0)
             N.check(c.lib.amx_step_reset(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                          ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
                                          self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
@@ -214,7 +225,10 @@ class RolloutEngine:
                                          None if reset_rows is None else reset_rows.data_ptr(), self.seed,
                                          self.obs[t + 1].data_ptr(), self.reset_count.data_ptr(),
                                          self.reset_rows[t].data_ptr(), self.steps0.data_ptr() if t == 0 else None,
-                                         B, s), "amx_step_reset")
+                                         ctr.data_ptr() if ctr is not None else None, ctr_delta,
+                                         self.obs[0].data_ptr() if src != t else None, B, s),
+                    "amx_step_reset")
+            self._ctr_folded = ctr is not None
         elif self.cost_type == "ss" and self.cost_rexp is not None:
             N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
                                         ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
@@ -269,7 +283,11 @@ class RolloutEngine:
         """K synchronous steps (default: the buffer depth), then the batched reward pass.
         Returns K*B transitions."""
         K = self.K if K is None else K
-        self.begin_rollout()
+        fused = self.auto_reset and self.motion is None and self.fuse_reset
+        if fused and self.t != 0:  # the first step reads the carried states in place (ob_rec)
+            self._carry, self.t, self._scored = self.t, 0, 0
+        else:
+            self.begin_rollout()
         for _ in range(K):
             self.step()
         self.score()
@@ -361,10 +379,12 @@ class RolloutEngine:
         side.wait_stream(torch.cuda.current_stream(c.device))
         with torch.cuda.stream(side):
             self._capturing = True
+            self._ctr_delta, self._ctr_folded = T, False
             try:
                 with torch.cuda.graph(graphs[0], stream=side):
                     self.rollout(T)
-                    N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), T, c.stream), "amx_counter_add")
+                    if not self._ctr_folded:  # (the fused step kernel advances it itself)
+                        N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), T, c.stream), "amx_counter_add")
                     if mmd:
                         self.relabel_pre()
                         if allreduce is None:
@@ -378,6 +398,7 @@ class RolloutEngine:
                             tail()
             finally:
                 self._capturing = False
+                self._ctr_delta = 0
         torch.cuda.current_stream(c.device).wait_stream(side)
         self._graph_ahead = True  # the captured steps did not run: the device counter is the truth
         two = mmd and allreduce is not None

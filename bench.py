@@ -269,23 +269,28 @@ def main():
 
     # HIP graph: the whole rollout (steps, scoring, relabel, expert cost) is captured once and
     # replayed, so per-kernel host launch overhead leaves the timed region (the RCCL all-reduce
-    # of N>1 runs eagerly between two graphs).  ROCm has no timing-event nodes in graphs, so
-    # the ensemble GEMMs time themselves (amx_set_gemm_timer: start stamp in the first layer,
-    # tick sum in the output layer's last workgroup; no extra launches).
+    # of N>1 runs eagerly between two graphs).  The f16x3 ensemble GEMMs time themselves in
+    # both launch modes (amx_set_gemm_timer: start stamp in the first layer, tick sum in the
+    # output layer's last workgroup; no extra launches): ROCm has no timing-event nodes in
+    # graphs, and in eager mode each timing-event record is a queue drain that opened a
+    # 5.6 us gap before the first and after the last GEMM of every step (rocprofv3 trace,
+    # profiles/r02_event_gaps.txt) -- 2 % of the timed region.  The other GEMM paths keep
+    # HIP events.
     graph = None
     use_graph = args.graph == "on" or (args.graph == "auto" and B * T < 16384 and args.gemm == "f16x3")
     if use_graph and args.gemm != "f16x3":
         raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
+    timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
     if use_graph:
         tail = cost.get_expert_cost if args.cost == "mmd" else None
-        timer = ctx.gemm_timer()
         graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail)
         graph()  # warm replay
-        torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    if timer is not None:
         timer.zero_()
 
     # ---- timed region -----------------------------------------------------------------------
-    ens.gemm_events = [] if graph is None else None
+    ens.gemm_events = [] if timer is None else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -310,7 +315,7 @@ def main():
     total_samples = samples * world
 
     # dominant kernel: the ensemble GEMM launches (HIP events on the launch stream)
-    if graph is None:
+    if timer is None:
         gemm_ms = sum(e0.elapsed_time(e1) for (e0, e1, _) in ens.gemm_events)
         n_fwd = len(ens.gemm_events)
     else:
@@ -383,9 +388,10 @@ def main():
                 "kernel": gi["kernel"],
                 "matrix_pipe_tflops": round(gi["products"] * achieved_tflops, 1) if gi["products"] else None,
                 "avg_launch_us": round(gemm_ms * 1e3 / max(launches, 1), 2),
-                "timing": ("HIP events around the GEMM launches" if graph is None else
-                           "in-kernel device realtime (amx_set_gemm_timer, 100 MHz): first hidden layer's start to "
-                           "the output layer's last workgroup, per forward (ROCm has no timing events in graphs)"),
+                "timing": ("HIP events around the GEMM launches" if timer is None else
+                           "in-kernel device realtime (amx_set_gemm_timer, 100 MHz, on the launch stream): first "
+                           "hidden layer's start to the output layer's last workgroup, per forward (event records "
+                           "drain the queue: 5.6 us gaps; no timing events in graphs)"),
                 "flops_per_launch": flops_per_fwd / per_fwd,
             },
             "step_flops_frac": round(value / world * step_flops / (peak * 1e12), 4),

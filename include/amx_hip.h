@@ -283,14 +283,20 @@ int amx_step_rexp(amx_ctx* ctx, const float* preds, int ldp, long long strideP, 
 /* amx_step (cost_rexp nullable: amx_step_rexp) fused with amx_reset_lanes(mask = done,
  * ob_src = ob_next) in one pass: done lanes get reset_count/model_idx/num_steps/row_out
  * and ob_out[b] = table[row] exactly as amx_reset_lanes; the others ob_out[b] = ob_next[b]
- * (from registers, no re-read).  ob_out must differ from ob and ob_next; model_idx is
- * read (the member of this step) and, for reset lanes, rewritten.  steps0_out (nullable):
- * receives num_steps before this step (the trajectory position of a rollout's first slot). */
+ * (from registers, no re-read).  ob_out must differ from ob_next; it may be ob (in place:
+ * every lane reads its row before writing it); model_idx is read (the member of this step)
+ * and, for reset lanes, rewritten.  ob_rec (nullable, a fourth buffer) receives a copy of ob
+ * (a rollout's slot 0 when the carried lane states are read where the last rollout left
+ * them, instead of a separate carry copy).  steps0_out (nullable):
+ * receives num_steps before this step (the trajectory position of a rollout's first slot).
+ * counter (nullable): *counter += counter_delta once per launch (amx_counter_add folded into a
+ * captured rollout's last step; no kernel of this launch reads the counter). */
 int amx_step_reset(amx_ctx* ctx, const float* preds, int ldp, long long strideP, int32_t* model_idx,
                    const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
                    float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, const double* table,
                    int R, const int32_t* rows, uint64_t seed, double* ob_out, int32_t* reset_count,
-                   int32_t* row_out, int32_t* steps0_out, int B, void* stream);
+                   int32_t* row_out, int32_t* steps0_out, uint64_t* counter, long long counter_delta,
+                   double* ob_rec, int B, void* stream);
 
 /* Disagreement only (DynamicsEnsemble.get_action_discrepancy / compute_threshold,
  * milo/milo/dynamics.py:145-165). */
@@ -349,15 +355,15 @@ int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stre
  * is read when a launch is issued (graph capture bakes it in).  null: off. */
 int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf);
 
-/* Split-K workspace of the f16x3 output layer (amx_gemm_out_unnorm_h3): at lane counts whose
- * row-block tiles would leave the output layer with an odd number of waves per workgroup
- * (5120 lanes x 4 members: 160-row blocks), the layer runs as 128 x 224 tiles with K split over
- * three workgroups whose raw partials the last arriver sums in slice order (deterministic).
- * amx_split_workspace_floats: floats of scratch (and *n_counters uint32 counters) a forward of
- * `rows` padded lanes needs, 0 when that shape does not split.  amx_set_split_workspace
- * registers caller-owned device memory with the context (counters zeroed by the caller once;
- * each launch leaves them zero); without it the layer runs unsplit.  One launch at a time per
- * context. */
+/* Split workspace of the f16x3 output layer (amx_gemm_out_unnorm_h3): at lane counts whose
+ * 128 x 224 output tiles are fewer than the CUs but at least half as many (4096-7168 lanes x 4
+ * members), the layer runs stream-K: one workgroup per CU, the tiles' K-tiles dealt out evenly,
+ * each tile's 1-3 K segments stored raw and summed in K order by the last arriver
+ * (deterministic).  amx_split_workspace_floats: floats of scratch (3 partial tiles per tile)
+ * and *n_counters uint32 counters a forward of `rows` padded lanes needs, 0 when that shape
+ * does not use it.  amx_set_split_workspace registers caller-owned device memory with the
+ * context (counters zeroed by the caller once; each launch leaves them zero); without it the
+ * layer runs on row-block tiles.  One launch at a time per context. */
 long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters);
 int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
                             int n_counters);

@@ -332,19 +332,20 @@ def test_gemm_timer_counts_every_forward(B):
     ctx.gemm_timer(False)
 
 
-def test_output_split_k_deterministic_and_close_to_unsplit():
-    """5120 lanes x 4 members: the output layer runs split-K (3 slices of K over 128 x 224 tiles,
-    last arriver sums the raw partials in slice order): repeated forwards give the same bits, the
-    arrival counters are left zero, and the result is within fp32 rounding of the unsplit
-    row-block tiles (amx_set_split_workspace unset)."""
+@pytest.mark.parametrize("B", [4096, 5120, 6144, 7168])
+def test_output_stream_k_deterministic_and_close_to_unsplit(B):
+    """4096-7168 lanes x 4 members (128-224 output tiles of 128 x 224, fewer than the CUs): the
+    output layer runs stream-K (the tiles' K-tiles dealt evenly over one workgroup per CU; each
+    tile's 1-3 segments summed in K order by the last arriver): repeated forwards give the same
+    bits, the arrival counters are left zero, and the result is within fp32 rounding of the
+    unsplit row-block tiles (amx_set_split_workspace unset)."""
     amx, ctx, ens, ens_w, norms, (s, a) = make(197, 36, [512] * 4, gemms=("f16x3",))
     e = ens["f16x3"]
-    B = 5120
     rs = np.random.RandomState(3)
     obd = torch.from_numpy(0.5 * rs.randn(B, 197)).to(DEV)
     acd = torch.from_numpy(rs.randn(B, 36)).to(DEV)
     p1 = e.forward_preds(obd, acd, B).clone()
-    assert getattr(ctx, "_split_ws", None) is not None, "5120 lanes should register the split-K workspace"
+    assert getattr(ctx, "_split_ws", None) is not None, f"{B} lanes should register the stream-K workspace"
     p2 = e.forward_preds(obd, acd, B).clone()
     torch.cuda.synchronize()
     assert torch.equal(p1, p2)
