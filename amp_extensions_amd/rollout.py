@@ -126,6 +126,7 @@ class RolloutEngine:
         self._ctr_delta = 0      # graph capture: steps of the captured rollout (counter advance)
         self._ctr_folded = False  # the last captured step kernel advanced the counter
         self._carry = 0           # rollout(): slot holding the carried lane states (0: in slot 0)
+        self._pending = None      # rollout_overlapped: the previous rollout's relabel, run at the next step 0
         self._graph_ahead = False  # replays advanced dev_step past the host counter
         # [sum phi (F) | count] of the rollout: the one buffer the cross-rank all-reduce touches
         self._fbuf = z(cost.feature_dim + 1, dt=torch.float64) if isinstance(cost, RBFLinearCost) else None
@@ -166,6 +167,15 @@ class RolloutEngine:
                                       c.stream), "amx_reset_lanes")
         self.t = 0
 
+    def _rollout_begin(self) -> None:
+        """rollout()'s start: with the fused step the first step reads the carried lane states
+        where the last rollout left them (ob_rec records them in slot 0), else begin_rollout."""
+        fused = self.auto_reset and self.motion is None and self.fuse_reset
+        if fused and self.t != 0:
+            self._carry, self.t, self._scored = self.t, 0, 0
+        else:
+            self.begin_rollout()
+
     def begin_rollout(self) -> None:
         """Carry the lane states of the previous rollout into slot 0."""
         if self.t != 0:
@@ -177,7 +187,17 @@ class RolloutEngine:
              noise: torch.Tensor | None = None) -> int:
         """One synchronous step of all lanes; returns the slot index t it was recorded in.
         `actions` [B, A] f64 on device replaces the policy; `noise` [B, A] f64 replaces the
-        policy's Philox noise; `reset_rows` [B] i32 forces the rows of lanes that reset."""
+        policy's Philox noise; `reset_rows` [B] i32 forces the rows of lanes that reset.
+        A relabel left pending by rollout_overlapped runs between the first step's ensemble
+        forward and its step kernel (the forward hides the all-reduce it waits for)."""
+        front = self._step_front(actions, noise)
+        if front[0] == 0 and self._pending is not None:
+            pending, self._pending = self._pending, None
+            pending()
+        return self._step_back(front, reset_rows)
+
+    def _step_front(self, actions, noise):
+        """Policy + ensemble forward of step t (everything before the step kernel)."""
         c, t, B = self.ctx, self.t, self.B
         if t >= self.K:
             raise RuntimeError(f"rollout buffer full ({self.K} steps): call begin_rollout()")
@@ -210,6 +230,14 @@ class RolloutEngine:
                             shared_x0=fuse_x0)
             x0_ready = fuse_x0
         preds = self.ens.forward_preds(ob, act, B, x0_ready=x0_ready)
+        return t, src, preds
+
+    def _step_back(self, front, reset_rows) -> int:
+        """Step kernel (fp64 update, termination, disagreement, cost row, reset) of step t."""
+        c, B, s = self.ctx, self.B, self.ctx.stream
+        t, src, preds = front
+        fused = self.auto_reset and self.motion is None and self.fuse_reset
+        ob, ob_next = self.obs[src], self.next_obs[t]
         if fused:  # step + table reset in one pass (amx_step_reset)
             ss = self.cost_type == "ss"
             # a captured rollout's last step also advances the device policy counter by T
@@ -283,11 +311,7 @@ class RolloutEngine:
         """K synchronous steps (default: the buffer depth), then the batched reward pass.
         Returns K*B transitions."""
         K = self.K if K is None else K
-        fused = self.auto_reset and self.motion is None and self.fuse_reset
-        if fused and self.t != 0:  # the first step reads the carried states in place (ob_rec)
-            self._carry, self.t, self._scored = self.t, 0, 0
-        else:
-            self.begin_rollout()
+        self._rollout_begin()
         for _ in range(K):
             self.step()
         self.score()
@@ -349,12 +373,13 @@ class RolloutEngine:
                 "amx_feature_message")
         return self._fbuf
 
-    def relabel_post(self) -> dict:
+    def relabel_post(self, T: int | None = None) -> dict:
         """Global half, one launch (amx_mmd_relabel): mean -> witness w (the fp64 mean rounded
         to fp32, count from the message's last slot) -> per-sample rewards of every recorded
-        transition, and the expert cost for the new w."""
+        transition (the first T steps; default: the current rollout's), and the expert cost for
+        the new w."""
         cost = self.cost
-        n = self.t * self.Bp
+        n = (self.t if T is None else T) * self.Bp
         self.mb_mmd = cost.relabel_device(self._fbuf, self.phi.data_ptr(), cost.feature_dim, self.disc.data_ptr(),
                                           float(self.ens.threshold), self.rewards.data_ptr(), self.ipm.data_ptr(),
                                           self.wbonus.data_ptr(), n)
@@ -411,6 +436,102 @@ class RolloutEngine:
             self._graph_ahead = True
             return T * self.B
         return replay
+
+    def rollout_overlapped(self, T: int, allreduce_async, tail=None) -> int:
+        """One rollout of T steps whose cross-rank all-reduce overlaps the NEXT rollout's first
+        ensemble forward (multi-rank MMD path): the rollout's [sum phi | count] message is
+        handed to `allreduce_async(buf)` (returns a handle with .wait(): e.g.
+        dist.all_reduce(async_op=True), which queues the GPU-side wait), and its relabel
+        (relabel_post + `tail()`) runs at the next rollout's step 0, between the forward and the
+        step kernel -- nothing the forward launches reads or writes the relabel's buffers
+        (phi, disc, the message, rewards).  flush_relabel() completes the last one.  The
+        results equal rollout(T); relabel(allreduce); tail() per rollout."""
+        if not isinstance(self.cost, RBFLinearCost):
+            raise RuntimeError("rollout_overlapped is the MMD path (RBFLinearCost)")
+        self.rollout(T)
+        self.relabel_pre()
+        h = allreduce_async(self._fbuf)
+
+        def pending():
+            h.wait()
+            self.relabel_post(T)
+            if tail is not None:
+                tail()
+        self._pending = pending
+        return T * self.B
+
+    def flush_relabel(self) -> None:
+        """Run the relabel rollout_overlapped left pending (no-op when none is)."""
+        if self._pending is not None:
+            pending, self._pending = self._pending, None
+            pending()
+
+    def graph_rollout_overlapped(self, T: int, allreduce_async, tail=None):
+        """rollout_overlapped as HIP graphs: G0 = the first step's policy + forward, G1 = the
+        previous rollout's relabel + tail, the first step kernel, steps 1..T-1, scoring and the
+        message; the all-reduce is issued between replays and waited for (GPU-side) only
+        before G1, so it runs under the next G0.  Returns (replay, flush): replay() runs one
+        rollout, flush() waits for the last all-reduce and runs its relabel (graph G2).  Run
+        one eager rollout + relabel first (t == T; its relabel is recomputed by the first
+        replay's G1, unchanged)."""
+        if not isinstance(self.cost, RBFLinearCost):
+            raise RuntimeError("graph_rollout_overlapped is the MMD path (RBFLinearCost)")
+        if self.t != T or self._pending is not None:
+            raise RuntimeError("run one eager rollout(T) + relabel before capturing")
+        fused = self.auto_reset and self.motion is None and self.fuse_reset
+        if not fused:
+            raise RuntimeError("graph_rollout_overlapped needs the fused step + table reset")
+        c = self.ctx
+        if self._graph_ahead:
+            self.step_counter = int(self.dev_step.item())
+        self.dev_step.fill_(self.step_counter)
+        graphs = [torch.cuda.CUDAGraph() for _ in range(3)]
+        side = torch.cuda.Stream(c.device)
+        side.wait_stream(torch.cuda.current_stream(c.device))
+        with torch.cuda.stream(side):
+            self._capturing = True
+            self._ctr_delta, self._ctr_folded = T, False
+            try:
+                with torch.cuda.graph(graphs[0], stream=side):
+                    self._rollout_begin()
+                    front = self._step_front(None, None)
+                with torch.cuda.graph(graphs[1], stream=side):
+                    self.relabel_post(T)
+                    if tail is not None:
+                        tail()
+                    self._step_back(front, None)
+                    for _ in range(T - 1):
+                        self.step()
+                    self.score()
+                    if not self._ctr_folded:
+                        N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), T, c.stream), "amx_counter_add")
+                    self.relabel_pre()
+                with torch.cuda.graph(graphs[2], stream=side):
+                    self.relabel_post(T)
+                    if tail is not None:
+                        tail()
+            finally:
+                self._capturing = False
+                self._ctr_delta = 0
+        torch.cuda.current_stream(c.device).wait_stream(side)
+        self._graph_ahead = True
+        state = {"h": None}
+
+        def replay():
+            graphs[0].replay()
+            if state["h"] is not None:
+                state["h"].wait()
+            graphs[1].replay()
+            state["h"] = allreduce_async(self._fbuf)
+            self._graph_ahead = True
+            return T * self.B
+
+        def flush():
+            if state["h"] is not None:
+                state["h"].wait()
+                state["h"] = None
+                graphs[2].replay()
+        return replay, flush
 
     def advantages(self, baseline, gamma: float = 0.995, gae_lambda=0.97, whiten: bool = False,
                    eps: float = 1e-6) -> dict:

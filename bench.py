@@ -89,6 +89,8 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the whole rollout as captured HIP graph(s); auto: when a rank's rollout is "
                         "small (< 16 384 samples) and host launch overhead would show")
+    p.add_argument("--overlap", choices=["on", "off"], default="on",
+                   help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward")
     p.add_argument("--motion", default=None, help="--cost amp: character + clip bundle (tools/pack_motion.py)")
     return p.parse_args()
 
@@ -210,6 +212,9 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
     allreduce = (lambda t: dist.all_reduce(t)) if world > 1 else None
+    # the overlapped form: the all-reduce is queued asynchronously (GPU-side wait) and runs under
+    # the next rollout's first ensemble forward (RolloutEngine.rollout_overlapped)
+    allreduce_async = (lambda t: dist.all_reduce(t, async_op=True)) if world > 1 else None
 
     # ---- model + data setup (untimed) -------------------------------------------------------
     hidden = [512] * 4
@@ -281,10 +286,20 @@ def main():
     if use_graph and args.gemm != "f16x3":
         raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
     timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
+    # N > 1 (MMD): each rollout's all-reduce overlaps the next rollout's first forward and its
+    # relabel runs after that forward; the last relabel is flushed inside the timed region
+    # (the first timed rollout also recomputes the warm-up's relabel: one extra relabel timed)
+    overlap = world > 1 and args.cost == "mmd" and args.overlap == "on"
+    tail = cost.get_expert_cost if args.cost == "mmd" else None
+    flush = eng.flush_relabel
     if use_graph:
-        tail = cost.get_expert_cost if args.cost == "mmd" else None
-        graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail)
-        graph()  # warm replay
+        if overlap:
+            graph, flush = eng.graph_rollout_overlapped(T, allreduce_async, tail=tail)
+            graph()  # warm replay
+            flush()
+        else:
+            graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail)
+            graph()  # warm replay
     torch.cuda.synchronize()
     if timer is not None:
         timer.zero_()
@@ -296,12 +311,18 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     samples = 0
-    if graph is None:
+    if graph is None and overlap:
+        for _ in range(args.steps):
+            samples += eng.rollout_overlapped(T, allreduce_async, tail=tail)
+        flush()
+    elif graph is None:
         for _ in range(args.steps):
             samples += one_rollout()
     else:
         for i in range(args.steps):
             samples += graph()
+        if overlap:
+            flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -373,7 +394,9 @@ def main():
                 "state_dim": S, "action_dim": A, "ensemble": "4 x dense-connect [512]x4 ReLU",
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
                 "parallelism": (f"dp{world} (the {args.total_samples}-sample rollout's lanes sharded over the "
-                                f"ranks, 1 all-reduce of [sum phi, count] per rollout)" if strong else
+                                f"ranks, 1 all-reduce of [sum phi, count] per rollout"
+                                f"{', overlapped with the next rollout' + chr(39) + 's first forward' if overlap else ''})"
+                                if strong else
                                 f"dp{world} (lane-sharded, {args.samples_per_gpu} samples per rank, 1 all-reduce "
                                 f"per rollout)"),
                 "termination_rate": round(term_rate, 5), "threshold": thr,

@@ -8,7 +8,9 @@ policy noise are injected from global per-lane arrays, so the union of the ranks
 is the same set of trajectories as one process running all B_TOTAL lanes.  The ranks'
 only exchange is RolloutEngine.relabel's all-reduce of [sum phi, count] (gloo here, over
 host copies; RCCL on the 8-GPU path).  Then a second engine checks the two-graph HIP-graph
-replay (graph_rollout with the all-reduce between the graphs) against eager rollouts.
+replay (graph_rollout with the all-reduce between the graphs) against eager rollouts, and two
+more the overlapped forms (rollout_overlapped / graph_rollout_overlapped: each all-reduce under
+the next rollout's first forward).
 """
 import os
 import sys
@@ -39,6 +41,15 @@ def main():
             h = t.cpu()
             dist.all_reduce(h)
             t.copy_(h)
+
+    class _Done:
+        def wait(self):
+            pass
+
+    def allreduce_async(t):  # the overlapped path's handle (gloo: completed at once)
+        if allreduce is not None:
+            allreduce(t)
+        return _Done()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     s, a, s2 = syn.offline(4096, S, A, 0)
@@ -88,7 +99,24 @@ def main():
         for _ in range(2):
             e1.rollout(); e1.relabel(allreduce); c1.get_expert_cost()
             replay()
+        # the overlapped forms (each all-reduce under the next rollout's first forward, its
+        # relabel after that forward; flush_relabel / flush for the last one), eager and graph
+        e3, c3 = engine(9)
+        e4, c4 = engine(9)
+        for e, c_ in ((e3, c3), (e4, c4)):
+            e.reset_all()
+            e.rollout(); e.relabel(allreduce); c_.get_expert_cost()
+        replay4, flush4 = e4.graph_rollout_overlapped(K, allreduce_async, tail=c4.get_expert_cost)
+        for _ in range(2):
+            e3.rollout_overlapped(K, allreduce_async, tail=c3.get_expert_cost)
+            replay4()
+        e3.flush_relabel()
+        flush4()
         torch.cuda.synchronize()
+        res.update(ovl_rewards=e3.rewards[:K, :B].cpu().numpy(), ovl_mmd=float(e3.mb_mmd.item()),
+                   ovl_obs=e3.obs.cpu().numpy(), ovl_expert=float(c3._expert_mean.item()),
+                   govl_rewards=e4.rewards[:K, :B].cpu().numpy(), govl_mmd=float(e4.mb_mmd.item()),
+                   govl_obs=e4.obs.cpu().numpy(), govl_expert=float(c4._expert_mean.item()))
         res.update(graph_rewards=e2.rewards[:K, :B].cpu().numpy(), eager_rewards=e1.rewards[:K, :B].cpu().numpy(),
                    graph_mmd=float(e2.mb_mmd.item()), eager_mmd=float(e1.mb_mmd.item()),
                    graph_obs=e2.obs.cpu().numpy(), eager_obs=e1.obs.cpu().numpy(),

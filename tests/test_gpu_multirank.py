@@ -74,3 +74,10 @@ def test_two_ranks_match_one_process_over_the_union(tmp_path):
         assert float(r["graph_mmd"]) == float(r["eager_mmd"])
         assert float(r["graph_expert"]) == float(r["eager_expert"])
     assert float(ranks[0]["graph_mmd"]) == float(ranks[1]["graph_mmd"])
+    # overlapped all-reduce (eager and graph) == eager rollout + relabel(allreduce), bit for bit
+    for r in ranks:
+        for pre in ("ovl", "govl"):
+            np.testing.assert_array_equal(r[pre + "_obs"], r["eager_obs"])
+            np.testing.assert_array_equal(r[pre + "_rewards"], r["eager_rewards"])
+            assert float(r[pre + "_mmd"]) == float(r["eager_mmd"])
+            assert float(r[pre + "_expert"]) == float(r["eager_expert"])
