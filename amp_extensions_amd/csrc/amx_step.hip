@@ -17,10 +17,30 @@
 
 namespace {
 
+// fp64 DPP move of both halves (lanes outside row_mask keep 0.0)
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RM, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum over the wave's 64 lanes, returned to every lane, on the DPP path (no LDS): xor 1 and 2
+// (quad_perm), the 8- and 16-lane mirrors (every lane of a row then holds the row sum), row
+// 0 -> 1 and 2 -> 3 (row_bcast:15), rows 0+1 -> 2, 3 (row_bcast:31), lane 63 read back.  A fixed
+// association: every caller (the fused step, k_disagreement) gets the same bits for the same
+// lane values.  (The LDS-based __shfl_xor butterfly cost 5.7 us of the 8192-lane step kernel's
+// 21.4 for its six pair sums, tools/step_time.py.)
 __device__ inline double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp_f64<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_f64<0x140, 0xf>(v);  // row_mirror
+  v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
 }
 
 // ---- assemble -----------------------------------------------------------------------
@@ -95,19 +115,21 @@ __device__ inline float lane_disagreement(const float* __restrict__ preds, long 
         acc[p++] += (double)d * (double)d;
       }
   }
-  float best = 0.f;
+  // max over pairs of (float)sqrt(sum) == (float)sqrt(max over pairs of sum): sqrt and the
+  // rounding are monotone, and the first-wins / NaN-skipping selection is the same on the sums
+  double best = 0.0;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const float n = (float)sqrt(wave_sum(acc[p]));
+    const double n = wave_sum(acc[p]);
     best = (p == 0 || n > best) ? n : best;
   }
-  return best;
+  return (float)sqrt(best);
 }
 
 // Generic member count: one pair at a time (re-reads the L2-hot rows), few registers.
 __device__ inline float lane_disagreement_any(const float* __restrict__ preds, long long strideP, int ldp, int b,
                                               int S, int M, int lane) {
-  float best = 0.f;
+  double best = 0.0;  // max of the sums, one sqrt (as lane_disagreement)
   bool first = true;
   for (int i = 0; i < M; ++i)
     for (int k = i + 1; k < M; ++k) {
@@ -116,11 +138,11 @@ __device__ inline float lane_disagreement_any(const float* __restrict__ preds, l
         const float d = preds[i * strideP + (long long)b * ldp + j] - preds[k * strideP + (long long)b * ldp + j];
         acc += (double)d * (double)d;
       }
-      const float n = (float)sqrt(wave_sum(acc));
+      const double n = wave_sum(acc);
       best = (first || n > best) ? n : best;
       first = false;
     }
-  return best;
+  return (float)sqrt(best);
 }
 
 // M = 4 (the MILO ensemble) gets the fused 6-pair pass; other sizes the generic loop.
@@ -292,11 +314,13 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
             }
         }
       }
+      double mx = 0.0;  // one sqrt of the max sum (lane_disagreement)
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
-        const float n = (float)sqrt(wave_sum(acc[q]));
-        d = (q == 0 || n > d) ? n : d;
+        const double n = wave_sum(acc[q]);
+        mx = (q == 0 || n > mx) ? n : mx;
       }
+      d = (float)sqrt(mx);
     }
   } else {
     if (a.disc) d = disagreement_dispatch(a.M, a.preds, a.strideP, a.ldp, b, S, lane);
@@ -381,15 +405,14 @@ __global__ __launch_bounds__(256) void k_reset(const uint8_t* __restrict__ mask,
 }
 
 // ---- policy ----------------------------------------------------------------------------------
-// One workgroup = 256 threads serving 256/TPL lanes, TPL = 16 or 32 threads per lane.
-// The whole MLP (W1 [H1][S], W2, W3) and the lanes' float32 observations are staged in LDS
-// once per workgroup.  Thread (lane l, u0) owns output units u = u0 + 16q of every layer; each
-// inner step loads one float4 of the lane's input row (broadcast over the lane's 16 threads)
-// and one float4 of each owned weight row — all loads issued before the FMAs, so the LDS
-// latency overlaps (rows beyond H are clamped to a valid row and their results dropped).
-// W rows use a padded stride (16-byte slots of rows 0..15 land on distinct banks).
+// One workgroup = 256 threads (4 waves) serving 16 lanes.  The whole MLP (W1 [H1][S], W2, W3)
+// and the lanes' float32 observations are staged in LDS once per workgroup; every dense layer
+// runs on the matrix pipe (v_mfma_f32_16x16x4_f32: the 16 lanes are the M dimension), its
+// 16-unit column blocks (and, for narrow layers, K halves) dealt over the 4 waves, then one
+// combine pass applies the fixed-order K-part sum, the bias and tanh.  Every LDS fragment read
+// is lane-distinct (no broadcast reads: see the note at pol_mfma_layer).  The Gaussian noise
+// takes one Philox block and one Box-Muller per (lane, action pair): both normals of the pair.
 constexpr int POL_LANES = 16;
-constexpr int POL_TPL = 16;
 constexpr int POL_MAXH = 256;
 
 __host__ __device__ inline int pol_stride(int k) {  // row stride (floats) for a [*, k] LDS matrix
@@ -405,9 +428,18 @@ __host__ __device__ inline int pol_blob_floats(int S, int H1, int H2, int A) {
   return (H1 * s1 + H2 * s2 + A * s3 + H1 + H2 + A + 3) & ~3;
 }
 
-__host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A, int lanes = POL_LANES) {
+// floats of the layers' partial-sum area: K parts x 16 lanes x (16 x column blocks)
+__host__ __device__ inline int pol_part_floats(int H1, int H2, int A) {
+  int h = H1 > H2 ? H1 : H2;
+  h = h > A ? h : A;
+  const int w = 16 * ((h + 15) / 16);
+  return POL_LANES * (w > 64 ? w : 64);
+}
+
+__host__ inline size_t pol_lds_bytes(int S, int H1, int H2, int A) {
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
-  const size_t fl = (size_t)pol_blob_floats(S, H1, H2, A) + lanes * (s1 + s2 + s3 + A);
+  const size_t fl = (size_t)pol_blob_floats(S, H1, H2, A) + POL_LANES * (s1 + s2 + s3 + 2 * A) +
+                    pol_part_floats(H1, H2, A);
   return fl * sizeof(float);
 }
 
@@ -469,86 +501,66 @@ __device__ inline void pol_stage_all(float* __restrict__ img, const float* __res
   }
 }
 
-// One dense layer for the lanes of a workgroup: thread (lane l, u0) computes units
-// u = u0 + 16q of lane l.  The lane's input row x is needed by all 16 threads of its DPP row
-// (16 consecutive threads): each thread reads its own float4 chunks c = u0 + 16j of the row
-// from LDS and the chunks are broadcast across the row with DPP row_newbcast.  Reading the
-// same 16 bytes from LDS with all 16 threads of a row (a broadcast ds_read_b128) returned
-// wrong data in wave lanes 48-63 on gfx950 whenever another workgroup on the CU ran
-// v_mfma_f32_16x16x32_f16 (reproduced with tools/victim.hip + tools/corunner.hip, DESIGN.md
-// §5.6), so no LDS read here is a broadcast: the weight rows of the 16 threads are distinct
-// (rows past H wrap around, their results are dropped) and the input comes through DPP.  The
-// summation order per unit is the chunk order k = 0 .. n4-1, as before.
-template <int XS>
-__device__ inline void pol_load_row(const float* __restrict__ x, int n4, int u0, pf4 (&xr)[XS]) {
+// One dense layer of the workgroup's 16 lanes on the matrix pipe: the raw x . W^T of 16 lanes x
+// N units, x rows [16][ldx] and W rows [N][ldw] in LDS, zero beyond K up to 4 nc.  Column block
+// nb (16 units) and K part kh of nblk x ksplit work items per wave (wave w takes items w, w + 4,
+// ...): 16x16x4 MFMAs over the chunks c = kq + 4 jj of its part, lane (i = l & 15, kq = l >> 4)
+// reading one float4 of x row i and one of W row 16 nb + i per 4 MFMAs (k = 4c + e: a
+// permutation of the K order, as any blocked fp32 matmul).  Fragment reads are lane-distinct:
+// a broadcast ds_read_b128 (all 16 threads of a row reading the same 16 B) returned wrong data
+// in lanes 48-63 on gfx950 beside a co-resident 16x16x32 f16 MFMA workgroup (tools/victim.hip
+// + tools/corunner.hip).  The raw partials go to `part` [ksplit][16][16 nblk]; after a barrier
+// pol_combine sums the K parts in order.  (Round 2: 3 MFMA layers + combine passes took the
+// in-kernel time from 17.4 to 15.9 us at 8192 lanes; the DPP-broadcast FMA chains before
+// spent 4.5 us in layer 1 alone.)
+__device__ inline int pol_ksplit(int nblk, int nc) {
+  const int jjt = (nc + 3) >> 2;
+  return nblk >= 4 ? 1 : (4 / nblk < jjt ? 4 / nblk : jjt);
+}
+
+__device__ inline void pol_mfma_layer(const float* __restrict__ x, int ldx, int nc, const float* __restrict__ w,
+                                      int ldw, int N, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int nblk = (N + 15) >> 4, jjt = (nc + 3) >> 2, ksplit = pol_ksplit(nblk, nc);
+  const int ldp = 16 * nblk;
+  for (int item = wave; item < nblk * ksplit; item += 4) {
+    const int nb = item % nblk, kh = item / nblk;
+    const int jj0 = kh * jjt / ksplit, jj1 = (kh + 1) * jjt / ksplit;
+    const int u = 16 * nb + i;
+    const float* xr = x + i * ldx;
+    const float* wr = w + (u < N ? u : 0) * ldw;
+    pf4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int jj = jj0; jj < jj1; ++jj) {
+      const int c = kq + 4 * jj;
+      const bool ok = c < nc;
+      const pf4 a = ok ? *reinterpret_cast<const pf4*>(xr + 4 * c) : pf4{0.f, 0.f, 0.f, 0.f};
+      const pf4 b = (ok && u < N) ? *reinterpret_cast<const pf4*>(wr + 4 * c) : pf4{0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+    }
+    float* pp = part + kh * 16 * ldp + 16 * nb + i;  // D row 4 kq + r, column i
 #pragma unroll
-  for (int j = 0; j < XS; ++j) {
-    const int c = u0 + 16 * j;
-    xr[j] = c < n4 ? *reinterpret_cast<const pf4*>(x + 4 * c) : pf4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) pp[(4 * kq + r) * ldp] = acc[r];
   }
 }
 
-template <int N>
-__device__ __forceinline__ float pol_bcast(float v) {  // lane N of each 16-lane DPP row to the whole row
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x150 + N, 0xf, 0xf,
-                                                               false));
-}
-
-template <int Q, int N>
-__device__ __forceinline__ void pol_chunk(const pf4& xk, const float* const (&wr)[Q], int k, float (&acc)[Q]) {
-  pf4 v;
-  v.x = pol_bcast<N>(xk.x);
-  v.y = pol_bcast<N>(xk.y);
-  v.z = pol_bcast<N>(xk.z);
-  v.w = pol_bcast<N>(xk.w);
-  pf4 a[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) a[q] = *reinterpret_cast<const pf4*>(wr[q] + 4 * k);
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    acc[q] = fmaf(a[q].x, v.x, acc[q]);
-    acc[q] = fmaf(a[q].y, v.y, acc[q]);
-    acc[q] = fmaf(a[q].z, v.z, acc[q]);
-    acc[q] = fmaf(a[q].w, v.w, acc[q]);
+// out[l][u] = act(sum over K parts + bias) for the 16 lanes x N units (after a barrier)
+__device__ inline void pol_combine(const float* __restrict__ part, int N, int nc, const float* __restrict__ bias,
+                                   bool tanh_act, float* __restrict__ out, int ldo) {
+  const int nblk = (N + 15) >> 4, ksplit = pol_ksplit(nblk, nc), ldp = 16 * nblk;
+  for (int e = threadIdx.x; e < POL_LANES * N; e += 256) {
+    const int l = e / N, u = e - l * N;
+    float z = part[l * ldp + u];
+    for (int kh = 1; kh < ksplit; ++kh) z += part[(kh * 16 + l) * ldp + u];
+    z = z + bias[u];                               // nn.Linear: x W^T + b
+    out[l * ldo + u] = tanh_act ? tanhf(z) : z;    // FCNetwork: tanh hidden, identity output
   }
 }
 
-template <int Q, int... N>
-__device__ __forceinline__ void pol_slot(const pf4& xk, const float* const (&wr)[Q], int k0, int n4, float (&acc)[Q],
-                                         std::integer_sequence<int, N...>) {
-  // chunks k0 .. k0+15 (the slot's owners are lanes 0..15 of the row); n4 is uniform
-  ((k0 + N < n4 ? pol_chunk<Q, N>(xk, wr, k0 + N, acc) : (void)0), ...);
-}
-
-template <int TPL, int Q>
-__device__ inline void pol_layer(const float* __restrict__ w, int ws, const float* __restrict__ x, int n4,
-                                 const float* __restrict__ bias, int H, int u0, float (&out)[Q], bool tanh_act) {
-  static_assert(TPL == 16, "one lane per 16-thread DPP row");
-  constexpr int XS = (POL_MAXH / 4 + 15) / 16;  // chunk slots per thread (rows up to POL_MAXH floats)
-  float acc[Q];
-  const float* wr[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    acc[q] = 0.f;
-    const int u = u0 + TPL * q;
-    wr[q] = w + (u < H ? u : u % H) * ws;  // distinct rows within the 16 threads (H >= 16)
-  }
-  pf4 xr[XS];
-  pol_load_row<XS>(x, n4, u0, xr);
-#pragma unroll
-  for (int j = 0; j < XS; ++j)
-    if (16 * j < n4) pol_slot<Q>(xr[j], wr, 16 * j, n4, acc, std::make_integer_sequence<int, 16>{});
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int u = u0 + TPL * q;
-    const float z = acc[q] + bias[u < H ? u : H - 1];
-    out[q] = tanh_act ? tanhf(z) : z;
-  }
-}
-
-template <int TPL, int QH, int QA>
 __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
-  constexpr int POL_LANES = 256 / TPL;  // lanes per workgroup
   extern __shared__ __attribute__((aligned(16))) float psm[];
   const int S = p.S, A = p.A, H1 = p.H1, H2 = p.H2;
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
@@ -559,73 +571,75 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   float* bb2 = bb1 + H1;
   float* bb3 = bb2 + H2;
   const int nblob = pol_blob_floats(S, H1, H2, A);
-  float* so = psm + nblob;               // [POL_LANES][s1]
-  float* h1 = so + POL_LANES * s1;       // [POL_LANES][s2]
-  float* h2 = h1 + POL_LANES * s2;       // [POL_LANES][s3]
-  float* xa_s = h2 + POL_LANES * s3;     // [POL_LANES][A] float32 actions for the fused assembly
+  float* so = psm + nblob;               // [16][s1]
+  float* h1 = so + POL_LANES * s1;       // [16][s2]
+  float* h2 = h1 + POL_LANES * s2;       // [16][s3]
+  float* mo = h2 + POL_LANES * s3;       // [16][A] policy means
+  float* xa_s = mo + POL_LANES * A;      // [16][A] float32 actions for the fused assembly
+  float* part = xa_s + POL_LANES * A;    // layer partial sums (pol_part_floats)
   const int t = threadIdx.x;
   const int b0 = blockIdx.x * POL_LANES;
   // staging: the packed weight image (pads already zero) and the block's observation rows;
-  // the observation pads / rows of lanes >= B are zeroed (they take part in the float4 dots)
+  // the observation pads / rows of lanes >= B are zeroed (they take part in the MFMAs)
   const int nl = (p.B - b0) < POL_LANES ? (p.B - b0) : POL_LANES;  // valid lanes of this block
   pol_zero_pads(so, s1, S, nl);
   for (int i = t + nl * s1; i < POL_LANES * s1; i += 256) so[i] = 0.f;
   pol_stage_all(psm, p.blob, nblob >> 2, so, s1, p.ob + (long long)b0 * S, nl * S, S);
   for (int i = t; i < POL_LANES * (s2 + s3); i += 256) h1[i] = 0.f;  // pads of h1/h2
   __syncthreads();
-
-  const int l = t / TPL, u0 = t % TPL;
-  const int b = b0 + l;
-  {
-    float o[QH];
-    pol_layer<TPL, QH>(w1, s1, so + l * s1, (S + 3) >> 2, bb1, H1, u0, o, true);
-#pragma unroll
-    for (int q = 0; q < QH; ++q) if (u0 + TPL * q < H1) h1[l * s2 + u0 + TPL * q] = o[q];
-  }
+  const int nc1 = (S + 3) >> 2, nc2 = (H1 + 3) >> 2, nc3 = (H2 + 3) >> 2;
+  pol_mfma_layer(so, s1, nc1, w1, s1, H1, part);
   __syncthreads();
-  {
-    float o[QH];
-    pol_layer<TPL, QH>(w2, s2, h1 + l * s2, (H1 + 3) >> 2, bb2, H2, u0, o, true);
-#pragma unroll
-    for (int q = 0; q < QH; ++q) if (u0 + TPL * q < H2) h2[l * s3 + u0 + TPL * q] = o[q];
-  }
+  pol_combine(part, H1, nc1, bb1, true, h1, s2);
   __syncthreads();
-  float o[QA];
-  pol_layer<TPL, QA>(w3, s3, h2 + l * s3, (H2 + 3) >> 2, bb3, A, u0, o, false);
-#pragma unroll
-  for (int q = 0; q < QA; ++q) {
-    const int u = u0 + TPL * q;
-    if (u >= A || b >= p.B) continue;
-    const float m = o[q];  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
-    if (p.mean_out) p.mean_out[(long long)b * A + u] = m;
-    double a_out;
-    if (p.eval_mode) {
-      a_out = (double)m;
-    } else {
-      double n;
-      if (p.noise) {
-        n = p.noise[(long long)b * A + u];
-      } else {
-        // Box-Muller on one Philox block: pair u/2 yields the normals of u = 2p, 2p+1
-        const int pr = u >> 1;
-        uint32_t ctr_lo = p.ctr_lo, ctr_hi = p.ctr_hi;
-        if (p.ctr_dev) {  // device counter + the by-value offset
-          const uint64_t cv = *p.ctr_dev + ((uint64_t)p.ctr_hi << 32 | p.ctr_lo);
-          ctr_lo = (uint32_t)cv;
-          ctr_hi = (uint32_t)(cv >> 32);
-        }
-        const amx::u32x4 r = amx::philox4x32_10(
-            {(uint32_t)b, ctr_lo, ((uint32_t)pr << 8) | (ctr_hi & 0xffu), amx::kTagPolicy}, p.k0, p.k1);
-        const double u1 = 1.0 - amx::u53(r.x, r.y);  // (0, 1]
-        const double u2 = amx::u53(r.z, r.w);
-        const double rad = sqrt(-2.0 * log(u1));
-        const double ang = 6.283185307179586 * u2;
-        n = (u & 1) ? rad * sin(ang) : rad * cos(ang);
-      }
-      a_out = (double)m + p.nscale[u] * n;  // gaussian_mlp.py:102-103 (float32 mean + float64 noise)
+  pol_mfma_layer(h1, s2, nc2, w2, s2, H2, part);
+  __syncthreads();
+  pol_combine(part, H2, nc2, bb2, true, h2, s3);
+  __syncthreads();
+  pol_mfma_layer(h2, s3, nc3, w3, s3, A, part);
+  __syncthreads();
+  pol_combine(part, A, nc3, bb3, false, mo, A);  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
+  __syncthreads();
+  // actions: one thread per (lane, pair u = 2pr, 2pr + 1): Box-Muller on one Philox block gives
+  // both normals of the pair (gaussian_mlp.py:102-103: float32 mean + float64 noise)
+  const int npairs = (A + 1) >> 1;
+  uint32_t ctr_lo = p.ctr_lo, ctr_hi = p.ctr_hi;
+  if (p.ctr_dev) {  // device counter + the by-value offset
+    const uint64_t cv = *p.ctr_dev + ((uint64_t)p.ctr_hi << 32 | p.ctr_lo);
+    ctr_lo = (uint32_t)cv;
+    ctr_hi = (uint32_t)(cv >> 32);
+  }
+  for (int e = t; e < POL_LANES * npairs; e += 256) {
+    const int l = e / npairs, pr = e - l * npairs;
+    const int b = b0 + l;
+    if (b >= p.B) continue;
+    double n[2] = {0.0, 0.0};
+    if (!p.eval_mode && !p.noise) {
+      const amx::u32x4 r = amx::philox4x32_10(
+          {(uint32_t)b, ctr_lo, ((uint32_t)pr << 8) | (ctr_hi & 0xffu), amx::kTagPolicy}, p.k0, p.k1);
+      const double u1 = 1.0 - amx::u53(r.x, r.y);  // (0, 1]
+      const double u2 = amx::u53(r.z, r.w);
+      const double rad = sqrt(-2.0 * log(u1));
+      const double ang = 6.283185307179586 * u2;
+      n[0] = rad * cos(ang);
+      n[1] = rad * sin(ang);
     }
-    p.act[(long long)b * A + u] = a_out;
-    if (p.x0) xa_s[l * A + u] = (float)a_out;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = 2 * pr + h;
+      if (u >= A) break;
+      const float m = mo[l * A + u];
+      if (p.mean_out) p.mean_out[(long long)b * A + u] = m;
+      double a_out;
+      if (p.eval_mode) {
+        a_out = (double)m;
+      } else {
+        const double nz = p.noise ? p.noise[(long long)b * A + u] : n[h];
+        a_out = (double)m + p.nscale[u] * nz;
+      }
+      p.act[(long long)b * A + u] = a_out;
+      if (p.x0) xa_s[l * A + u] = (float)a_out;
+    }
   }
   if (!p.x0) return;
   __syncthreads();
@@ -901,12 +915,7 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
                              (ctx->M == 1 || stride_rexp >= (long long)n_slots * slot_stride)),
                 "amx_policy_act: row_exp needs x0_buf, 1 <= n_slots <= 64, slot_stride >= B, stride_rexp");
   if (B == 0) return AMX_OK;
-  // 16 threads per lane, 16 lanes per workgroup (32 threads per lane measured 1.3 % slower
-  // per rollout in round 1, profiles/r01_policy_tpl.txt)
-  const int hmax = H1 > H2 ? H1 : H2;
-  constexpr int tpl = 16;
-  const int lanes = 256 / tpl;
-  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A, lanes);
+  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S/H too large for LDS staging (%zu B)", lds);
   PolicyArgs p;
   p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;
@@ -917,15 +926,7 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
   p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
   p.row_exp = row_exp; p.stride_rexp = stride_rexp; p.slot_stride = slot_stride; p.n_slots = n_slots;
   p.S = ctx->S; p.A = ctx->A; p.B = B;
-  dim3 grid((B + lanes - 1) / lanes);
-  // outputs per thread, rounded up to a compiled width: hidden layers QH, action layer QA
-  const int qh = (hmax + tpl - 1) / tpl;
-  const int qa = (ctx->A + tpl - 1) / tpl;
-  hipStream_t st = (hipStream_t)stream;
-  if (qh <= 2 && qa <= 2) hipLaunchKernelGGL((k_policy<16, 2, 2>), grid, dim3(256), lds, st, p);
-  else if (qh <= 2 && qa <= 3) hipLaunchKernelGGL((k_policy<16, 2, 3>), grid, dim3(256), lds, st, p);
-  else if (qh <= 4 && qa <= 4) hipLaunchKernelGGL((k_policy<16, 4, 4>), grid, dim3(256), lds, st, p);
-  else hipLaunchKernelGGL((k_policy<16, 16, 16>), grid, dim3(256), lds, st, p);
+  hipLaunchKernelGGL(k_policy, dim3((B + POL_LANES - 1) / POL_LANES), dim3(256), lds, (hipStream_t)stream, p);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
