@@ -98,13 +98,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
         }
       }
     }
-  } else {  // EPI_RFF (instantiated for the 128x128 tile only)
-    static_assert(BM == 128 && BN == 128 && TL::NT == 256, "RFF epilogue assumes the 128x128 tile");
-    // Stage the raw 128x128 tile through LDS, then one column per thread: coalesced phi
-    // rows, one (non-unrolled) cos call site instead of 64 inlined copies, and the fp64
-    // column sum of the valid rows in fixed row order (deterministic).
-    constexpr int CLD = BN + 4;
-    float* Cs = smem;  // [BM][CLD] = 67,584 B, reuses the stage buffers (last barrier passed)
+  } else {  // EPI_RFF (128 x 128 or 128 x 64 tiles of 256 threads)
+    static_assert(BM == 128 && (BN == 128 || BN == 64) && TL::NT == 256, "RFF epilogue tiles");
+    // Stage the raw BM x BN tile through LDS, then one column per thread over BM / PARTS rows:
+    // coalesced phi rows, one (non-unrolled) cos call site instead of 64 inlined copies, and
+    // the fp64 column sum of the valid rows in fixed row order, the PARTS part sums added in
+    // part order (deterministic; 2 parts at BN 128, 4 at BN 64).
+    constexpr int CLD = BN + 4, PARTS = 256 / BN, PR = BM / PARTS;
+    float* Cs = smem;  // [BM][CLD] (<= 67,584 B), reuses the stage buffers (last barrier passed)
 #pragma unroll
     for (int n = 0; n < TN; ++n)
 #pragma unroll
@@ -115,14 +116,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
           Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
         }
     __syncthreads();
-    const int c = t & (BN - 1), half = t >> 7;
+    const int c = t & (BN - 1), part = t / BN;
     const int col = tn * BN + c;
     const float bv = a.bias[col];
     double csum = 0.0;
     float* Cg = a.C;
 #pragma unroll 2
-    for (int i = 0; i < BM / 2; ++i) {
-      const int r = half * (BM / 2) + i;
+    for (int i = 0; i < PR; ++i) {
+      const int r = part * PR + i;
       const int row = tm * BM + r;
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
       const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
@@ -131,10 +132,15 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
       csum += valid ? (double)phi : 0.0;
     }
     __syncthreads();
-    double* red = reinterpret_cast<double*>(smem);
-    if (half == 1) red[c] = csum;
+    double* red = reinterpret_cast<double*>(smem);  // [PARTS][BN]
+    red[part * BN + c] = csum;
     __syncthreads();
-    if (half == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[c];
+    if (part == 0) {
+      double sum = red[c];
+#pragma unroll
+      for (int q = 1; q < PARTS; ++q) sum += red[q * BN + c];
+      a.col_partials[(long long)tm * a.N + col] = sum;
+    }
   }
 }
 
@@ -1221,6 +1227,10 @@ using H256 = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 template <int MB> using HRow = TileH3<2, 4, 1, 1, 2, 2, true, true, true, MB, 4, true, true, true>;
 template <int RW, int NBO> using HOut = TileH3<RW, 1, 1, 1, 2, 2, true, true, true, 2, NBO, true, true, true>;
 using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;
+// RFF features at row counts whose 128 x 128 tiles fill less than the CUs (the 4- and 8-GPU
+// strong-scaling shares): 128 x 64, 4 waves of 32 x 64 (half the work per workgroup, twice
+// the workgroups; the same column-partial layout [rows / 128][F])
+using H128x64k32 = TileH3<4, 1, 1, 2, 2, 2>;
 using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
 using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true, true>;  // + DEEPA (-2 %)
 
@@ -1273,7 +1283,8 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   const int tiles = a.tiles_m * a.tiles_n * a.groups;
   const int nwg = a.streamk ? a.streamk : tiles;  // stream-K: a.streamk workgroups
   if (tiles == 0) return AMX_OK;
-  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
+  constexpr size_t rff_lds = (size_t)TL::BM * (TL::BN + 4) * 4;  // the RFF epilogue's staged tile
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_lds) ? rff_lds : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
@@ -1662,7 +1673,10 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.C = phi; a.ldc = ldphi;
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
-  if (K % 32 == 0) return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
+  if (K % 32 == 0) {
+    if ((rows / 128) * (F / 128) < ctx->n_cus && F % 64 == 0) return launch_h3<EPI_RFF, H128x64k32>(a, (hipStream_t)stream);
+    return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
+  }
   return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);
 }
 
