@@ -1674,6 +1674,7 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
   if (K % 32 == 0) {
+    // (at 40 960 rows the 128 x 128 tile is faster: 121 vs 145 us under the profiler)
     if ((rows / 128) * (F / 128) < ctx->n_cus && F % 64 == 0) return launch_h3<EPI_RFF, H128x64k32>(a, (hipStream_t)stream);
     return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
   }
