@@ -445,7 +445,9 @@ class RolloutEngine:
         (relabel_post + `tail()`) runs at the next rollout's step 0, between the forward and the
         step kernel -- nothing the forward launches reads or writes the relabel's buffers
         (phi, disc, the message, rewards).  flush_relabel() completes the last one.  The
-        results equal rollout(T); relabel(allreduce); tail() per rollout."""
+        results equal rollout(T); relabel(allreduce); tail() per rollout.  Valid while the
+        rollouts share the policy (fixed-policy collection, evaluation): a trainer that updates
+        the policy from one rollout's rewards before the next uses rollout + relabel."""
         if not isinstance(self.cost, RBFLinearCost):
             raise RuntimeError("rollout_overlapped is the MMD path (RBFLinearCost)")
         self.rollout(T)

@@ -89,8 +89,12 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the whole rollout as captured HIP graph(s); auto: when a rank's rollout is "
                         "small (< 16 384 samples) and host launch overhead would show")
-    p.add_argument("--overlap", choices=["on", "off"], default="on",
-                   help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward")
+    p.add_argument("--fuse-assembly", choices=["on", "off"], default="off",
+                   help="f16x3: the policy launch also writes the ensemble's x0 slice (RolloutEngine.fuse_assembly)")
+    p.add_argument("--overlap", choices=["on", "off"], default="off",
+                   help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward (valid "
+                        "only while consecutive rollouts share the policy: fixed-policy collection / evaluation; "
+                        "a trainer updates the policy between iterations, so the default is the serial order)")
     p.add_argument("--motion", default=None, help="--cost amp: character + clip bundle (tools/pack_motion.py)")
     return p.parse_args()
 
@@ -230,7 +234,7 @@ def main():
     thr = ens.compute_threshold(st.to(dev), at.to(dev))
     reset_source = syn.reset_table(65536, S, 1)
     if args.cost == "amp":
-        # humanoid3d + spinkick clip (the reference's data files, held as a test fixture);
+        # humanoid3d + spinkick clip (the package's data bundle, amp_extensions_amd/data, or --motion);
         # expert rows = AMP features of the clip at uniform times (RecordAMPObsExpert)
         from amp_extensions_amd.motion import ReferenceMotion
         reset_source = ReferenceMotion.from_bundle(ctx, args.motion)
@@ -253,6 +257,7 @@ def main():
     B, T = plan_lanes(per_rank, args.max_lanes, args.lanes)
     eng = amx.RolloutEngine(ens, reset_source, lanes=B, policy=pol, cost=cost,
                             seed=(7 << 32) + rank, max_steps=T)
+    eng.fuse_assembly = args.fuse_assembly == "on"
     eng.reset_all()
     # steady-state phase: a long-running lane fleet has its trajectories at uniformly spread
     # positions, so horizon resets (1/300 per step) happen inside the timed region as they do
@@ -286,9 +291,11 @@ def main():
     if use_graph and args.gemm != "f16x3":
         raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
     timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
-    # N > 1 (MMD): each rollout's all-reduce overlaps the next rollout's first forward and its
-    # relabel runs after that forward; the last relabel is flushed inside the timed region
-    # (the first timed rollout also recomputes the warm-up's relabel: one extra relabel timed)
+    # --overlap on (N > 1, MMD): each rollout's all-reduce overlaps the next rollout's first
+    # forward and its relabel runs after that forward; the last relabel is flushed inside the
+    # timed region (the first timed rollout also recomputes the warm-up's relabel: one extra
+    # relabel timed).  Off by default: a trainer's policy update sits between two iterations'
+    # rollouts, so the headline keeps the serial rollout -> all-reduce -> relabel order.
     overlap = world > 1 and args.cost == "mmd" and args.overlap == "on"
     tail = cost.get_expert_cost if args.cost == "mmd" else None
     flush = eng.flush_relabel
