@@ -10,10 +10,27 @@
 
 namespace {
 
+// fp64 DPP move of both halves (lanes outside row_mask keep 0.0)
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, RM, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, RM, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum over the wave's 64 lanes, returned to every lane, on the DPP path (no LDS traffic; the
+// same fixed association as amx_step.hip's): quad xor 1, 2, the 8- and 16-lane mirrors, rows
+// 0 -> 1, 2 -> 3 (row_bcast:15), rows 0+1 -> 2, 3 (row_bcast:31), lane 63 read back.
 __device__ inline double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
+  v += dpp_f64<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_f64<0x140, 0xf>(v);  // row_mirror
+  v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 into rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 into rows 2, 3
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), 63);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), 63);
+  return __hiloint2double(hi, lo);
 }
 
 // out[f] = sum_p partials[p][f].  Block = 64 columns x 16 waves; wave w sums its contiguous
@@ -192,9 +209,7 @@ __device__ inline void rows_dot(const float4 (&p)[R][NC > 0 ? NC : 1], const flo
       d[i] = s;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-      for (int i = 0; i < R; ++i) d[i] += __shfl_xor(d[i], o);
+    for (int i = 0; i < R; ++i) d[i] = wave_sum(d[i]);  // row_dot's reduction
   }
 }
 
