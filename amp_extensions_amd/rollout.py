@@ -351,6 +351,7 @@ class RolloutEngine:
         """Relabel the recorded transitions (batch_reinforce.py:103-169, MMD + ensemble).
         `allreduce(tensor)` sums a device tensor across ranks in place (None: one rank)."""
         cost = self.cost
+        self.flush_relabel()  # a relabel rollout_overlapped left pending comes first
         self.score()
         if isinstance(cost, GAILCost):
             return {}  # rewards come from the discriminator pass
