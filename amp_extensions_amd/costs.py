@@ -107,6 +107,12 @@ class RBFLinearCost:
         # set when the last relabel_device launch also computed the expert cost for the current w
         self._expert_fresh = False
         self._counter = torch.zeros(4, dtype=torch.int32, device=ctx.device)  # amx_mmd_relabel's arrivals
+        # expert rows this rank scores (shard_expert: a contiguous block per rank, partial sums
+        # all-reduced asynchronously -- the expert cost only feeds the bonus_mmd log)
+        self._elo, self._ehi = 0, self.n_expert
+        self._ear = None   # allreduce_async of the sharded partial sum (None: one rank, whole buffer)
+        self._eh = None    # the pending all-reduce handle of the last sharded partial sum
+        self._escale = torch.tensor([1.0 - lambda_b], dtype=torch.float32, device=ctx.device)
 
     # linear_cost.py:73-82
     def fit_bandwidth(self, data: torch.Tensor) -> float:
@@ -136,6 +142,46 @@ class RBFLinearCost:
             self.w = torch.empty(self.feature_dim, dtype=torch.float32, device=c.device)
             self._mmd = torch.empty(1, dtype=torch.float32, device=c.device)
 
+    def shard_expert(self, rank: int, world: int, allreduce_async) -> None:
+        """Score only this rank's contiguous block of the resident expert rows in the relabel
+        and sum the ranks' fp64 partial sums with `allreduce_async(buf)` (returns a handle with
+        .wait(), e.g. dist.all_reduce(async_op=True)), issued by expert_allreduce() off the
+        rollout's critical path: get_expert_cost (linear_cost.py:105-109; bonus_mmd's expert
+        term, batch_reinforce.py:169, a log value) waits for it when read.  SURVEY §8(e): phi_e
+        replicated, the expert buffer's cost sharded, one scalar all-reduce for the log."""
+        from .dist import shard
+        if world > self.n_expert:
+            raise ValueError(f"{self.n_expert} expert rows cannot be sharded over {world} ranks")
+        self._elo, self._ehi = shard(self.n_expert, rank, world)
+        self._ear = allreduce_async if world > 1 else None
+
+    @property
+    def expert_sharded(self) -> bool:
+        return self._ear is not None
+
+    def expert_allreduce(self):
+        """Issue the all-reduce of the last relabel's partial expert sum (sharded mode; no-op
+        otherwise); returns the handle (the next relabel waits for it, GPU-side, before it
+        overwrites the sum)."""
+        if self._ear is None or not self._expert_fresh:
+            return None
+        self._eh = self._ear(self._expert_out[:1])
+        return self._eh
+
+    def wait_expert_allreduce(self) -> None:
+        """Queue the wait (GPU-side) for the pending expert-sum all-reduce (graph replays call it
+        before the graph whose relabel overwrites the sum; eager relabels call it themselves)."""
+        if self._eh is not None and not torch.cuda.is_current_stream_capturing():
+            self._eh.wait()
+            self._eh = None
+
+    def _expert_args(self):
+        """(rows pointer, row count, mean_out) of the expert rows this rank scores."""
+        ld = self.expert_rep.stride(0)
+        ptr = self.expert_rep.data_ptr() + self._elo * ld * self.expert_rep.element_size()
+        mean = None if self._ear is not None else self._expert_mean.data_ptr()
+        return ptr, self._ehi - self._elo, mean
+
     def relabel_device(self, msg: torch.Tensor, phi, ldphi: int, disc, thr: float, reward, ipm, wb,
                        n: int) -> torch.Tensor:
         """The relabel tail in one launch (amx_mmd_relabel): w and w.w from the (all-reduced)
@@ -147,14 +193,14 @@ class RBFLinearCost:
         expert = self.cost_range is not None
         if expert and self._expert_mean is None:
             self._expert_mean = torch.empty(1, dtype=torch.float32, device=c.device)
+        self.wait_expert_allreduce()  # the previous partial sum's all-reduce reads the buffer this launch writes
+        eptr, ne, emean = self._expert_args() if expert else (None, self.n_expert, None)
         N.check(c.lib.amx_mmd_relabel(c.h, msg.data_ptr(), 0.0, self.phi_e.data_ptr(), self.feature_dim,
                                       self.w.data_ptr(), self._mmd.data_ptr(), phi, ldphi, disc, float(thr),
                                       self.lambda_b, 1 if expert else 0, self.c_min if expert else 0.0,
                                       self.c_max if expert else 0.0, reward, ipm, wb, n,
-                                      self.expert_rep.data_ptr() if expert else None, self.expert_rep.stride(0),
-                                      self.n_expert, self._expert_out.data_ptr(),
-                                      self._expert_mean.data_ptr() if expert else None, self._counter.data_ptr(),
-                                      c.stream), "amx_mmd_relabel")
+                                      eptr, self.expert_rep.stride(0), ne, self._expert_out.data_ptr(),
+                                      emean, self._counter.data_ptr(), c.stream), "amx_mmd_relabel")
         self._expert_fresh = expert
         return self._mmd
 
@@ -208,10 +254,25 @@ class RBFLinearCost:
         if self.cost_range is None:   # the reference clamps with c_min/c_max, unset without a range
             raise AttributeError("'RBFLinearCost' object has no attribute 'c_min'")
         c = self.ctx
-        if self._expert_fresh:  # computed for the current w by the relabel launch
-            return self._expert_mean[0]
         if self._expert_mean is None:
             self._expert_mean = torch.empty(1, dtype=torch.float32, device=c.device)
+        if self._ear is not None:  # sharded: this rank's partial sum, all-reduced
+            if not self._expert_fresh or self._eh is None:
+                if not self._expert_fresh:
+                    self.wait_expert_allreduce()
+                    eptr, ne, _ = self._expert_args()
+                    N.check(c.lib.amx_expert_cost(c.h, eptr, self.expert_rep.stride(0), self.w.data_ptr(),
+                                                  self.feature_dim, ne, self.c_min, self.c_max,
+                                                  self._expert_out.data_ptr(), None, float(self.lambda_b),
+                                                  c.stream), "amx_expert_cost")
+                    self._expert_fresh = True
+                self.expert_allreduce()
+            self.wait_expert_allreduce()
+            # (1 - lambda) * float32(sum / n) as k_sum_small's mean_out (the fp32 product of torch)
+            torch.mul((self._expert_out[:1] / self.n_expert).float(), self._escale, out=self._expert_mean)
+            return self._expert_mean[0]
+        if self._expert_fresh:  # computed for the current w by the relabel launch
+            return self._expert_mean[0]
         N.check(c.lib.amx_expert_cost(c.h, self.expert_rep.data_ptr(), self.expert_rep.stride(0), self.w.data_ptr(),
                                       self.feature_dim, self.n_expert, self.c_min, self.c_max,
                                       self._expert_out.data_ptr(), self._expert_mean.data_ptr(),

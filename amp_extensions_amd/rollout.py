@@ -386,12 +386,15 @@ class RolloutEngine:
                                           self.wbonus.data_ptr(), n)
         return {"mb_mmd": self.mb_mmd}
 
-    def graph_rollout(self, T: int | None = None, allreduce=None, tail=None):
+    def graph_rollout(self, T: int | None = None, allreduce=None, tail=None, before_relabel=None, after=None):
         """Capture one full rollout (K steps + scoring + relabel + `tail()`, e.g. the expert
         cost) as HIP graph(s) on the current device and return `replay()`; replaying it is
         equivalent to `rollout(T); relabel(allreduce); tail()` (the policy's Philox counter
         lives on the device).  With `allreduce` (several ranks) the collective stays eager
-        between two graphs.  Run one eager rollout first (workspaces allocated, t == T)."""
+        between two graphs; `before_relabel()` runs on the host right before the relabel's graph
+        and `after()` after the last one (e.g. RBFLinearCost.wait_expert_allreduce /
+        expert_allreduce of a sharded expert cost).  Run one eager rollout first (workspaces
+        allocated, t == T)."""
         T = self.K if T is None else T
         if self.t != T:
             raise RuntimeError("run one eager rollout(T) before capturing")
@@ -432,8 +435,12 @@ class RolloutEngine:
         def replay():
             graphs[0].replay()
             if two:
+                if before_relabel is not None:
+                    before_relabel()
                 allreduce(self._fbuf)
                 graphs[1].replay()
+            if after is not None:
+                after()
             self._graph_ahead = True
             return T * self.B
         return replay
@@ -469,14 +476,15 @@ class RolloutEngine:
             pending, self._pending = self._pending, None
             pending()
 
-    def graph_rollout_overlapped(self, T: int, allreduce_async, tail=None):
+    def graph_rollout_overlapped(self, T: int, allreduce_async, tail=None, before_relabel=None, after=None):
         """rollout_overlapped as HIP graphs: G0 = the first step's policy + forward, G1 = the
         previous rollout's relabel + tail, the first step kernel, steps 1..T-1, scoring and the
         message; the all-reduce is issued between replays and waited for (GPU-side) only
         before G1, so it runs under the next G0.  Returns (replay, flush): replay() runs one
         rollout, flush() waits for the last all-reduce and runs its relabel (graph G2).  Run
         one eager rollout + relabel first (t == T; its relabel is recomputed by the first
-        replay's G1, unchanged)."""
+        replay's G1, unchanged).  `before_relabel()` / `after()`: host hooks around the graphs
+        holding a relabel (as graph_rollout's)."""
         if not isinstance(self.cost, RBFLinearCost):
             raise RuntimeError("graph_rollout_overlapped is the MMD path (RBFLinearCost)")
         if self.t != T or self._pending is not None:
@@ -524,8 +532,12 @@ class RolloutEngine:
             graphs[0].replay()
             if state["h"] is not None:
                 state["h"].wait()
+            if before_relabel is not None:
+                before_relabel()
             graphs[1].replay()
             state["h"] = allreduce_async(self._fbuf)
+            if after is not None:
+                after()
             self._graph_ahead = True
             return T * self.B
 
@@ -533,7 +545,11 @@ class RolloutEngine:
             if state["h"] is not None:
                 state["h"].wait()
                 state["h"] = None
+                if before_relabel is not None:
+                    before_relabel()
                 graphs[2].replay()
+                if after is not None:
+                    after()
         return replay, flush
 
     def advantages(self, baseline, gamma: float = 0.995, gae_lambda=0.97, whiten: bool = False,

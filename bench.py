@@ -266,10 +266,19 @@ def main():
     eng.num_steps.copy_(torch.randint(0, horizon, (B,), generator=torch.Generator().manual_seed(11 + rank),
                                       dtype=torch.int32).to(dev))
 
+    # N > 1 (MMD): each rank scores N_e / N expert rows in its relabel and the fp64 partial sums
+    # are all-reduced asynchronously (the expert cost is the bonus_mmd log's term),
+    # waited for (GPU-side) only before the next relabel overwrites the sum
+    shard = world > 1 and args.cost == "mmd"
+    if shard:
+        cost.shard_expert(rank, world, allreduce_async)
+
     def one_rollout():
         eng.rollout(T)
         eng.relabel(allreduce)  # MMD: feature mean -> w -> rewards (GAIL: rewards already scored)
-        if args.cost == "mmd":
+        if shard:
+            cost.expert_allreduce()
+        elif args.cost == "mmd":
             cost.get_expert_cost()
         return T * B
 
@@ -297,15 +306,16 @@ def main():
     # relabel timed).  Off by default: a trainer's policy update sits between two iterations'
     # rollouts, so the headline keeps the serial rollout -> all-reduce -> relabel order.
     overlap = world > 1 and args.cost == "mmd" and args.overlap == "on"
-    tail = cost.get_expert_cost if args.cost == "mmd" else None
+    tail = cost.get_expert_cost if args.cost == "mmd" and not shard else None
+    hooks = dict(before_relabel=cost.wait_expert_allreduce, after=cost.expert_allreduce) if shard else {}
     flush = eng.flush_relabel
     if use_graph:
         if overlap:
-            graph, flush = eng.graph_rollout_overlapped(T, allreduce_async, tail=tail)
+            graph, flush = eng.graph_rollout_overlapped(T, allreduce_async, tail=tail, **hooks)
             graph()  # warm replay
             flush()
         else:
-            graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail)
+            graph = eng.graph_rollout(T, allreduce=allreduce, tail=tail, **hooks)
             graph()  # warm replay
     torch.cuda.synchronize()
     if timer is not None:
@@ -320,7 +330,7 @@ def main():
     samples = 0
     if graph is None and overlap:
         for _ in range(args.steps):
-            samples += eng.rollout_overlapped(T, allreduce_async, tail=tail)
+            samples += eng.rollout_overlapped(T, allreduce_async, tail=cost.expert_allreduce if shard else tail)
         flush()
     elif graph is None:
         for _ in range(args.steps):
@@ -351,6 +361,8 @@ def main():
         gemm_ms = float(tv[2]) / 1e5  # 100 MHz ticks -> ms
         n_fwd = int(tv[3])
         ctx.gemm_timer(False)
+    shard_note = (f"; expert cost over {args.expert_rows}/{world} expert rows per rank, its fp64 sum all-reduced "
+                  f"off the critical path" if shard else "")
     per_fwd = ctx.L + 1  # GEMM launches per forward
     launches = n_fwd * per_fwd
     flops_per_fwd = ens.mlp_flops_per_sample() * B
@@ -402,6 +414,7 @@ def main():
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
                 "parallelism": (f"dp{world} (the {args.total_samples}-sample rollout's lanes sharded over the "
                                 f"ranks, 1 all-reduce of [sum phi, count] per rollout"
+                                f"{shard_note}"
                                 f"{', overlapped with the next rollout' + chr(39) + 's first forward' if overlap else ''})"
                                 if strong else
                                 f"dp{world} (lane-sharded, {args.samples_per_gpu} samples per rank, 1 all-reduce "

@@ -71,6 +71,8 @@ def main():
 
     def engine(seed):
         cost = amx.RBFLinearCost(expert, feature_dim=512, bw_quantile=0.1, lambda_b=0.0025, seed=100, ctx=ctx)
+        if world > 1:  # each rank scores its block of the expert rows; the partial sums all-reduced
+            cost.shard_expert(rank, world, allreduce_async)
         pol = amx.DevicePolicy(ctx, pw, ls, seed=D.rank_seed(5, rank))
         return amx.RolloutEngine(ens, table, lanes=B, term=term, policy=pol, cost=cost, seed=D.rank_seed(seed, rank),
                                  max_steps=K), cost
@@ -95,10 +97,16 @@ def main():
             e.reset_all()
         e1.rollout(); e1.relabel(allreduce); c1.get_expert_cost()
         e2.rollout(); e2.relabel(allreduce); c2.get_expert_cost()
-        replay = e2.graph_rollout(K, allreduce=allreduce, tail=c2.get_expert_cost)
+
+        def graph_args(c_):  # sharded expert cost: its all-reduce around the relabel graph
+            if c_.expert_sharded:
+                return dict(tail=None, before_relabel=c_.wait_expert_allreduce, after=c_.expert_allreduce)
+            return dict(tail=c_.get_expert_cost)
+        replay = e2.graph_rollout(K, allreduce=allreduce, **graph_args(c2))
         for _ in range(2):
             e1.rollout(); e1.relabel(allreduce); c1.get_expert_cost()
             replay()
+        c2.get_expert_cost()
         # the overlapped forms (each all-reduce under the next rollout's first forward, its
         # relabel after that forward; flush_relabel / flush for the last one), eager and graph
         e3, c3 = engine(9)
@@ -106,12 +114,15 @@ def main():
         for e, c_ in ((e3, c3), (e4, c4)):
             e.reset_all()
             e.rollout(); e.relabel(allreduce); c_.get_expert_cost()
-        replay4, flush4 = e4.graph_rollout_overlapped(K, allreduce_async, tail=c4.get_expert_cost)
+        replay4, flush4 = e4.graph_rollout_overlapped(K, allreduce_async, **graph_args(c4))
         for _ in range(2):
-            e3.rollout_overlapped(K, allreduce_async, tail=c3.get_expert_cost)
+            e3.rollout_overlapped(K, allreduce_async,
+                                  tail=c3.expert_allreduce if c3.expert_sharded else c3.get_expert_cost)
             replay4()
         e3.flush_relabel()
         flush4()
+        c3.get_expert_cost()
+        c4.get_expert_cost()
         torch.cuda.synchronize()
         res.update(ovl_rewards=e3.rewards[:K, :B].cpu().numpy(), ovl_mmd=float(e3.mb_mmd.item()),
                    ovl_obs=e3.obs.cpu().numpy(), ovl_expert=float(c3._expert_mean.item()),
