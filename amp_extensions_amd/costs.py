@@ -112,6 +112,7 @@ class RBFLinearCost:
         self._elo, self._ehi = 0, self.n_expert
         self._ear = None   # allreduce_async of the sharded partial sum (None: one rank, whole buffer)
         self._eh = None    # the pending all-reduce handle of the last sharded partial sum
+        self._estate = "global"  # sharded sum in _expert_out[0]: "partial" (this rank's) or "global"
         self._escale = torch.tensor([1.0 - lambda_b], dtype=torch.float32, device=ctx.device)
 
     # linear_cost.py:73-82
@@ -160,13 +161,22 @@ class RBFLinearCost:
         return self._ear is not None
 
     def expert_allreduce(self):
-        """Issue the all-reduce of the last relabel's partial expert sum (sharded mode; no-op
-        otherwise); returns the handle (the next relabel waits for it, GPU-side, before it
-        overwrites the sum)."""
-        if self._ear is None or not self._expert_fresh:
+        """Issue the all-reduce of the last relabel's partial expert sum (sharded mode, once per
+        partial sum; no-op otherwise); returns the handle (the next relabel waits for it,
+        GPU-side, before it overwrites the sum)."""
+        if self._ear is None or not self._expert_fresh or self._estate != "partial":
             return None
         self._eh = self._ear(self._expert_out[:1])
+        self._estate = "global"
         return self._eh
+
+    def expert_allreduce_replayed(self):
+        """expert_allreduce after a replayed graph whose relabel wrote a new partial sum (the
+        graph's `after` hook: the captured launch does not pass through relabel_device)."""
+        if self._ear is None or self.cost_range is None:
+            return None
+        self._expert_fresh, self._estate = True, "partial"
+        return self.expert_allreduce()
 
     def wait_expert_allreduce(self) -> None:
         """Queue the wait (GPU-side) for the pending expert-sum all-reduce (graph replays call it
@@ -202,6 +212,8 @@ class RBFLinearCost:
                                       eptr, self.expert_rep.stride(0), ne, self._expert_out.data_ptr(),
                                       emean, self._counter.data_ptr(), c.stream), "amx_mmd_relabel")
         self._expert_fresh = expert
+        if expert and self._ear is not None and not torch.cuda.is_current_stream_capturing():
+            self._estate = "partial"  # (a captured launch: expert_allreduce_replayed after each replay)
         return self._mmd
 
     def fit_w(self, phi_sum: torch.Tensor, count: float) -> float:
@@ -257,16 +269,15 @@ class RBFLinearCost:
         if self._expert_mean is None:
             self._expert_mean = torch.empty(1, dtype=torch.float32, device=c.device)
         if self._ear is not None:  # sharded: this rank's partial sum, all-reduced
-            if not self._expert_fresh or self._eh is None:
-                if not self._expert_fresh:
-                    self.wait_expert_allreduce()
-                    eptr, ne, _ = self._expert_args()
-                    N.check(c.lib.amx_expert_cost(c.h, eptr, self.expert_rep.stride(0), self.w.data_ptr(),
-                                                  self.feature_dim, ne, self.c_min, self.c_max,
-                                                  self._expert_out.data_ptr(), None, float(self.lambda_b),
-                                                  c.stream), "amx_expert_cost")
-                    self._expert_fresh = True
-                self.expert_allreduce()
+            if not self._expert_fresh:  # w changed since the last relabel: score this rank's block
+                self.wait_expert_allreduce()
+                eptr, ne, _ = self._expert_args()
+                N.check(c.lib.amx_expert_cost(c.h, eptr, self.expert_rep.stride(0), self.w.data_ptr(),
+                                              self.feature_dim, ne, self.c_min, self.c_max,
+                                              self._expert_out.data_ptr(), None, float(self.lambda_b),
+                                              c.stream), "amx_expert_cost")
+                self._expert_fresh, self._estate = True, "partial"
+            self.expert_allreduce()   # (no-op unless the sum is still this rank's partial)
             self.wait_expert_allreduce()
             # (1 - lambda) * float32(sum / n) as k_sum_small's mean_out (the fp32 product of torch)
             torch.mul((self._expert_out[:1] / self.n_expert).float(), self._escale, out=self._expert_mean)

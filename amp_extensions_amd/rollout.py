@@ -393,7 +393,7 @@ class RolloutEngine:
         lives on the device).  With `allreduce` (several ranks) the collective stays eager
         between two graphs; `before_relabel()` runs on the host right before the relabel's graph
         and `after()` after the last one (e.g. RBFLinearCost.wait_expert_allreduce /
-        expert_allreduce of a sharded expert cost).  Run one eager rollout first (workspaces
+        expert_allreduce_replayed of a sharded expert cost).  Run one eager rollout first (workspaces
         allocated, t == T)."""
         T = self.K if T is None else T
         if self.t != T:

@@ -307,7 +307,7 @@ def main():
     # rollouts, so the headline keeps the serial rollout -> all-reduce -> relabel order.
     overlap = world > 1 and args.cost == "mmd" and args.overlap == "on"
     tail = cost.get_expert_cost if args.cost == "mmd" and not shard else None
-    hooks = dict(before_relabel=cost.wait_expert_allreduce, after=cost.expert_allreduce) if shard else {}
+    hooks = dict(before_relabel=cost.wait_expert_allreduce, after=cost.expert_allreduce_replayed) if shard else {}
     flush = eng.flush_relabel
     if use_graph:
         if overlap:

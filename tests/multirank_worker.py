@@ -88,7 +88,8 @@ def main():
     mmd = float(info["mb_mmd"].item())
     res = dict(lo=lo, hi=hi, mb_mmd=mmd, rewards=eng.rewards[:K, :B].cpu().numpy(),
                next_obs=eng.next_obs.cpu().numpy(), done=eng.done.cpu().numpy(),
-               phi_sum=eng.phi_sum.cpu().numpy(), expert_cost=float(cost.get_expert_cost().item()))
+               phi_sum=eng.phi_sum.cpu().numpy(), expert_cost=float(cost.get_expert_cost().item()),
+               expert_cost_again=float(cost.get_expert_cost().item()))  # read twice: one all-reduce
     # ---- HIP-graph replay of whole rollouts (two graphs around the all-reduce) vs eager -----
     if world > 1 or os.environ.get("AMX_GRAPH_SINGLE") == "1":
         e1, c1 = engine(9)
@@ -100,7 +101,7 @@ def main():
 
         def graph_args(c_):  # sharded expert cost: its all-reduce around the relabel graph
             if c_.expert_sharded:
-                return dict(tail=None, before_relabel=c_.wait_expert_allreduce, after=c_.expert_allreduce)
+                return dict(tail=None, before_relabel=c_.wait_expert_allreduce, after=c_.expert_allreduce_replayed)
             return dict(tail=c_.get_expert_cost)
         replay = e2.graph_rollout(K, allreduce=allreduce, **graph_args(c2))
         for _ in range(2):
