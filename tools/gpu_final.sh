@@ -13,9 +13,14 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke_$TAG.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.log 2>&1 || { echo "bench FAILED"; tail -20 gpurun_out/bench_$TAG.log; exit 1; }
 tail -1 gpurun_out/bench_$TAG.log | cut -c1-140
-for n in 20000 10000 5000; do
+# per-rank shares of the strong-scaling runs (40000/N samples; with --expert-rows 50000/N the
+# rank's sharded expert block, the serial all-reduce aside)
+for spec in 20000:25000 10000:12500 5000:6250; do
+  n=${spec%%:*}; e=${spec##*:}
   timeout -k 10 200 python bench.py --no-cpu-baseline --total-samples $n > gpurun_out/bench_${TAG}_$n.log 2>&1 || { echo "bench $n FAILED"; tail -20 gpurun_out/bench_${TAG}_$n.log; exit 1; }
   tail -1 gpurun_out/bench_${TAG}_$n.log | cut -c1-140
+  timeout -k 10 200 python bench.py --no-cpu-baseline --total-samples $n --expert-rows $e > gpurun_out/bench_${TAG}_${n}_e$e.log 2>&1 || { echo "bench $n/$e FAILED"; tail -20 gpurun_out/bench_${TAG}_${n}_e$e.log; exit 1; }
+  tail -1 gpurun_out/bench_${TAG}_${n}_e$e.log | cut -c1-140
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_8k" -o run --output-format csv -- python "$R/bench.py" --no-cpu-baseline --steps 5 --warmup 2 > "$R/gpurun_out/prof_${TAG}_8k.log" 2>&1 || { echo "rocprof failed"; tail -5 "$R/gpurun_out/prof_${TAG}_8k.log"; exit 1; }
