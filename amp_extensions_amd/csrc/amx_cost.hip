@@ -459,6 +459,15 @@ extern "C" int amx_mmd_reward_raw(amx_ctx* ctx, const float* phi, int ldphi, con
   return mmd_reward(false, ctx, phi, ldphi, w, F, disc, 1.0f, lambda_b, 0.f, 0.f, reward, ipm, wbonus, n, stream);
 }
 
+// Blocks of the expert-cost reduction over n rows (k_expert_cost and k_mmd_relabel share it, so
+// both sum the same block partials in the same order): 16 rows per block (4 waves x one batch),
+// at most 1024 blocks (grid-stride beyond: 50 000 rows -> 1024 blocks; a rank's 6 250-row shard
+// -> 391 instead of 1024 blocks of mostly idle waves).
+static int expert_blocks(int n) {
+  const int b = (n + 15) / 16;
+  return b < 1024 ? (b > 0 ? b : 1) : 1024;
+}
+
 extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi, const float* w, int F, int n,
                                float c_min, float c_max, double* out, float* mean_out, double lambda_b,
                                void* stream) {
@@ -466,7 +475,7 @@ extern "C" int amx_expert_cost(amx_ctx* ctx, const float* phi_e_rows, int ldphi,
   AMX_CHECK_ARG(F > 0 && F % 256 == 0 && ldphi >= F && ldphi % 4 == 0, "amx_expert_cost: F=%d ldphi=%d", F, ldphi);
   AMX_CHECK_ARG(n > 0, "amx_expert_cost: n=%d", n);
   // partials live in out[1 .. nb]; out must hold 1 + 1024 doubles
-  const int nb = (n + 3) / 4 < 1024 ? (n + 3) / 4 : 1024;
+  const int nb = expert_blocks(n);
   hipLaunchKernelGGL(k_expert_cost, dim3(nb), dim3(256), 0, (hipStream_t)stream, phi_e_rows, ldphi, w, F, n, c_min,
                      c_max, out + 1);
   AMX_CHECK_LAUNCH();
@@ -563,7 +572,7 @@ extern "C" int amx_mmd_relabel(amx_ctx* ctx, const double* msg, double count, co
   a.one_m_lambda = (float)(1.0 - lambda_b); a.lambda_b = (float)lambda_b; a.c_min = c_min; a.c_max = c_max;
   a.reward = reward; a.ipm = ipm; a.wb = wbonus; a.n = n;
   a.erows = expert_rows; a.lde = ld_e; a.ne_rows = expert_rows ? n_e : 0;
-  a.ne = expert_rows ? ((n_e + 3) / 4 < 1024 ? (n_e + 3) / 4 : 1024) : 0;
+  a.ne = expert_rows ? expert_blocks(n_e) : 0;
   a.eout = expert_out; a.emean = expert_mean; a.escale = (float)(1.0 - lambda_b); a.counter = counter;
   const size_t lds = (size_t)F * sizeof(float);
   hipStream_t st = (hipStream_t)stream;

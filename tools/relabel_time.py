@@ -12,17 +12,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import amp_extensions_amd as amx
 from amp_extensions_amd import _native as N
 
-F, NE = 512, 50000
+F = 512
 ctx = amx.AmxContext(197, 36, n_models=4, hidden=512, n_hidden=4, feat_dim=F, device="cuda")
 lib, h, s = ctx.lib, ctx.h, ctx.stream
 g = torch.Generator(device="cpu").manual_seed(0)
 sc = (2.0 / F) ** 0.5
-erows = (torch.cos(torch.rand(NE, F, generator=g) * 6.3) * sc).cuda()
-phi_e = erows.double().mean(0).float()
+erows_all = (torch.cos(torch.rand(50000, F, generator=g) * 6.3) * sc).cuda()
 counter = torch.zeros(4, dtype=torch.int32, device="cuda")
 eo = torch.zeros(1025, dtype=torch.float64, device="cuda")
 em = torch.zeros(1, dtype=torch.float32, device="cuda")
-for n in (40960, 5120):
+for n, NE in ((40960, 50000), (5120, 50000), (5120, 6250), (10240, 12500)):
+    erows = erows_all[:NE]
+    phi_e = erows.double().mean(0).float()
     phi = (torch.cos(torch.rand(n, F, generator=g) * 6.3) * sc).cuda()
     disc = torch.rand(n, generator=g).cuda() * 0.1
     msg = torch.cat([phi.double().sum(0), torch.tensor([float(n)], dtype=torch.float64, device="cuda")])
@@ -46,4 +47,4 @@ for n in (40960, 5120):
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / reps
     byts = 4 * F * (n + NE) + 16 * n
-    print(f"rollout rows {n:6d} + expert rows {NE}: {us:7.2f} us/launch, {byts / us / 1e6:6.2f} TB/s algorithmic")
+    print(f"rollout rows {n:6d} + expert rows {NE:5d}: {us:7.2f} us/launch, {byts / us / 1e6:6.2f} TB/s algorithmic")
