@@ -1234,6 +1234,7 @@ using H128x64k32 = TileH3<4, 1, 1, 2, 2, 2>;
 using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
 using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true, true>;  // + DEEPA (-2 %)
 
+
 using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
 using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 
