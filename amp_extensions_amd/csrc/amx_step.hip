@@ -414,6 +414,7 @@ __global__ __launch_bounds__(256) void k_reset(const uint8_t* __restrict__ mask,
 // takes one Philox block and one Box-Muller per (lane, action pair): both normals of the pair.
 constexpr int POL_LANES = 16;
 constexpr int POL_MAXH = 256;
+constexpr int POL_X0_COLS = 320;  // fused assembly: k0_pad (= S + A rounded up to 32) at most this
 
 __host__ __device__ inline int pol_stride(int k) {  // row stride (floats) for a [*, k] LDS matrix
   const int r = (k + 3) & ~3;
@@ -643,44 +644,65 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   }
   if (!p.x0) return;
   __syncthreads();
-  // fused amx_assemble_input[_rexp] (dynamics.py:225-227), one wave per row as k_assemble: the
-  // block's POL_LANES rows of x0 (once when stride_m is 0: the f16x3 GEMMs read every model's x0
-  // slice from model 0's rows, else for every model), and with row_exp slot 0 = the exponent of
-  // the row's max |x0| and slots 1..n_slots-1 reset, for every model
+  // fused amx_assemble_input[_rexp] (dynamics.py:225-227): 16 threads per row (one DPP row of
+  // the wave; columns c0 + 16q), the block's POL_LANES rows of x0 (once when stride_m is 0: the
+  // f16x3 GEMMs read every model's x0 slice from model 0's rows, else for every model), and
+  // with row_exp slot 0 = the exponent of the row's max |x0| and slots 1..n_slots-1 reset, for
+  // every model -- the same values and bits as k_assemble
   const float* mu_s = p.norm;
   const float* sd_s = p.norm + S;
   const float* mu_a = p.norm + 2 * S;
   const float* sd_a = p.norm + 2 * S + A;
   const int k0 = p.k0_pad;
-  const int lane = t & 63, wave = t >> 6;
   const int copies = p.stride_m == 0 ? 1 : p.M;
-  for (int ll = wave; ll < POL_LANES; ll += 256 / 64) {
-    const int bb = b0 + ll;
-    if (bb >= p.B) break;  // wave-uniform; rows only grow
-    uint32_t mx = 0;
-    for (int j = lane; j < k0; j += 64) {
+  const int ll = t >> 4, c0 = t & 15;  // 256 threads = the 16 rows x 16 column lanes
+  const int bb = b0 + ll;
+  const bool row_ok = bb < p.B;
+  // the normalizers of this thread's columns, loaded together (one round trip, not one per column)
+  constexpr int QT = POL_X0_COLS / 16;
+  float mu[QT], sd[QT];
+#pragma unroll
+  for (int q = 0; q < QT; ++q) {
+    const int j = c0 + 16 * q;
+    mu[q] = 0.f;
+    sd[q] = 1.f;
+    if (j < S) {
+      mu[q] = mu_s[j];
+      sd[q] = sd_s[j];
+    } else if (j < S + A) {
+      mu[q] = mu_a[j - S];
+      sd[q] = sd_a[j - S];
+    }
+  }
+  uint32_t mx = 0;
+  if (row_ok) {
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+      const int j = c0 + 16 * q;
+      if (j >= k0) break;
       float x = 0.f;
       if (j < S) {
-        x = (so[ll * s1 + j] - mu_s[j]) / sd_s[j];
+        x = (so[ll * s1 + j] - mu[q]) / sd[q];
       } else if (j < S + A) {
-        x = (xa_s[ll * A + j - S] - mu_a[j - S]) / sd_a[j - S];
+        x = (xa_s[ll * A + j - S] - mu[q]) / sd[q];
       }
       for (int mm = 0; mm < copies; ++mm) p.x0[mm * p.stride_m + (long long)bb * p.ldk + j] = x;
       const uint32_t bits = __float_as_uint(x) & 0x7fffffffu;
       mx = mx > bits ? mx : bits;
     }
-    if (p.row_exp == nullptr) continue;
+  }
+  if (p.row_exp == nullptr) return;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
-      mx = mx > o ? mx : o;
-    }
-    if (lane < p.n_slots) {
-      int e = (int)(mx >> 23) - 126;  // max|x0| < 2^e, clamped as the GEMM's exponents
-      e = e < -100 ? -100 : (e > 100 ? 100 : e);
-      const int v = lane == 0 ? e : -100;
-      for (int mm = 0; mm < p.M; ++mm) p.row_exp[mm * p.stride_rexp + lane * p.slot_stride + bb] = v;
-    }
+  for (int off = 8; off > 0; off >>= 1) {  // max over the row's 16 threads
+    const uint32_t o = (uint32_t)__shfl_xor((int)mx, off);
+    mx = mx > o ? mx : o;
+  }
+  if (!row_ok) return;
+  int e = (int)(mx >> 23) - 126;  // max|x0| < 2^e, clamped as the GEMM's exponents
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  for (int sl = c0; sl < p.n_slots; sl += 16) {
+    const int v = sl == 0 ? e : -100;
+    for (int mm = 0; mm < p.M; ++mm) p.row_exp[mm * p.stride_rexp + sl * p.slot_stride + bb] = v;
   }
 }
 
@@ -908,6 +930,8 @@ static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, 
   AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH && ctx->S <= POL_MAXH,
                 "amx_policy_act: S=%d H1=%d H2=%d A=%d (max %d)", ctx->S, H1, H2, ctx->A, POL_MAXH);
   AMX_CHECK_ARG(B >= 0, "amx_policy_act: B=%d", B);
+  AMX_CHECK_ARG(!x0_buf || ctx->k0_pad <= POL_X0_COLS, "amx_policy_act: fused assembly needs k0_pad <= %d (%d)",
+                POL_X0_COLS, ctx->k0_pad);
   AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
                             (ctx->M == 1 || stride_m == 0 || stride_m >= (long long)ldk * B)),
                 "amx_policy_act: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B");

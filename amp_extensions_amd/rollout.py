@@ -53,8 +53,8 @@ class RolloutEngine:
         self.auto_reset = auto_reset
         self.fuse_reset = True  # table resets run inside the step kernel (amx_step_reset)
         # f16x3: the policy launch writes the ensemble's x0 + row exponents (bit-identical, tested;
-        # off: 32.9 us vs 22.2 + 7.3 us for policy + separate assembly at 8192 lanes,
-        # profiles/r02_policy_ab.txt)
+        # off: with the MFMA policy and a 16-threads-per-row tail the fused launch takes 28-31 us
+        # against 21 + 7 us for policy + separate assembly, no gain; bench --fuse-assembly on)
         self.fuse_assembly = False
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
