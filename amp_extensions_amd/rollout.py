@@ -575,8 +575,18 @@ class RolloutEngine:
                                                                        out=torch.empty_like(adv))
         return out
 
-    def bonus_mmd(self) -> float:
-        """infos['bonus_mmd'] = mean(-rewards) - expert cost (batch_reinforce.py:169)."""
+    def bonus_mmd(self, allreduce=None) -> float:
+        """infos['bonus_mmd'] = mean(-rewards) - expert cost (batch_reinforce.py:169).
+        `allreduce` (lanes sharded over ranks, as for relabel): the mean over every rank's
+        samples, from one all-reduce of the fp64 [sum, count] pair (SURVEY §8(e)'s logging
+        scalars); the expert cost is already global (one rank's shard sum all-reduced, or
+        every rank scoring all expert rows)."""
         T, B = self.t, self.B
-        mean_cost = (-self.rewards[:T, :B]).double().mean()
+        cost = -self.rewards[:T, :B].double()
+        if allreduce is None:
+            mean_cost = cost.mean()
+        else:
+            m = torch.stack([cost.sum(), torch.full((), float(T * B), dtype=torch.float64, device=cost.device)])
+            allreduce(m)
+            mean_cost = m[0] / m[1]
         return float(mean_cost.item()) - float(self.cost.get_expert_cost().item())

@@ -89,7 +89,8 @@ def main():
     res = dict(lo=lo, hi=hi, mb_mmd=mmd, rewards=eng.rewards[:K, :B].cpu().numpy(),
                next_obs=eng.next_obs.cpu().numpy(), done=eng.done.cpu().numpy(),
                phi_sum=eng.phi_sum.cpu().numpy(), expert_cost=float(cost.get_expert_cost().item()),
-               expert_cost_again=float(cost.get_expert_cost().item()))  # read twice: one all-reduce
+               expert_cost_again=float(cost.get_expert_cost().item()),  # read twice: one all-reduce
+               bonus_mmd=eng.bonus_mmd(allreduce))  # global mean(-rewards) - expert cost
     # ---- HIP-graph replay of whole rollouts (two graphs around the all-reduce) vs eager -----
     if world > 1 or os.environ.get("AMX_GRAPH_SINGLE") == "1":
         e1, c1 = engine(9)

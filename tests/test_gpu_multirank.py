@@ -65,6 +65,7 @@ def test_two_ranks_match_one_process_over_the_union(tmp_path):
         np.testing.assert_allclose(r["phi_sum"], one["phi_sum"], rtol=1e-12)  # the all-reduced fp64 sums
         np.testing.assert_allclose(float(r["expert_cost"]), float(one["expert_cost"]), rtol=1e-6)
         assert float(r["expert_cost_again"]) == float(r["expert_cost"])
+        np.testing.assert_allclose(float(r["bonus_mmd"]), float(one["bonus_mmd"]), rtol=1e-6)
     assert ranks[0]["done"].any()  # the horizon-3 lanes reset inside the rollout
     # every rank holds the same global witness
     assert float(ranks[0]["mb_mmd"]) == float(ranks[1]["mb_mmd"])
