@@ -1,6 +1,6 @@
-// Internal building blocks shared by the GEMM launches (amx_gemm.hip) and the fused ensemble
-// forward (amx_ens.hip): vector types, GemmArgs, the XCD-aware tile map, and the f16x3 tile
-// family (fp32 as two scaled fp16 limbs, three MFMA products).
+// Internal building blocks of the GEMM launches (amx_gemm.hip): vector types, GemmArgs, the
+// XCD-aware tile map, and the f16x3 tile family (fp32 as two scaled fp16 limbs, three MFMA
+// products).
 #pragma once
 
 #include "amx_common.h"
