@@ -101,9 +101,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
   } else {  // EPI_RFF (128 x 128 or 128 x 64 tiles of 256 threads)
     static_assert(BM == 128 && (BN == 128 || BN == 64) && TL::NT == 256, "RFF epilogue tiles");
     // Stage the raw BM x BN tile through LDS, then one column per thread over BM / PARTS rows:
-    // coalesced phi rows, one (non-unrolled) cos call site instead of 64 inlined copies, and
-    // the fp64 column sum of the valid rows in fixed row order, the PARTS part sums added in
-    // part order (deterministic; 2 parts at BN 128, 4 at BN 64).
+    // coalesced phi rows, the cos of 8 rows in flight (unroll 8: 94-101 vs 102-112 us for the
+    // 40 960-row pass, same bits; full unrolling is slower), and the fp64 column sum of the
+    // valid rows in fixed row order, the PARTS part sums added in part order (deterministic;
+    // 2 parts at BN 128, 4 at BN 64).
     constexpr int CLD = BN + 4, PARTS = 256 / BN, PR = BM / PARTS;
     float* Cs = smem;  // [BM][CLD] (<= 67,584 B), reuses the stage buffers (last barrier passed)
 #pragma unroll
@@ -121,7 +122,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
     const float bv = a.bias[col];
     double csum = 0.0;
     float* Cg = a.C;
-#pragma unroll 2
+#pragma unroll 8
     for (int i = 0; i < PR; ++i) {
       const int r = part * PR + i;
       const int row = tm * BM + r;
