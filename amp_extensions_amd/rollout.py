@@ -36,6 +36,11 @@ from .humanoid import TerminationConfig
 from .policy import DevicePolicy
 
 
+# graph captures are "thread_local": in "global" mode a CUDA call made by ANY other thread during
+# the capture (an RCCL process group's watchdog polling its work events) can invalidate it; the
+# captured rollout itself only launches onto this thread's capture stream
+_CAPTURE_MODE = "thread_local"
+
 class RolloutEngine:
     def __init__(self, ensemble: DeviceEnsemble, reset_table, lanes: int, term: TerminationConfig | None = None,
                  policy: DevicePolicy | None = None, cost=None, seed: int = 0, max_steps: int = 16,
@@ -410,7 +415,7 @@ class RolloutEngine:
             self._capturing = True
             self._ctr_delta, self._ctr_folded = T, False
             try:
-                with torch.cuda.graph(graphs[0], stream=side):
+                with torch.cuda.graph(graphs[0], stream=side, capture_error_mode=_CAPTURE_MODE):
                     self.rollout(T)
                     if not self._ctr_folded:  # (the fused step kernel advances it itself)
                         N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), T, c.stream), "amx_counter_add")
@@ -421,7 +426,7 @@ class RolloutEngine:
                     if tail is not None and (allreduce is None or not mmd):
                         tail()
                 if mmd and allreduce is not None:
-                    with torch.cuda.graph(graphs[1], stream=side):
+                    with torch.cuda.graph(graphs[1], stream=side, capture_error_mode=_CAPTURE_MODE):
                         self.relabel_post()
                         if tail is not None:
                             tail()
@@ -503,10 +508,10 @@ class RolloutEngine:
             self._capturing = True
             self._ctr_delta, self._ctr_folded = T, False
             try:
-                with torch.cuda.graph(graphs[0], stream=side):
+                with torch.cuda.graph(graphs[0], stream=side, capture_error_mode=_CAPTURE_MODE):
                     self._rollout_begin()
                     front = self._step_front(None, None)
-                with torch.cuda.graph(graphs[1], stream=side):
+                with torch.cuda.graph(graphs[1], stream=side, capture_error_mode=_CAPTURE_MODE):
                     self.relabel_post(T)
                     if tail is not None:
                         tail()
@@ -517,7 +522,7 @@ class RolloutEngine:
                     if not self._ctr_folded:
                         N.check(c.lib.amx_counter_add(c.h, self.dev_step.data_ptr(), T, c.stream), "amx_counter_add")
                     self.relabel_pre()
-                with torch.cuda.graph(graphs[2], stream=side):
+                with torch.cuda.graph(graphs[2], stream=side, capture_error_mode=_CAPTURE_MODE):
                     self.relabel_post(T)
                     if tail is not None:
                         tail()
