@@ -44,6 +44,9 @@ struct Tile {
 };
 
 
+// LDS of the RFF epilogue: the staged BM x (BN + 4) f32 tile and BM row-validity flags
+constexpr size_t rff_epi_lds(int bm, int bn) { return ((size_t)bm * (bn + 4) + bm) * 4; }
+
 // ---- epilogue (shared by the f32 and the bf16x6 main loops: the 32x32 C/D register map
 // is dtype-independent on gfx950) ---------------------------------------------------------
 template <int EPI, class TL>
@@ -106,7 +109,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
     // valid rows in fixed row order, the PARTS part sums added in part order (deterministic;
     // 2 parts at BN 128, 4 at BN 64).
     constexpr int CLD = BN + 4, PARTS = 256 / BN, PR = BM / PARTS;
-    float* Cs = smem;  // [BM][CLD] (<= 67,584 B), reuses the stage buffers (last barrier passed)
+    float* Cs = smem;  // [BM][CLD] + BM row flags (rff_epi_lds), reuses the stage buffers (last barrier passed)
 #pragma unroll
     for (int n = 0; n < TN; ++n)
 #pragma unroll
@@ -116,6 +119,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
           const int r = wm * TM * 32 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
           Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
         }
+    // the tile's row validity (n_valid, row_mask) once per row, beside the staged tile: the
+    // column loop reads it from LDS (one broadcast per row) instead of a global load per row
+    int* vf = reinterpret_cast<int*>(smem + BM * CLD);
+    if (t < BM) {
+      const int row = tm * BM + t;
+      vf[t] = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
+    }
     __syncthreads();
     const int c = t & (BN - 1), part = t / BN;
     const int col = tn * BN + c;
@@ -129,8 +139,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
       const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
       Cg[(long long)row * a.ldc + col] = phi;
-      const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
-      csum += valid ? (double)phi : 0.0;
+      csum += vf[r] ? (double)phi : 0.0;
     }
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);  // [PARTS][BN]
@@ -600,6 +609,11 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           Cs[(lrow0 + m * 16 + 4 * lq + j) * CLD + wn * TL::WCOLS + n * 16 + lc] = acc[m][n][j];
+    int* vf = reinterpret_cast<int*>(Cs + 128 * CLD);  // row validity, as the 32x32 path's epilogue
+    if (threadIdx.x < 128) {
+      const int row = tm * 128 + threadIdx.x;
+      vf[threadIdx.x] = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
+    }
     __syncthreads();
     const int t = threadIdx.x, c = t & 127, half = t >> 7;
     const int col = tn * 128 + c;
@@ -612,8 +626,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
       const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
       a.C[(long long)row * a.ldc + col] = phi;
-      const bool valid = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
-      csum += valid ? (double)phi : 0.0;
+      csum += vf[r] ? (double)phi : 0.0;
     }
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);
@@ -1260,7 +1273,8 @@ int launch_nt(GemmArgs& a, hipStream_t stream) {
   a.tiles_n = a.N / TL::BN;
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
-  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_epi_lds(TL::BM, TL::BN)) ? rff_epi_lds(TL::BM, TL::BN) : TL::LDS;
+  hipLaunchKernelGGL((k_gemm_nt<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -1272,7 +1286,7 @@ int launch_x6(GemmArgs& a, hipStream_t stream) {
   const int nwg = a.tiles_m * a.tiles_n * a.groups;
   if (nwg == 0) return AMX_OK;
   // the RFF epilogue stages the 128x(128+4) f32 tile through LDS (67.6 KB)
-  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < 128 * 132 * 4) ? 128 * 132 * 4 : TL::LDS;
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_epi_lds(TL::BM, TL::BN)) ? rff_epi_lds(TL::BM, TL::BN) : TL::LDS;
   hipLaunchKernelGGL((k_gemm_x6<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
@@ -1285,8 +1299,7 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   const int tiles = a.tiles_m * a.tiles_n * a.groups;
   const int nwg = a.streamk ? a.streamk : tiles;  // stream-K: a.streamk workgroups
   if (tiles == 0) return AMX_OK;
-  constexpr size_t rff_lds = (size_t)TL::BM * (TL::BN + 4) * 4;  // the RFF epilogue's staged tile
-  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_lds) ? rff_lds : TL::LDS;
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_epi_lds(TL::BM, TL::BN)) ? rff_epi_lds(TL::BM, TL::BN) : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
