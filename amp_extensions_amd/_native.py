@@ -49,7 +49,7 @@ SIGNATURES = {
     "amx_set_motion": (c_int, [vp, vp, c_ll]),
     "amx_motion_duration": (c_dbl, [vp]),
     "amx_motion_states": (c_int, [vp, vp, c_int, c_int, vp, c_ll, vp]),
-    "amx_reset_lanes_motion": (c_int, [vp, vp, vp, c_u64, c_int, vp, vp, vp, vp, vp, vp, c_int, vp]),
+    "amx_reset_lanes_motion": (c_int, [vp, vp, vp, c_u64, c_dbl, c_int, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_amp_obs_size": (c_int, [vp]),
     "amx_state_amp_obs": (c_int, [vp, vp, vp, c_ll, c_int, c_int, vp, c_ll, vp]),
     "amx_motion_amp_obs": (c_int, [vp, vp, c_dbl, c_int, c_int, vp, c_ll, vp]),

@@ -213,7 +213,11 @@ class RBFLinearCost:
                                       emean, self._counter.data_ptr(), c.stream), "amx_mmd_relabel")
         self._expert_fresh = expert
         if expert and self._ear is not None and not torch.cuda.is_current_stream_capturing():
-            self._estate = "partial"  # (a captured launch: expert_allreduce_replayed after each replay)
+            # (a captured launch: expert_allreduce_replayed after each replay).  The partial sum's
+            # all-reduce is issued here, right behind the relabel, so every rank issues the same
+            # collective sequence whether or not it later reads get_expert_cost (which only waits)
+            self._estate = "partial"
+            self.expert_allreduce()
         return self._mmd
 
     def fit_w(self, phi_sum: torch.Tensor, count: float) -> float:

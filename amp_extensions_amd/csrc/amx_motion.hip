@@ -301,7 +301,9 @@ __device__ void motion_state(const MView& m, double time, int flags, double* __r
       viol = fmin(0.0, L.bp[j].y - ext - pad);
     }
   }
-  const double min_viol = wave_min(viol);
+  // reset_args['resolve'] = False (flags & 8) skips the lift (SceneSimChar.cpp:714-716); the
+  // flag is uniform over the wave, so the reduction is entered by every lane or by none
+  const double min_viol = (flags & 8) ? 0.0 : wave_min(viol);
   // ---- CtController::BuildStatePose / BuildStateVel ---------------------------------------------
   double p[7];
   for (int k = 0; k < 7; ++k) p[k] = L.pose[k];
@@ -668,10 +670,11 @@ __global__ __launch_bounds__(64) void k_motion_states(const double* __restrict__
 
 // SimEnv.reset on masked lanes with motion states: reset_count/model_idx/num_steps as in
 // k_reset (sim_env.py:277, 282-283); t = times[b] or uniform(0, duration) from
-// Philox(seed, lane, reset#) (np_random.uniform(low=0, high=time_max), :276).
+// Philox(seed, lane, reset#) (np_random.uniform(low=0, high=time_max), :276; time_max = the
+// clip length, or reset_args['time_max'] with custom_time, :77).
 __global__ __launch_bounds__(64) void k_reset_motion(const double* __restrict__ blob, const uint8_t* __restrict__ mask,
                                                      const double* __restrict__ times, uint32_t k0, uint32_t k1,
-                                                     int flags, const double* ob_src, double* ob_out,
+                                                     double tmax, int flags, const double* ob_src, double* ob_out,
                                                      int32_t* num_steps, int32_t* model_idx, int32_t* reset_count,
                                                      double* t_out, int S, int M, int B) {
   __shared__ MotionLds L;
@@ -691,7 +694,7 @@ __global__ __launch_bounds__(64) void k_reset_motion(const double* __restrict__ 
     t = times[b];
   } else {
     const amx::u32x4 r = amx::philox4x32_10({(uint32_t)b, (uint32_t)rc, 0u, amx::kTagMotion}, k0, k1);
-    t = 0.0 + (m.h[4] - 0.0) * amx::u53(r.x, r.y);
+    t = 0.0 + (tmax - 0.0) * amx::u53(r.x, r.y);
   }
   motion_state(m, t, flags, ob_out + (long long)b * S, L);
   if (tid == 0) {
@@ -767,14 +770,15 @@ extern "C" int amx_motion_states(amx_ctx* c, const double* times, int B, int fla
 }
 
 extern "C" int amx_reset_lanes_motion(amx_ctx* c, const uint8_t* mask, const double* times, uint64_t seed,
-                                      int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
+                                      double time_max, int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
                                       int32_t* model_idx, int32_t* reset_count, double* t_out, int B, void* stream) {
   AMX_CHECK_ARG(c && c->d_motion, "amx_reset_lanes_motion: no motion set (amx_set_motion)");
   AMX_CHECK_ARG(ob_out && num_steps && model_idx && reset_count && B >= 0, "amx_reset_lanes_motion: null pointer");
   AMX_CHECK_ARG(mask == nullptr || ob_src != nullptr, "amx_reset_lanes_motion: masked reset needs ob_src");
+  AMX_CHECK_ARG(time_max == time_max, "amx_reset_lanes_motion: time_max is NaN");
   if (B == 0) return AMX_OK;
   hipLaunchKernelGGL(k_reset_motion, dim3(B), dim3(64), 0, (hipStream_t)stream, c->d_motion, mask, times,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), flags, ob_src, ob_out, num_steps, model_idx,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), time_max > 0.0 ? time_max : c->motion_duration, flags, ob_src, ob_out, num_steps, model_idx,
                      reset_count, t_out, c->S, c->M, B);
   AMX_CHECK_LAUNCH();
   return AMX_OK;

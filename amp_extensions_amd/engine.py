@@ -45,6 +45,9 @@ class AmxContext:
         if not h:
             raise N.AmxNativeError("amx_create failed: " + self.lib.amx_last_error().decode())
         self.h = h
+        # device buffers registered with the context (split-K workspaces, timers): captured HIP
+        # graphs bake their pointers into kernel arguments, so none is ever freed before the context
+        self._retained = []
         k0, ldk, nout, kr = (N.C.c_int(), N.C.c_int(), N.C.c_int(), N.C.c_int())
         N.check(self.lib.amx_layout(h, N.C.byref(k0), N.C.byref(ldk), N.C.byref(nout), N.C.byref(kr)), "amx_layout")
         self.k0_pad, self.ldk, self.n_out_pad, self.k_rff_pad = k0.value, ldk.value, nout.value, kr.value
@@ -64,6 +67,9 @@ class AmxContext:
             N.check(self.lib.amx_set_gemm_timer(self.h, None), "amx_set_gemm_timer")
             return None
         self._timer = torch.zeros(4, dtype=torch.int64, device=self.device)
+        # graphs captured while an earlier timer was registered keep writing to it: every
+        # buffer ever handed to the context lives as long as the context
+        self._retained.append(self._timer)
         N.check(self.lib.amx_set_gemm_timer(self.h, self._timer.data_ptr()), "amx_set_gemm_timer")
         return self._timer
 
@@ -209,7 +215,9 @@ class DeviceEnsemble:
 
     def _ensure_split_workspace(self, Bp: int) -> None:
         """Register the output layer's split-K scratch with the context when Bp lanes split
-        (amx_split_workspace_floats > 0); the buffer only grows."""
+        (amx_split_workspace_floats > 0); the buffer only grows.  A replaced buffer stays
+        alive (AmxContext._retained): graphs captured before the growth still launch with its
+        pointers, and its self-resetting arrival counters are zero between launches."""
         c = self.ctx
         nc = N.C.c_int(0)
         floats = int(c.lib.amx_split_workspace_floats(c.h, c.M, Bp, N.C.byref(nc)))
@@ -223,6 +231,7 @@ class DeviceEnsemble:
         N.check(c.lib.amx_set_split_workspace(c.h, scratch.data_ptr(), floats, counters.data_ptr(), nc.value),
                 "amx_set_split_workspace")
         c._split_ws = (scratch, counters)
+        c._retained.append(c._split_ws)
 
     def forward_preds(self, ob: torch.Tensor, act: torch.Tensor, B: int | None = None,
                       assembled: bool = False, x0_ready: bool = False) -> torch.Tensor:

@@ -138,11 +138,12 @@ class ReferenceMotion:
     """A reference clip on the device; `states(t)` = SimEnv.reset's recorded state at t."""
 
     def __init__(self, ctx: AmxContext, character, motion, record_world_root_pos: bool = False,
-                 record_world_root_rot: bool = True, record_all_world: bool = False):
+                 record_world_root_rot: bool = True, record_all_world: bool = False, resolve: bool = True):
         """`character`/`motion`: file paths (DeepMimic JSON) or already-parsed dicts
         ({"Skeleton", "BodyDefs"} / {"Loop", "Frames"}).  The record flags come from the
         controller file (humanoid3d_rot_ctrl.txt: RecordWorldRootPos false,
-        RecordWorldRootRot true)."""
+        RecordWorldRootRot true); `resolve` is reset_args['resolve'] (False: no ground lift,
+        SceneSimChar.cpp:714-716)."""
         if isinstance(character, str):
             character = json.load(open(character))
         if isinstance(motion, str):
@@ -156,6 +157,7 @@ class ReferenceMotion:
         times, frames, vels = preprocess_frames(raw, jt)
         self.blob = build_blob(jt, bt, times, frames, vels, self.loop)
         self.flags = int(record_world_root_pos) | (int(record_world_root_rot) << 1) | (int(record_all_world) << 2)
+        self.resolve = bool(resolve)
         N.check(ctx.lib.amx_set_motion(ctx.h, self.blob.ctypes.data, self.blob.size), "amx_set_motion")
         self.duration = float(times[-1])
         self.S = ctx.S
@@ -170,6 +172,11 @@ class ReferenceMotion:
             character = json.loads(str(z["character_json"]))
             motion = {"Loop": str(z["loop"]), "Frames": z["frames"].tolist()}
         return cls(ctx, character, motion, **flags)
+
+    @property
+    def kernel_flags(self) -> int:
+        """The record flags + bit 3 (no ground resolve) as amx_motion_states takes them."""
+        return self.flags | (0 if self.resolve else 8)
 
     @property
     def amp_obs_size(self) -> int:
@@ -213,6 +220,7 @@ class ReferenceMotion:
         c = self.ctx
         t = torch.as_tensor(times, dtype=torch.float64).reshape(-1).to(c.device).contiguous()
         out = torch.empty(t.numel(), self.S, dtype=torch.float64, device=c.device)
-        N.check(c.lib.amx_motion_states(c.h, t.data_ptr(), t.numel(), self.flags, out.data_ptr(), self.S, c.stream),
+        N.check(c.lib.amx_motion_states(c.h, t.data_ptr(), t.numel(), self.kernel_flags, out.data_ptr(), self.S,
+                                        c.stream),
                 "amx_motion_states")
         return out

@@ -65,6 +65,9 @@ class RolloutEngine:
         dev = c.device
         from .motion import ReferenceMotion
         self.motion = reset_table if isinstance(reset_table, ReferenceMotion) else None
+        # motion resets draw t ~ U(0, reset_time_max) (sim_env.py:276); 0 = the clip length (:77),
+        # reset_args['time_max'] with custom_time
+        self.reset_time_max = 0.0
         self.table = None
         if self.motion is None:
             table = torch.as_tensor(reset_table, dtype=torch.float64)
@@ -148,7 +151,8 @@ class RolloutEngine:
         c = self.ctx
         N.check(c.lib.amx_reset_lanes_motion(c.h, None if mask is None else mask.data_ptr(),
                                              None if times is None else times.data_ptr(), self.seed,
-                                             self.motion.flags, src.data_ptr(), dst.data_ptr(),
+                                             float(self.reset_time_max), self.motion.kernel_flags,
+                                             src.data_ptr(), dst.data_ptr(),
                                              self.num_steps.data_ptr(), self.model_idx.data_ptr(),
                                              self.reset_count.data_ptr(), None if t_out is None else t_out.data_ptr(),
                                              self.B, c.stream), "amx_reset_lanes_motion")
@@ -566,6 +570,7 @@ class RolloutEngine:
         `whiten` applies process_paths' (adv - mean) / (std + eps) (batch_reinforce.py:284-285).
         All outputs are device tensors [T, B] (values f32, returns/advantages f64)."""
         from .gae import gae_grid, whiten_grid
+        self.flush_relabel()  # the rewards of a relabel rollout_overlapped left pending
         c, T, B = self.ctx, self.t, self.B
         rows = T * B
         obs = self.obs[:T].reshape(rows, c.S)
@@ -585,7 +590,9 @@ class RolloutEngine:
         `allreduce` (lanes sharded over ranks, as for relabel): the mean over every rank's
         samples, from one all-reduce of the fp64 [sum, count] pair (SURVEY §8(e)'s logging
         scalars); the expert cost is already global (one rank's shard sum all-reduced, or
-        every rank scoring all expert rows)."""
+        every rank scoring all expert rows).  With `allreduce` every rank must call it (it is a
+        collective)."""
+        self.flush_relabel()  # the rewards of a relabel rollout_overlapped left pending
         T, B = self.t, self.B
         cost = -self.rewards[:T, :B].double()
         if allreduce is None:

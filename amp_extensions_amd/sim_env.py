@@ -33,29 +33,65 @@ class Box:
         self.shape, self.dtype = self.low.shape, np.dtype(dtype)
 
 
+# SimEnv's reset_args default (gym-simenv/gym_simenv/envs/sim_env.py:29-32; run.py:113-117 builds
+# the same keys from milo/milo/arguments.py:26-43)
+DEFAULT_RESET_ARGS = {'custom_time': False, 'time_min': 0, 'time_max': 0, 'resolve': True, 'noise_bef_rot': False,
+                      'noise_min': 0, 'noise_max': 0, 'radian': 0, 'rot_vel_w_pose': False, 'vel_noise': False,
+                      'interp': False, 'knee_rot': False}
+
+
+def parse_deepmimic_args(path: str) -> dict:
+    """DeepMimic's ArgParser.load_file (deepmimic/deepmimic/util/arg_parser.py:40-54, 14-38):
+    lines starting with '#' and '#' tokens are comments, '--key' opens a key, the first
+    occurrence of a key wins."""
+    table: dict = {}
+    key, vals = "", []
+    toks = []
+    with open(path) as f:
+        for line in f.read().splitlines():
+            if line and not line.startswith("#"):
+                toks += line.split()
+    for tok in toks:
+        if tok.startswith("#"):
+            continue
+        if tok.startswith("--"):
+            if key and key not in table:
+                table[key] = vals
+            key, vals = tok[2:], []
+        else:
+            vals.append(tok)
+    if key and key not in table:
+        table[key] = vals
+    return table
+
+
+def _resolve_data_path(p: str, args_path: str) -> str | None:
+    """DeepMimic opens the arg file's data paths relative to its working directory (the
+    deepmimic package root, the arg file's parent's parent): try the path as given, relative to
+    the arg file's directory and its parent, then relative to the current directory."""
+    base = os.path.dirname(os.path.abspath(args_path))
+    for cand in (p, os.path.join(base, p), os.path.join(os.path.dirname(base), p), os.path.join(os.getcwd(), p)):
+        if os.path.exists(cand):
+            return cand
+    return None
+
+
+def _arg_file(table: dict, key: str, args_path: str, required: bool = False) -> str | None:
+    val = table.get(key)
+    path = _resolve_data_path(val[0], args_path) if val else None
+    if required and path is None:
+        raise FileNotFoundError(f"{args_path}: --{key} {val[0] if val else '(missing)'} not found")
+    return path
+
+
 def termination_from_args(deepmimic_args: str | None, horizon: int, enable_velocity_check: bool) -> TerminationConfig:
     """Read the ctrl flags and BodyDefs the reference reads (sim_env.py:84-115) when the
     DeepMimic arg file is available; otherwise the humanoid3d spinkick defaults."""
     cfg = TerminationConfig(horizon=horizon, enable_velocity_check=enable_velocity_check)
     if not deepmimic_args or not os.path.exists(deepmimic_args):
         return cfg
-    args = {}
-    key = None
-    for tok in open(deepmimic_args).read().split():
-        if tok.startswith("--"):
-            key = tok[2:]
-            args[key] = []
-        elif key is not None:
-            args[key].append(tok)
-    base = os.path.dirname(os.path.abspath(deepmimic_args))
-
-    def _resolve(p):
-        for cand in (p, os.path.join(base, p), os.path.join(os.getcwd(), p)):
-            if os.path.exists(cand):
-                return cand
-        return None
-
-    ctrl = _resolve(args.get("char_ctrl_files", [""])[0]) if args.get("char_ctrl_files") else None
+    args = parse_deepmimic_args(deepmimic_args)
+    ctrl = _arg_file(args, "char_ctrl_files", deepmimic_args)
     if ctrl:
         cj = json.load(open(ctrl))
         cfg.record_vel_as_pos = bool(cj.get("RecordVelAsPos", False))
@@ -63,7 +99,7 @@ def termination_from_args(deepmimic_args: str | None, horizon: int, enable_veloc
         cfg.record_world_root_pos = bool(cj.get("RecordWorldRootPos", False))
         if "UpdateRate" in cj:
             cfg.sampling_rate = 1.0 / float(cj["UpdateRate"])
-    char = _resolve(args.get("character_files", [""])[0]) if args.get("character_files") else None
+    char = _arg_file(args, "character_files", deepmimic_args)
     if char:
         hj = json.load(open(char))
         defs = hj["BodyDefs"]
@@ -71,21 +107,72 @@ def termination_from_args(deepmimic_args: str | None, horizon: int, enable_veloc
     return cfg
 
 
-class SimEnv:
+def motion_from_args(ctx: AmxContext, deepmimic_args: str, resolve: bool = True):
+    """The reset source DeepMimicCore builds from the arg file (`--character_files`,
+    `--motion_file`, `--char_ctrl_files`; run_amp_humanoid3d_spinkick_args.txt:17,24,23): a
+    `ReferenceMotion` with the controller's record flags (sim_env.py:86-91)."""
+    from .motion import ReferenceMotion
+    if not deepmimic_args or not os.path.exists(deepmimic_args):
+        raise FileNotFoundError(f"DeepMimic arg file {deepmimic_args!r} not found")
+    args = parse_deepmimic_args(deepmimic_args)
+    char = _arg_file(args, "character_files", deepmimic_args, required=True)
+    motion = _arg_file(args, "motion_file", deepmimic_args, required=True)
+    ctrl = _arg_file(args, "char_ctrl_files", deepmimic_args)
+    cj = json.load(open(ctrl)) if ctrl else {}
+    return ReferenceMotion(ctx, char, motion, record_world_root_pos=bool(cj.get("RecordWorldRootPos", False)),
+                           record_world_root_rot=bool(cj.get("RecordWorldRootRot", False)),
+                           record_all_world=bool(cj.get("RecordAllWorld", False)), resolve=resolve)
+
+
+def check_reset_args(reset_args: dict | None) -> dict:
+    """reset_args with the reference's defaults filled in.  The noise options (noise_min /
+    noise_max, radian) draw from DeepMimicCore's C++ RNG in cKinCharacter::AddNoise
+    (anim/KinCharacter.cpp:340-400): that stream cannot be reproduced, so they are refused
+    rather than approximated.  `interp` and the flags that only shape the rotation noise
+    (rot_vel_w_pose, vel_noise, knee_rot, noise_bef_rot) act only inside RandomRotatePoseVel,
+    which returns before touching the state when radian == 0 (KinCharacter.cpp:360-364): with
+    the noise off they are exact no-ops, as in the reference."""
+    ra = dict(DEFAULT_RESET_ARGS)
+    ra.update(reset_args or {})
+    if float(ra["noise_min"]) != 0.0 or float(ra["noise_max"]) != 0.0 or float(ra["radian"]) != 0.0:
+        raise NotImplementedError(
+            "reset_args noise (noise_min/noise_max/radian) is drawn from DeepMimicCore's C++ RNG "
+            "(cKinCharacter::AddNoise, anim/KinCharacter.cpp:340-400), which cannot be reproduced on the device")
+    return ra
+
+
+try:  # gym is optional: register the drop-in under the reference's id when it is importable
+    import gym as _gym
+    _EnvBase = _gym.Env
+except Exception:  # pragma: no cover - gym is not installed in this image
+    _gym = None
+    _EnvBase = object
+
+
+class SimEnv(_EnvBase):
     """gym_simenv SimEnv (sim_env.py:13-288) on the HIP engine, one lane."""
 
     def __init__(self, dynamic_ensemble, deepmimic_args=None, enable_velocity_check=False, horizon=HORIZON,
                  device=None, seed=None, reset_args=None, reset_table=None):
-        """`reset_table`: a [R, S] reset-state table (row floor(t)), or a `ReferenceMotion`
-        (amp_extensions_amd.motion): the state at motion time t computed on the device as
-        DeepMimicCore's reset_time(t) builds it."""
-        if reset_table is None:
-            raise ValueError("SimEnv needs a reset source: a ReferenceMotion or a reset_table")
+        """Constructed as run.py:120 does (`gym.make('simenv-v0', deepmimic_args=...,
+        dynamic_ensemble=..., reset_args=...)`): the reset source is the arg file's character
+        and motion (DeepMimicCore's reset_time path restated on the device, motion.py).
+        `reset_table` (extension): a ReferenceMotion or a [R, S] reset-state table (row
+        floor(t); the synthetic benchmark layout) in place of the arg file's motion.
+        reset_args: custom_time / time_max set the reset-time window (sim_env.py:76-77),
+        resolve the ground lift; noise options raise NotImplementedError (check_reset_args)."""
+        self.reset_args = check_reset_args(reset_args)
         self.dynamic_ensemble = dynamic_ensemble
         dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
+        self.device = device
         self.enable_velocity_check = enable_velocity_check
         self.horizon = horizon
         self.term = termination_from_args(deepmimic_args, horizon, enable_velocity_check)
+        if reset_table is None:
+            if not deepmimic_args:
+                raise ValueError("SimEnv needs a reset source: deepmimic_args (character + motion files), "
+                                 "a ReferenceMotion or a reset_table")
+            reset_table = motion_from_args(dev_ens.ctx, deepmimic_args, resolve=bool(self.reset_args["resolve"]))
         self._eng = RolloutEngine(dev_ens, reset_table, lanes=1, term=self.term, seed=0, max_steps=1,
                                   auto_reset=False)
         c = self._eng.ctx
@@ -93,9 +180,15 @@ class SimEnv:
         self.observation_space = Box([-np.inf] * c.S, [np.inf] * c.S)
         self.action_space = Box([-np.inf] * c.A, [np.inf] * c.A)
         self.motion = self._eng.motion
-        # sim_env.py:77: time_max = the motion length (a table's length in rows otherwise)
-        self.time_max = self.motion.get_motion_length() if self.motion is not None else \
-            float(np.asarray(reset_table).shape[0])
+        if self.motion is not None and not self.reset_args["resolve"] and self.motion.resolve:
+            raise ValueError("reset_args['resolve'] is False but the ReferenceMotion resolves ground intersections")
+        # sim_env.py:76-77: the window is [0, time_max) (time_min is stored but reset ignores it,
+        # :276); time_max = the motion length (a table's length in rows) unless custom_time
+        n_src = self.motion.get_motion_length() if self.motion is not None else float(np.asarray(reset_table).shape[0])
+        self.time_min = self.reset_args["time_min"] if self.reset_args["custom_time"] else 0
+        self.time_max = float(self.reset_args["time_max"]) if self.reset_args["custom_time"] else n_src
+        if self.motion is None and self.time_max > n_src:
+            raise ValueError(f"reset_args time_max {self.time_max} exceeds the reset table's {int(n_src)} rows")
         self.ob = None
         self.num_steps = 0
         self.reset_counter = 0
@@ -168,11 +261,30 @@ class BatchedSimEnv:
     """B SimEnv lanes in lock-step (vectorised semantics, auto-reset)."""
 
     def __init__(self, dynamic_ensemble, reset_table, lanes: int, deepmimic_args=None, enable_velocity_check=False,
-                 horizon=HORIZON, seed: int = 0, policy=None, cost=None, max_steps: int = 32, record_means=False):
+                 horizon=HORIZON, seed: int = 0, policy=None, cost=None, max_steps: int = 32, record_means=False,
+                 reset_args=None):
+        """`reset_table` None: the arg file's character + motion (as SimEnv); reset_args as
+        SimEnv's (custom_time / time_max bound the lanes' Philox reset times, or the table rows
+        drawn; noise raises NotImplementedError)."""
+        self.reset_args = check_reset_args(reset_args)
         dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
         self.term = termination_from_args(deepmimic_args, horizon, enable_velocity_check)
+        if reset_table is None:
+            if not deepmimic_args:
+                raise ValueError("BatchedSimEnv needs a reset source: deepmimic_args, a ReferenceMotion or a table")
+            reset_table = motion_from_args(dev_ens.ctx, deepmimic_args, resolve=bool(self.reset_args["resolve"]))
+        custom = self.reset_args["custom_time"]
+        from .motion import ReferenceMotion
+        if custom and not isinstance(reset_table, ReferenceMotion):
+            rows = int(np.ceil(float(self.reset_args["time_max"])))
+            n = int(torch.as_tensor(reset_table).shape[0])
+            if not 0 < rows <= n:
+                raise ValueError(f"reset_args time_max {self.reset_args['time_max']} outside the table's {n} rows")
+            reset_table = torch.as_tensor(reset_table)[:rows]
         self.engine = RolloutEngine(dev_ens, reset_table, lanes=lanes, term=self.term, policy=policy, cost=cost,
                                     seed=seed, max_steps=max_steps, record_means=record_means)
+        if custom and self.engine.motion is not None:
+            self.engine.reset_time_max = float(self.reset_args["time_max"])
         self.num_envs = lanes
 
     def reset(self):
@@ -191,3 +303,10 @@ class BatchedSimEnv:
     @property
     def observations(self):
         return self.engine.obs[self.engine.t]
+
+
+if _gym is not None:  # gym-simenv/gym_simenv/__init__.py:3-6 (milo/milo/__init__.py:3-6)
+    try:
+        _gym.envs.registration.register(id="simenv-v0", entry_point="amp_extensions_amd.sim_env:SimEnv")
+    except Exception:  # already registered (e.g. by the reference's own gym_simenv package)
+        pass

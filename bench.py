@@ -11,8 +11,9 @@ buffer}.  Synthetic data of the BASELINE shape (obs 197, act 36; --faithful for 
 226/28 layout the reference scene actually builds) and random-init weights of the
 reference architecture.  Inputs are resident in HBM before timing starts.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run
-(one rank per GPU, RCCL).  Rank 0 prints ONE JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 either via torch.distributed.run
+(WORLD_SIZE set: it must equal --gpus) or directly, in which case bench.py starts the N rank
+processes itself (one per GPU, RCCL).  Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -96,6 +97,10 @@ def parse():
                         "only while consecutive rollouts share the policy: fixed-policy collection / evaluation; "
                         "a trainer updates the policy between iterations, so the default is the serial order)")
     p.add_argument("--motion", default=None, help="--cost amp: character + clip bundle (tools/pack_motion.py)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="print this rank's launch layout (rank, world, rendezvous) and exit before any GPU or "
+                        "CPU-baseline work (checks the --gpus N process launch)")
+    p.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return p.parse_args()
 
 
@@ -184,11 +189,75 @@ def plan_lanes(samples: int, max_lanes: int, lanes: int = 0):
     return best[1], best[2]
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: start N fresh rank processes of this script (one per GPU,
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on 127.0.0.1),
+    as the reference's sampler starts its worker pool inside the call
+    (milo/milo/sampler.py:111-121).  The parent never touches the GPU (no torch import, no HIP
+    call: the children are plain child processes, nothing is exec'ed over a GPU process); rank
+    0 prints the JSON line.  Returns the worst exit status."""
+    import signal
+    import subprocess
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+
+    def forward(sig, _frame):  # a launcher/timeout signalling the parent reaches the ranks too
+        for q in procs:
+            if q.poll() is None:
+                q.send_signal(sig)
+        raise SystemExit(128 + sig)
+    signal.signal(signal.SIGTERM, forward)
+    signal.signal(signal.SIGINT, forward)
+    rc = 0
+    try:
+        while [p.poll() for p in procs].count(None):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad and rc == 0:
+                rc = bad[0]
+                for q in procs:  # one rank failed: the others would wait in a collective forever
+                    if q.poll() is None:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+        if rc == 0:
+            rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} but --gpus {args.gpus}")
+    elif args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "pid": os.getpid(),
+                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
+              flush=True)
+        if rank == args.dry_run_fail_rank:
+            raise SystemExit(3)
+        if args.dry_run_fail_rank >= 0:
+            time.sleep(60)  # the launcher must stop the surviving ranks
+        return
     if args.cost == "amp":
         args.faithful = True   # the AMP features are defined on the humanoid3d CtController state
     S, A = (226, 28) if args.faithful else (197, 36)

@@ -211,15 +211,18 @@ int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, int K, const
  *   Requires S == 1 + 15 J (CtController pose + velocity layout, sim/CtController.cpp:305-319).
  * amx_motion_states: ob[b] = the state recorded after reset_time(times[b]) (motion pose and
  *   velocity at t, plane placement, ground resolve, CtController::BuildStatePose/Vel);
- *   flags: 1 RecordWorldRootPos, 2 RecordWorldRootRot, 4 RecordAllWorld.
+ *   flags: 1 RecordWorldRootPos, 2 RecordWorldRootRot, 4 RecordAllWorld, 8 no ground resolve
+ *   (reset_args['resolve'] = False: SceneSimChar::ResetSceneTime skips ResolveCharGroundIntersect,
+ *   deepmimic/deepmimic/DeepMimicCore/scenes/SceneSimChar.cpp:714-716).
  * amx_reset_lanes_motion: amx_reset_lanes with those states; t = times[b] or
- *   uniform(0, duration) from Philox(seed, lane, reset#) (sim_env.py:276); t_out nullable. */
+ *   uniform(0, time_max) from Philox(seed, lane, reset#) (sim_env.py:276); time_max <= 0 means the
+ *   clip length (sim_env.py:77; reset_args['time_max'] with custom_time); t_out nullable. */
 int amx_set_motion(amx_ctx* ctx, const double* blob, long long n);
 double amx_motion_duration(const amx_ctx* ctx);
 int amx_motion_states(amx_ctx* ctx, const double* times, int B, int flags, double* ob, long long ldo,
                       void* stream);
 int amx_reset_lanes_motion(amx_ctx* ctx, const uint8_t* mask, const double* times, uint64_t seed,
-                           int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
+                           double time_max, int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
                            int32_t* model_idx, int32_t* reset_count, double* t_out, int B, void* stream);
 
 /* AMP observation features (SceneImitateAMP::BuildAMPObs, deepmimic/deepmimic/DeepMimicCore/

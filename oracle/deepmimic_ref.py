@@ -319,8 +319,9 @@ def body_aabb_min_y(body, R, c):
 
 
 def reset_state(joints, bodies, motion, time, record_world_root_pos=False, record_world_root_rot=True,
-                record_all_world=False, ground_pad=0.001):
-    """The 226-d state SimEnv.reset records after reset_time(time)."""
+                record_all_world=False, ground_pad=0.001, resolve=True):
+    """The 226-d state SimEnv.reset records after reset_time(time); `resolve` = reset_args'
+    'resolve' (SceneSimChar::ResetSceneTime, scenes/SceneSimChar.cpp:714-716)."""
     pose = motion.pose(time)
     vel = motion.vel(time)
     pose[0] = 0.0   # SetCharRandPlacement on the plane: root x, z -> 0 (y kept)
@@ -329,7 +330,7 @@ def reset_state(joints, bodies, motion, time, record_world_root_pos=False, recor
     bpos = [o[j] + R[j] @ bodies[j]["attach"] for j in range(len(joints))]
     # ResolveCharGroundIntersect
     min_viol = 0.0
-    for j in range(len(joints)):
+    for j in range(len(joints) if resolve else 0):
         min_viol = min(min_viol, body_aabb_min_y(bodies[j], R[j], bpos[j]) - ground_pad)
     if min_viol < 0:
         pose[1] += -min_viol

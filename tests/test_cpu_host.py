@@ -206,3 +206,31 @@ def test_motion_bundle_matches_reference_data(golden):
         assert json.loads(str(z["character_json"])) == json.loads(str(g["character_json"]))
         np.testing.assert_array_equal(z["frames"], g["frames"])
         assert str(z["loop"]) == str(g["loop"])
+
+
+def test_deepmimic_arg_file_parsing_and_reset_args(tmp_path):
+    """SimEnv's host side of the run.py construction (sim_env.py:76-99): DeepMimic's ArgParser
+    rules (comment lines and tokens skipped, the first occurrence of a key wins, data paths
+    resolved from the package root), the ctrl flags and BodyDefs read into the termination
+    config, and reset_args: defaults filled in, noise refused (C++ RNG stream), interp and the
+    rotation-noise flags accepted as the no-ops they are with radian == 0."""
+    from amp_extensions_amd import sim_env as SE
+    from test_gpu_simenv_dropin import RUN_PY_RESET_ARGS, write_deepmimic_tree
+    args = write_deepmimic_tree(str(tmp_path))
+    table = SE.parse_deepmimic_args(args)
+    assert table["motion_file"] == ["data/motions/humanoid3d_spinkick.txt"]  # first occurrence wins
+    assert "model_files" not in table and table["time_lim_min"] == ["0.5"]
+    assert table["fall_contact_bodies"] == [str(i) for i in FALL_BODIES]
+    assert SE._arg_file(table, "motion_file", args) == os.path.join(str(tmp_path), "data/motions/humanoid3d_spinkick.txt")
+    cfg = SE.termination_from_args(args, 300, False)
+    assert cfg.record_world_root_pos is False and cfg.record_all_world is False
+    assert abs(cfg.sampling_rate - 1.0 / 30) < 1e-15 and len(cfg.body_defs) == 15
+    ra = SE.check_reset_args({"custom_time": True, "time_max": 0.5})
+    assert ra["resolve"] is True and ra["time_max"] == 0.5 and ra["radian"] == 0
+    assert SE.check_reset_args(RUN_PY_RESET_ARGS)["interp"] == 1.0
+    assert SE.check_reset_args(dict(RUN_PY_RESET_ARGS, vel_noise=True, knee_rot=True, interp=0.3))
+    for bad in ({"noise_max": 0.1}, {"noise_min": -0.1}, {"radian": 0.2}):
+        with pytest.raises(NotImplementedError):
+            SE.check_reset_args(dict(RUN_PY_RESET_ARGS, **bad))
+    with pytest.raises(FileNotFoundError):
+        SE.motion_from_args(None, str(tmp_path / "missing_args.txt"))

@@ -57,7 +57,7 @@ def test_reset_lanes_motion_draws_and_records(setup):
     mi = torch.zeros(L, dtype=torch.int32, device=DEV)
     rc = torch.zeros(L, dtype=torch.int32, device=DEV)
     tout = torch.zeros(L, dtype=torch.float64, device=DEV)
-    N.check(ctx.lib.amx_reset_lanes_motion(ctx.h, None, None, 1234, rm.flags, ob.data_ptr(), ob.data_ptr(),
+    N.check(ctx.lib.amx_reset_lanes_motion(ctx.h, None, None, 1234, 0.0, rm.flags, ob.data_ptr(), ob.data_ptr(),
                                            ns.data_ptr(), mi.data_ptr(), rc.data_ptr(), tout.data_ptr(), L,
                                            ctx.stream))
     t = tout.cpu().numpy()
