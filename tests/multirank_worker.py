@@ -21,7 +21,14 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-S, A, B_TOTAL, K, HORIZON = 197, 36, 512, 4, 3
+S, A = 197, 36
+# the shape: AMX_MR_LANES lanes in total over the ranks, AMX_MR_STEPS steps per rollout,
+# AMX_MR_EXPERT expert rows (default: a small case; the test also runs the N = 8 per-rank share,
+# 2 x 5120 lanes x 1 step with 12 500 expert rows -> 6 250 per rank)
+B_TOTAL = int(os.environ.get("AMX_MR_LANES", "512"))
+K = int(os.environ.get("AMX_MR_STEPS", "4"))
+N_EXPERT = int(os.environ.get("AMX_MR_EXPERT", "2048"))
+HORIZON = 3
 
 
 def main():
@@ -46,10 +53,23 @@ def main():
         def wait(self):
             pass
 
-    def allreduce_async(t):  # the overlapped path's handle (gloo: completed at once)
-        if allreduce is not None:
-            allreduce(t)
-        return _Done()
+    class _Pending:
+        """A real asynchronous gloo all-reduce of a host copy: wait() completes it and copies the
+        sum back on the current stream, so the GPU-side orderings the overlapped and sharded paths
+        rely on (wait before the relabel reads the message / overwrites the expert sum) are
+        exercised with the collective still in flight across the ranks."""
+
+        def __init__(self, t):
+            import torch.distributed as dist
+            self.t, self.h = t, t.cpu()
+            self.work = dist.all_reduce(self.h, async_op=True)
+
+        def wait(self):
+            self.work.wait()
+            self.t.copy_(self.h)
+
+    def allreduce_async(t):  # the overlapped path's handle
+        return _Pending(t) if allreduce is not None else _Done()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     s, a, s2 = syn.offline(4096, S, A, 0)
@@ -58,7 +78,7 @@ def main():
     ctx = amx.AmxContext(S, A, n_models=4, hidden=512, n_hidden=4, feat_dim=512, device=dev)
     ens = amx.DeviceEnsemble(ctx, init_ensemble_weights(S, A, [512] * 4, 4, 100), norms)
     ens.compute_threshold(torch.from_numpy(s).float().to(dev), torch.from_numpy(a).float().to(dev))
-    expert = torch.from_numpy(syn.expert(2048, S, 3))
+    expert = torch.from_numpy(syn.expert(N_EXPERT, S, 3))
     pw, ls = init_mlp_policy_params(S, A)
     table = syn.reset_table(1024, S, 1)
     lo, hi = D.shard(B_TOTAL, rank, world)

@@ -33,7 +33,7 @@ def _run(rank, world, port, out, env=None):
                              str(port), out], env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
 
 
-def _wait(procs, timeout=240):
+def _wait(procs, timeout=400):
     outs = []
     try:
         for p in procs:
@@ -47,26 +47,43 @@ def _wait(procs, timeout=240):
         assert p.returncode == 0, o[-4000:]
 
 
-def test_two_ranks_match_one_process_over_the_union(tmp_path):
+# (total lanes, steps, expert rows): a small case whose per-rank and union GEMM tiles are the same
+# (per-lane results bit-identical), and the N = 8 per-rank share (5120 lanes x 1 step, 6 250
+# expert rows per rank) whose union (10 240 lanes) runs other tiles than a rank's 5 120 (stream-K
+# output layer, 128 x 64 RFF tiles): there per-lane deltas agree to fp32 rounding
+SHAPES = [(512, 4, 2048), (10240, 1, 12500)]
+
+
+@pytest.mark.parametrize("lanes,steps,expert", SHAPES)
+def test_two_ranks_match_one_process_over_the_union(tmp_path, lanes, steps, expert):
+    env = dict(AMX_MR_LANES=str(lanes), AMX_MR_STEPS=str(steps), AMX_MR_EXPERT=str(expert))
     port = _free_port()
     outs = [str(tmp_path / f"rank{r}.npz") for r in range(2)]
-    _wait([_run(r, 2, port, outs[r]) for r in range(2)])
+    _wait([_run(r, 2, port, outs[r], env) for r in range(2)])
     single = str(tmp_path / "single.npz")
-    _wait([_run(0, 1, 0, single)])
+    _wait([_run(0, 1, 0, single, env)])
     ranks = [np.load(o) for o in outs]
     one = np.load(single)
+    exact = lanes == 512
     assert int(ranks[0]["hi"]) == int(ranks[1]["lo"]) and int(ranks[1]["hi"]) == one["rewards"].shape[1]
     for r in ranks:
         lo, hi = int(r["lo"]), int(r["hi"])
-        np.testing.assert_array_equal(r["next_obs"], one["next_obs"][:, lo:hi])
+        if exact:
+            np.testing.assert_array_equal(r["next_obs"], one["next_obs"][:, lo:hi])
+        else:
+            ref = one["next_obs"][:, lo:hi]
+            assert (np.abs(r["next_obs"] - ref) / np.maximum(1.0, np.abs(ref))).max() <= 2e-6
         np.testing.assert_array_equal(r["done"], one["done"][:, lo:hi])
-        np.testing.assert_allclose(r["rewards"], one["rewards"][:, lo:hi], rtol=1e-6, atol=1e-9)
-        np.testing.assert_allclose(float(r["mb_mmd"]), float(one["mb_mmd"]), rtol=1e-6)
-        np.testing.assert_allclose(r["phi_sum"], one["phi_sum"], rtol=1e-12)  # the all-reduced fp64 sums
-        np.testing.assert_allclose(float(r["expert_cost"]), float(one["expert_cost"]), rtol=1e-6)
+        np.testing.assert_allclose(r["rewards"], one["rewards"][:, lo:hi], rtol=1e-6 if exact else 1e-5,
+                                   atol=1e-9 if exact else 1e-7)
+        np.testing.assert_allclose(float(r["mb_mmd"]), float(one["mb_mmd"]), rtol=1e-6 if exact else 1e-5)
+        # the all-reduced fp64 sums
+        np.testing.assert_allclose(r["phi_sum"], one["phi_sum"], rtol=1e-12 if exact else 1e-6)
+        np.testing.assert_allclose(float(r["expert_cost"]), float(one["expert_cost"]), rtol=1e-6 if exact else 1e-5)
         assert float(r["expert_cost_again"]) == float(r["expert_cost"])
-        np.testing.assert_allclose(float(r["bonus_mmd"]), float(one["bonus_mmd"]), rtol=1e-6)
-    assert ranks[0]["done"].any()  # the horizon-3 lanes reset inside the rollout
+        np.testing.assert_allclose(float(r["bonus_mmd"]), float(one["bonus_mmd"]), rtol=1e-6 if exact else 1e-5)
+    if steps >= 3:
+        assert ranks[0]["done"].any()  # the horizon-3 lanes reset inside the rollout
     # every rank holds the same global witness
     assert float(ranks[0]["mb_mmd"]) == float(ranks[1]["mb_mmd"])
     # two-graph replay with the all-reduce between the graphs == eager rollout + relabel(allreduce)
