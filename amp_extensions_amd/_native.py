@@ -93,7 +93,10 @@ SIGNATURES = {
     "amx_gae": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, vp, vp, c_ll, vp, c_dbl, c_dbl, vp, vp, vp]),
     "amx_adv_whiten": (c_int, [vp, c_int, c_int, vp, vp, c_ll, vp, c_dbl, vp, vp, vp]),
     "amx_philox": (c_int, [vp, c_u64, c_u32, c_u32, c_u32, vp, c_int, vp]),
+    "amx_mt_seed": (c_int, [vp, c_int, vp, vp, c_int]),
+    "amx_mt_policy_noise": (c_int, [vp, c_int, vp, c_int, c_int, c_int, vp, c_ll, c_ll]),
 }
+AMX_MT_STATE_BYTES = 2512
 
 AMX_ROW_TILE = 128
 AMX_K_TILE = 32

@@ -9,23 +9,27 @@ policy's per-step draws (np.random.uniform() for the eps test, then randn(A)); t
 reset counter makes trajectory j run on ensemble member j mod M.  The result lists worker
 0's paths in order, then worker 1's, ...
 
-Here a worker's trajectories run concurrently on GPU lanes.  Trajectory j+1 of worker i is
-admitted to a free lane only while completed_i + R * in_flight_i < q (R = horizon, the longest
-a trajectory can run; 'trajectories' mode: count_i + in_flight_i < q).  An admitted j
-therefore has sum_{j' < j} len_j' < q, and admission continues until completed_i >= q with
-nothing in flight: the admitted set is exactly trajectories 1..n_i of the sequential
-reference, n_i = min{n : sum_{j <= n} len_j >= q}, whatever the lane timing.  With
-rng='reference' every trajectory's reset time and noise come from the reference's own seeds
-(host MT19937 / PCG64 draws, uploaded per chunk), so the output equals the reference's
-paths up to the ensemble's fp32 arithmetic; rng='device' draws them from Philox on the GPU
-(same structure and admission, different random streams, no host RNG work).
+Here a worker's trajectories run concurrently on GPU lanes.  Every trajectory is
+exact-seeded (its reset time, noise and ensemble member depend only on (i, j)), so they can
+run in any order and concurrency: trajectory j of worker i is admitted while the lengths its
+predecessors have reached so far sum to less than q (a lower bound on the sum that decides
+whether j is needed), dropped as soon as that bound reaches q, and the result is exactly
+trajectories 1..n_i of the sequential reference, n_i = min{n : sum_{j <= n} len_j >= q}
+('trajectories' mode: the first q).  How many run at once is set by an estimate of the
+lengths still to come (the horizon R: the reference's worst case; or, speculatively, the
+mean length of the trajectories ended so far), see _collect.  With rng='reference' every
+trajectory's reset time and noise come from the reference's own seeds (the PCG64 reset draw
+per trajectory; the MT19937 policy noise from per-lane generators in the HIP library's host
+code, amx_mt_policy_noise, uploaded per chunk), so the output equals the reference's paths up
+to the ensemble's fp32 arithmetic; rng='device' draws them from Philox on the GPU (same
+structure and admission, different random streams, no host RNG work).
 
-Lanes: W * ceil(q / R) lanes suffice for the admission rule (each in-flight trajectory
-reserves R samples), capped by the env's lane count.  Steps run in chunks of K synchronous
-steps between host decisions; a lane whose trajectory ends inside a chunk idles to its end.
-The transitions of in-flight lanes are compacted on the device after every chunk (index
-gather into a transition store) and the store is reordered into path order and copied to
-the host ONCE at the end; each path's arrays are views of that copy.
+Lanes: W * ceil(q / R) lanes suffice for the worst-case rule (x4 with speculation), capped by
+the env's lane count.  Steps run in chunks of K synchronous steps between host decisions,
+replayed as one captured HIP graph per chunk; a lane whose trajectory ends inside a chunk
+idles to its end.  The transitions of in-flight lanes are compacted on the device after every
+chunk (one index gather into a transition store) and the store is reordered into path order
+and copied to the host ONCE at the end; each path's arrays are views of that copy.
 """
 from __future__ import annotations
 
@@ -35,6 +39,7 @@ import time
 import numpy as np
 import torch
 
+from . import _native as N
 from .rollout import RolloutEngine
 from .sim_env import BatchedSimEnv
 
@@ -45,24 +50,14 @@ def _gym_np_random(seed: int) -> np.random.Generator:
 
 
 class _Traj:
-    __slots__ = ("worker", "j", "seed", "rs", "lane", "length", "segs")
+    __slots__ = ("worker", "j", "seed", "lane", "length", "ended", "segs")
 
     def __init__(self, worker: int, j: int, seed: int):
         self.worker, self.j, self.seed = worker, j, seed
-        self.rs = None
         self.lane = -1
-        self.length = 0
+        self.length = 0       # transitions so far (the final length once ended)
+        self.ended = False
         self.segs = []  # (store row, count) pieces in step order
-
-
-def _noise_block(rs: np.random.RandomState, K: int, A: int) -> np.ndarray:
-    """K steps of MLP.get_action's draws (gaussian_mlp.py:99-102): np.random.uniform() for the
-    eps test, then randn(A) -- in the legacy stream order of np.random.seed(s_ij)."""
-    out = np.empty((K, A))
-    for k in range(K):
-        rs.random_sample()
-        out[k] = rs.standard_normal(A)
-    return out
 
 
 class _Store:
@@ -111,100 +106,209 @@ def _sampler_engine(env, lanes: int, K: int, policy) -> RolloutEngine:
     return eng
 
 
-def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, rng: str, eval_mode: bool):
+class _HostNoise:
+    """Per-lane numpy-legacy MT19937 generators of the reference policy noise, advanced in the
+    HIP library's host code (amx_mt_seed / amx_mt_policy_noise: bit-exact with
+    np.random.seed(s); [np.random.uniform(); np.random.randn(A)] per step) into a pinned
+    [K, L, A] buffer, one call per chunk for all lanes in flight."""
+
+    def __init__(self, lib, L: int, K: int, A: int):
+        self.lib, self.L, self.K, self.A = lib, L, K, A
+        self.states = np.zeros((L, N.AMX_MT_STATE_BYTES), np.uint8)
+        self.host = torch.zeros(K, L, A, dtype=torch.float64, pin_memory=torch.cuda.is_available())
+
+    def seed(self, lanes: np.ndarray, seeds: np.ndarray) -> None:
+        sl = np.ascontiguousarray(lanes, np.int32)
+        sd = np.ascontiguousarray(np.asarray(seeds, np.int64) & 0xFFFFFFFF, np.uint32)
+        N.check(self.lib.amx_mt_seed(self.states.ctypes.data, self.L, sl.ctypes.data, sd.ctypes.data, sl.size),
+                "amx_mt_seed")
+
+    def draw(self, lanes: np.ndarray) -> torch.Tensor:
+        sl = np.ascontiguousarray(lanes, np.int32)
+        N.check(self.lib.amx_mt_policy_noise(self.states.ctypes.data, self.L, sl.ctypes.data, sl.size, self.K,
+                                             self.A, self.host.data_ptr(), self.L * self.A, self.A),
+                "amx_mt_policy_noise")
+        return self.host
+
+
+class _ChunkGraph:
+    """The K synchronous steps of a chunk captured once as a HIP graph (the lanes' resets and
+    the noise upload stay outside, on the same stream), so a chunk costs one replay instead of
+    ~8 launches per step from Python."""
+
+    def __init__(self, eng: RolloutEngine, K: int, noise_dev):
+        c = eng.ctx
+        self.eng, self.K = eng, K
+        self.g = torch.cuda.CUDAGraph()
+        if eng._graph_ahead:
+            eng.step_counter = int(eng.dev_step.item())
+        eng.dev_step.fill_(eng.step_counter)
+        side = torch.cuda.Stream(c.device)
+        side.wait_stream(torch.cuda.current_stream(c.device))
+        t0 = eng.t
+        with torch.cuda.stream(side):
+            eng._capturing = True
+            try:
+                with torch.cuda.graph(self.g, stream=side, capture_error_mode="thread_local"):
+                    for k in range(K):
+                        eng.step(noise=None if noise_dev is None else noise_dev[k])
+                    N.check(c.lib.amx_counter_add(c.h, eng.dev_step.data_ptr(), K, c.stream), "amx_counter_add")
+            finally:
+                eng._capturing = False
+        torch.cuda.current_stream(c.device).wait_stream(side)
+        eng.t, eng.step_counter = t0, eng.step_counter - K  # the captured steps did not run
+        eng._graph_ahead = True
+
+    def replay(self) -> None:
+        self.g.replay()
+        self.eng.t = self.K
+        self.eng.step_counter += self.K
+        self.eng._graph_ahead = True
+
+
+def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, rng: str, eval_mode: bool,
+             speculate: bool = True, graph: bool = True):
+    """Run the W workers' trajectory sequences on the engine's lanes (see the module notes).
+
+    Admission: a worker's trajectories are admitted in seed order j.  Trajectory j is needed iff
+    the exact lengths of 1..j-1 sum to less than the quota q; the lengths reached so far give a
+    lower bound LB_j of that sum, so j is admitted only while LB_j < q and an in-flight
+    trajectory whose LB_j >= q is provably not needed and is dropped (its lane freed).  Among
+    admissible trajectories the concurrency is capped by an estimate: sum over the admitted of
+    (final length, or max(length so far, L^)) < q, with L^ = the horizon R (speculate=False: the
+    reference's worst case, never wasted work) or the mean length of the trajectories ended so far
+    (speculate=True: short trajectories admit more at once; any surplus trajectory completes or is
+    dropped and never enters the result).  Each trajectory is exact-seeded, so its transitions do
+    not depend on when or on which lane it ran: the result is trajectories 1..n_i of every worker,
+    n_i = min{n : sum_{j <= n} len_j >= q}, for any admission order."""
     c = eng.ctx
     L, S, A, K, dev = eng.B, c.S, c.A, eng.K, c.device
     R = eng.term.horizon
-    reserve = R if mode == "samples" else 1
     motion = eng.motion
     time_max = motion.get_motion_length() if motion is not None else float(eng.table.shape[0])
-    st = [dict(next_j=1, completed=0, ntraj=0, inflight=0, done=[]) for _ in range(W)]
+    adm: list[list[_Traj]] = [[] for _ in range(W)]   # admitted trajectories, in j order
+    next_j = [1] * W
+    done_w = [False] * W
+    lane_tr: list[_Traj | None] = [None] * L
     free = list(range(L - 1, -1, -1))
-    active: dict[int, _Traj] = {}
     store = _Store(dev, S, A, W * (quota + R) if mode == "samples" else W * quota * 64)
     eng.eval_mode = eval_mode
-
-    def admissible(w: int) -> bool:
-        s = st[w]
-        have = s["completed"] if mode == "samples" else s["ntraj"]
-        return have + reserve * s["inflight"] < quota
-
-    noise_dev = torch.zeros(K, L, A, dtype=torch.float64, device=dev) if rng == "reference" else None
+    ref_noise = rng == "reference" and not eval_mode
+    hn = _HostNoise(c.lib, L, K, A) if ref_noise else None
+    noise_dev = torch.zeros(K, L, A, dtype=torch.float64, device=dev) if ref_noise else None
     mask_dev = torch.empty(L, dtype=torch.uint8, device=dev)
-    steps, budget = 0, (W * quota + W) * (R + K) + 16 * K
+    ended_sum, ended_n = 0, 0
+    chunk_graph = None
+    chunks, budget = 0, 4 * (W * quota + W) * (R + K) // K + 64
+
+    def drop(tr: _Traj) -> None:
+        if tr.lane >= 0:
+            lane_tr[tr.lane] = None
+            free.append(tr.lane)
+            tr.lane = -1
+
     while True:
-        # ---- admit trajectories to free lanes (round-robin over the workers) ----
+        # ---- per worker: drop the unneeded, detect completion, admit (round-robin) ----
+        lhat = (ended_sum / ended_n) if (speculate and ended_n >= 4) else float(R)
+        for w in range(W):
+            if done_w[w]:
+                continue
+            trs = adm[w]
+            if mode == "samples":
+                lb, cut = 0, len(trs)
+                for i, tr in enumerate(trs):
+                    if lb >= quota:
+                        cut = i
+                        break
+                    lb += tr.length
+                for tr in trs[cut:]:
+                    drop(tr)
+                del trs[cut:]
+                if trs and all(tr.ended for tr in trs) and sum(tr.length for tr in trs) >= quota:
+                    done_w[w] = True
+            elif len(trs) == quota and all(tr.ended for tr in trs):
+                done_w[w] = True
         new = []
         progress = True
         while free and progress:
             progress = False
             for w in range(W):
-                if free and admissible(w):
-                    s = st[w]
-                    tr = _Traj(w, s["next_j"], 12345 + base_seed * w + s["next_j"])
-                    s["next_j"] += 1
-                    s["inflight"] += 1
+                if not free or done_w[w]:
+                    continue
+                trs = adm[w]
+                if mode == "samples":
+                    lb = sum(tr.length for tr in trs)
+                    est = sum(tr.length if tr.ended else max(tr.length, lhat) for tr in trs)
+                    ok = lb < quota and est < quota
+                else:
+                    ok = len(trs) < quota
+                if ok:
+                    j = next_j[w]
+                    next_j[w] += 1
+                    tr = _Traj(w, j, 12345 + base_seed * w + j)
                     tr.lane = free.pop()
-                    active[tr.lane] = tr
+                    lane_tr[tr.lane] = tr
+                    trs.append(tr)
                     new.append(tr)
                     progress = True
-        if not active:
+        active = np.array([b for b in range(L) if lane_tr[b] is not None], np.int64)
+        if active.size == 0:
             break
-        if steps > budget:
+        chunks += 1
+        if chunks > budget:
             raise RuntimeError("sample_points: step budget exhausted (trajectories longer than the horizon?)")
         # ---- resets: the new trajectories (reset counter j-1 -> member j mod M) and the idle lanes ----
         eng.begin_rollout()
-        mask = np.zeros(L, np.uint8)
-        idle = [b for b in range(L) if b not in active]
-        mask[idle] = 1
+        mask = np.ones(L, np.uint8)
+        mask[active] = 0
         counts = np.zeros(L, np.int32)
         rows = np.zeros(L, np.float64 if motion is not None else np.int32)
+        new_lanes = np.array([tr.lane for tr in new], np.int64)
         for tr in new:
             mask[tr.lane] = 1
             counts[tr.lane] = tr.j - 1
             if rng == "reference":
                 t = _gym_np_random(tr.seed).uniform(low=0, high=time_max)  # seed_env + reset (sim_env.py:132,276)
                 rows[tr.lane] = t if motion is not None else int(np.floor(t))
-                tr.rs = np.random.RandomState(tr.seed)                   # np.random.seed (sampler.py:39)
-        if mask.any():
-            sel = torch.from_numpy(np.nonzero(mask)[0]).to(dev)
-            eng.reset_count.index_copy_(0, sel, torch.from_numpy(counts[mask != 0]).to(dev))
-            mask_dev.copy_(torch.from_numpy(mask))
-            rows_dev = torch.from_numpy(rows).to(dev) if rng == "reference" else None
-            eng.reset_lanes(mask_dev, rows_dev)
+        if hn is not None and new:
+            hn.seed(new_lanes, np.array([tr.seed for tr in new]))  # np.random.seed (sampler.py:39)
+        sel = torch.from_numpy(np.nonzero(mask)[0]).to(dev)
+        eng.reset_count.index_copy_(0, sel, torch.from_numpy(counts[mask != 0]).to(dev))
+        mask_dev.copy_(torch.from_numpy(mask))
+        rows_dev = torch.from_numpy(rows).to(dev) if rng == "reference" else None
+        eng.reset_lanes(mask_dev, rows_dev)
         # ---- K synchronous steps ----
-        if noise_dev is not None and not eval_mode:
-            nz = np.zeros((K, L, A))
-            for lane, tr in active.items():
-                nz[:, lane] = _noise_block(tr.rs, K, A)
-            noise_dev.copy_(torch.from_numpy(nz))
-        for k in range(K):
-            eng.step(noise=None if noise_dev is None else noise_dev[k])
-        steps += K
+        if hn is not None:
+            noise_dev.copy_(hn.draw(active), non_blocking=True)
+        if graph and chunk_graph is None and chunks >= 2:  # (the first chunk allocates the workspaces)
+            eng.begin_rollout()
+            chunk_graph = _ChunkGraph(eng, K, noise_dev)
+        if chunk_graph is not None:
+            chunk_graph.replay()
+        else:
+            for k in range(K):
+                eng.step(noise=None if noise_dev is None else noise_dev[k])
         done = eng.done[:K].cpu().numpy().astype(bool)  # [K, L]: the chunk's one host sync
-        # ---- compact the in-flight lanes' transitions into the store ----
-        idx, pieces = [], []
-        for lane, tr in active.items():
-            hit = np.nonzero(done[:, lane])[0]
-            n = int(hit[0]) + 1 if hit.size else K
-            idx.append(np.arange(n) * L + lane)
-            pieces.append((tr, n, bool(hit.size)))
-        flat = np.concatenate(idx)
+        # ---- compact the in-flight lanes' transitions into the store (vectorised) ----
+        d = done[:, active]
+        hit = d.any(axis=0)
+        n = np.where(hit, d.argmax(axis=0) + 1, K)
+        tot = int(n.sum())
+        starts = np.cumsum(n) - n
+        step_of = np.arange(tot) - np.repeat(starts, n)
+        flat = step_of * L + np.repeat(active, n)
         base = store.append(eng, K, torch.from_numpy(flat).to(dev))
-        for tr, n, ended in pieces:
-            tr.segs.append((base, n))
-            base += n
-            tr.length += n
-            if ended:
-                s = st[tr.worker]
-                s["inflight"] -= 1
-                s["completed"] += tr.length
-                s["ntraj"] += 1
-                s["done"].append(tr)
-                del active[tr.lane]
-                free.append(tr.lane)
+        for i, b in enumerate(active.tolist()):
+            tr = lane_tr[b]
+            tr.segs.append((base + int(starts[i]), int(n[i])))
+            tr.length += int(n[i])
+            if hit[i]:
+                tr.ended = True
+                ended_sum += tr.length
+                ended_n += 1
+                drop(tr)
     # ---- reorder into path order on the device, one copy to the host ----
-    trajs = [tr for s in st for tr in sorted(s["done"], key=lambda x: x.j)]
+    trajs = [tr for w in range(W) for tr in adm[w]]
     if not trajs:
         return [], 0
     perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
@@ -226,13 +330,15 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
 
 def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_workers: int = 4, mode: str = "samples",
                   eval_mode: bool = False, verbose: bool = False, deepmimic: bool = False, rng: str = "reference",
-                  chunk: int = 8):
+                  chunk: int = 8, speculate: bool = True, graph: bool = True):
     """milo.sampler.sample_points on the GPU.  `env` is a BatchedSimEnv (or a RolloutEngine):
     its ensemble, reset source and termination are used, and its lane count caps the
     concurrency; `policy` a DevicePolicy.  Returns the reference's list of path dicts
     (observations / next_observations / actions float64, rewards 0, agent_infos {mean,
     log_std, evaluation}, env_infos, terminated).  A missing info['valid'] counts as valid
-    (SimEnv returns {}; the reference's deepmimic=True branch, sampler.py:61, would raise)."""
+    (SimEnv returns {}; the reference's deepmimic=True branch, sampler.py:61, would raise).
+    `speculate`: admit beyond the worst-case reservation from the observed trajectory lengths
+    (same result, see _collect); `graph`: replay each chunk's steps as a captured HIP graph."""
     assert mode == "samples" or mode == "trajectories"
     if rng not in ("reference", "device"):
         raise ValueError("rng must be 'reference' or 'device'")
@@ -241,13 +347,16 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
     quota = math.ceil(num_to_collect / W)  # sampler.py:113
     R = src.term.horizon
     need = W * (math.ceil(quota / R) if mode == "samples" else quota)
+    if speculate and mode == "samples":
+        need *= 4  # room for trajectories shorter than the horizon (lengths ~R/4) to run at once
     lanes = max(1, min(need, src.B))
     K = max(1, min(int(chunk), R))
     eng = _sampler_engine(env, lanes, K, policy)
     if rng == "device":
         policy.seed = (12345 + int(base_seed)) & 0xFFFFFFFFFFFFFFFF
     t0 = time.time()
-    paths, n = _collect(eng, W, quota, mode, int(base_seed), rng, eval_mode) if quota > 0 else ([], 0)
+    paths, n = (_collect(eng, W, quota, mode, int(base_seed), rng, eval_mode, speculate=speculate, graph=graph)
+                if quota > 0 else ([], 0))
     if verbose:
         print(f"Collected {n} and {len(paths)} trajectories in {time.time() - t0} seconds")
     return paths

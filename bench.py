@@ -83,7 +83,9 @@ def parse():
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
-    p.add_argument("--cpu-samples", type=int, default=0, help="env-steps per worker at each sweep point (default 1500)")
+    p.add_argument("--cpu-samples", type=int, default=0,
+                   help="env-steps per worker at each sweep point (default: sized for --cpu-point-s)")
+    p.add_argument("--cpu-point-s", type=float, default=3.0, help="seconds of sampling per sweep point")
     p.add_argument("--cpu-final-samples", type=int, default=200000,
                    help="env-steps of the timed best-W run (five 40 000-sample rollouts: 10-30 s of CPU work)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
@@ -96,6 +98,12 @@ def parse():
                    help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward (valid "
                         "only while consecutive rollouts share the policy: fixed-policy collection / evaluation; "
                         "a trainer updates the policy between iterations, so the default is the serial order)")
+    p.add_argument("--mode", choices=["engine", "paths"], default="engine",
+                   help="engine: persistent lanes x synchronous steps + device relabel (throughput); paths: the "
+                        "reference's semantics through the drop-in surfaces -- sample_points(num_to_collect, "
+                        "num_workers=--workers): complete exact-seeded trajectories per worker quota, path dicts "
+                        "on the host -- then relabel_paths (batch_reinforce.py:88-169)")
+    p.add_argument("--workers", type=int, default=4, help="--mode paths: sampler workers (run.py --num_cpu, default 4)")
     p.add_argument("--motion", default=None, help="--cost amp: character + clip bundle (tools/pack_motion.py)")
     p.add_argument("--dry-run", action="store_true",
                    help="print this rank's launch layout (rank, world, rendezvous) and exit before any GPU or "
@@ -127,25 +135,29 @@ def cpu_share() -> int:
 
 def cpu_baseline_leg(S, A, args):
     """The oracle's restated reference sampler + host relabel, timed on this host's cores
-    (BASELINE.md §3): a sweep over the worker count W (powers of two up to the CPU share this
-    process has, plus the share itself), each point a bounded sample (about 1 500 env-steps per
-    worker); the best W is then timed end to end (sampler + relabel) on --cpu-final-samples
-    env-steps (default 200 000 = five 40 000-sample rollouts, 10-30 s of CPU work).  Runs before anything
-    touches the GPU (the worker pools fork)."""
+    (BASELINE.md §3).  A W = 1 calibration point sets the sweep's sample sizes so that every
+    sweep point (W = powers of two up to the CPU share this process has, plus the share
+    itself) runs about --cpu-point-s seconds of sampling; the best W is then timed end to end
+    (sampler + relabel, the relabel on the whole CPU share as the reference's one-process torch
+    relabel would use it) on --cpu-final-samples env-steps, twice: the value is the faster of
+    the two and both are reported.  Runs before anything touches the GPU (the pools fork)."""
     from oracle import cpu_baseline as cb
     share = cpu_share()
     if args.cpu_workers:
         grid = [args.cpu_workers]
     else:
         grid = sorted({w for w in (1, 2, 4, 8, 16, 32, 64, 128, 256) if w <= share} | {share})
-    per_worker = max(300, (args.cpu_samples or 1500))
+    cal = cb.run(S, A, workers=1, samples=300, expert_rows=args.expert_rows, relabel=False)
+    rate1 = cal["sampler_steps_per_s"]
     sweep = []
     for w in grid:
-        r = cb.run(S, A, workers=w, samples=per_worker * w, expert_rows=args.expert_rows, relabel=False)
+        n = args.cpu_samples * w if args.cpu_samples else int(max(300 * w, args.cpu_point_s * rate1 * w))
+        r = cb.run(S, A, workers=w, samples=n, expert_rows=args.expert_rows, relabel=False)
         sweep.append((w, r))
     best_w, best = max(sweep, key=lambda x: x[1]["sampler_steps_per_s"])
-    best = cb.run(S, A, workers=best_w, samples=max(per_worker * best_w, args.cpu_final_samples),
-                  expert_rows=args.expert_rows, relabel=True)
+    finals = [cb.run(S, A, workers=best_w, samples=max(best["samples"], args.cpu_final_samples),
+                     expert_rows=args.expert_rows, relabel=True, relabel_threads=share) for _ in range(2)]
+    best = max(finals, key=lambda r: r["end_to_end_steps_per_s"])
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -155,17 +167,20 @@ def cpu_baseline_leg(S, A, args):
                     break
     except OSError:
         pass
-    pts = ", ".join(f"W={w}: {r['sampler_steps_per_s']:.0f}" for w, r in sweep)
+    pts = ", ".join(f"W={w}: {r['sampler_steps_per_s']:.0f} ({r['sampler_s']:.1f}s)" for w, r in sweep)
+    e2e = [round(r["end_to_end_steps_per_s"], 1) for r in finals]
     return {
         "value": round(best["end_to_end_steps_per_s"], 1), "unit": "env-steps/s", "cores": best["workers"],
         "kind": "port",
         "sample": (f"{best['samples']} env-steps ({best['paths']} complete trajectories) by {best['workers']} "
                    f"forked sampler workers (torch threads 1) + host relabel (fit_cost + per-path bonus costs, "
-                   f"{args.expert_rows}-row expert buffer, {best['workers']} torch threads); sampler alone "
+                   f"{args.expert_rows}-row expert buffer, {best['relabel_threads']} torch threads); sampler alone "
                    f"{best['sampler_steps_per_s']:.0f} env-steps/s; sampler {best['sampler_s']:.2f}s + relabel "
-                   f"{best['relabel_s']:.2f}s"),
+                   f"{best['relabel_s']:.2f}s; best of 2 end-to-end runs"),
+        "end_to_end_runs": e2e,
+        "spread": round((max(e2e) - min(e2e)) / max(e2e), 4),
         "sweep_sampler_steps_per_s": pts,
-        "best_workers": best_w,
+        "best_workers": best_w, "relabel_threads": best["relabel_threads"],
         "cpu_share": share, "os_cpu_count": os.cpu_count(), "cpu_model": cpu,
     }
 
@@ -338,7 +353,7 @@ def main():
     # N > 1 (MMD): each rank scores N_e / N expert rows in its relabel and the fp64 partial sums
     # are all-reduced asynchronously (the expert cost is the bonus_mmd log's term),
     # waited for (GPU-side) only before the next relabel overwrites the sum
-    shard = world > 1 and args.cost == "mmd"
+    shard = world > 1 and args.cost == "mmd" and args.mode == "engine"
     if shard:
         cost.shard_expert(rank, world, allreduce_async)
 
@@ -350,6 +365,23 @@ def main():
         elif args.cost == "mmd":
             cost.get_expert_cost()
         return T * B
+
+    paths_info = {}
+    if args.mode == "paths":
+        # the reference's call sequence (batch_reinforce.py:88-90, 103-169): sample_points with W
+        # workers' exact-seeded trajectories (path dicts on the host), then the relabel of those
+        # paths; this rank's workers get their own seed block
+        from amp_extensions_amd.relabel import relabel_paths
+        it = [0]
+
+        def one_rollout():
+            it[0] += 1
+            paths = amx.sample_points(eng, pol, num_to_collect=per_rank, base_seed=1000 * rank + it[0],
+                                      num_workers=args.workers)
+            relabel_paths(paths, cost, ens, allreduce=allreduce)
+            n = sum(len(p["rewards"]) for p in paths)
+            paths_info.update(paths=len(paths), samples=n)
+            return n
 
     for _ in range(args.warmup):
         one_rollout()
@@ -365,7 +397,8 @@ def main():
     # profiles/r02_event_gaps.txt) -- 2 % of the timed region.  The other GEMM paths keep
     # HIP events.
     graph = None
-    use_graph = args.graph == "on" or (args.graph == "auto" and B * T < 16384 and args.gemm == "f16x3")
+    use_graph = args.mode == "engine" and (args.graph == "on" or (args.graph == "auto" and B * T < 16384 and
+                                                                  args.gemm == "f16x3"))
     if use_graph and args.gemm != "f16x3":
         raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
     timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
@@ -414,7 +447,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    term_rate = float(eng.done[:T].float().mean().item())
+    term_rate = float(eng.done[:T].float().mean().item()) if args.mode == "engine" else None
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -479,6 +512,15 @@ def main():
                 "samples_per_rollout": T * B * world, "samples_per_rollout_per_gpu": T * B,
                 "lanes_per_gpu": B, "sync_steps": T,
                 "launch": "eager" if graph is None else "HIP graph replay of the whole rollout",
+                **({} if args.mode == "engine" else {
+                    "mode": (f"reference semantics: sample_points(num_to_collect={per_rank}, num_workers="
+                             f"{args.workers}) -> complete exact-seeded trajectories (per-worker quota "
+                             f"ceil(N/W)), host path dicts -> relabel_paths; chunks of 8 steps replayed as "
+                             f"HIP graphs, speculative admission"),
+                    "samples_per_rollout": paths_info.get("samples", 0) * world,
+                    "samples_per_rollout_per_gpu": paths_info.get("samples", 0),
+                    "paths_per_rollout_per_gpu": paths_info.get("paths", 0),
+                    "lanes_per_gpu": None, "sync_steps": None, "launch": "sampler chunks"}),
                 "state_dim": S, "action_dim": A, "ensemble": "4 x dense-connect [512]x4 ReLU",
                 "rff_features": 512, "expert_rows": args.expert_rows, "policy": "tanh MLP(32,32)",
                 "parallelism": (f"dp{world} (the {args.total_samples}-sample rollout's lanes sharded over the "

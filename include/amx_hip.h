@@ -39,6 +39,7 @@ extern "C" {
 #define AMX_K_TILE 32
 #define AMX_MAX_MODELS 8
 #define AMX_MAX_BODIES 32
+#define AMX_MT_STATE_BYTES 2512  /* one numpy-legacy MT19937 state (amx_mt_seed) */
 
 enum {
   AMX_OK = 0,
@@ -524,6 +525,17 @@ int amx_adv_whiten(amx_ctx* ctx, int T, int L, const int32_t* len, const int64_t
  * device RNG the reset/policy kernels use. */
 int amx_philox(amx_ctx* ctx, uint64_t seed, uint32_t ctr1, uint32_t ctr2, uint32_t ctr3,
                uint32_t* out, int n, void* stream);
+
+/* Host-side (no device, no context) policy noise of the reference sampler, bit-exact with
+ * numpy's legacy RandomState as mjrl MLP.get_action draws it (mjrl/mjrl/policies/
+ * gaussian_mlp.py:95-104: np.random.uniform() for the eps test, then np.random.randn(A), per
+ * step) after get_samples' np.random.seed(seed) (milo/milo/sampler.py:39).  `states` is host
+ * memory of n_states * AMX_MT_STATE_BYTES; amx_mt_seed seeds states[slots[i]] with seeds[i]
+ * (np.random.seed(int)); amx_mt_policy_noise advances states[slots[i]] by `steps` get_action
+ * calls, writing the randn values to out[k * ld_step + slots[i] * ld_slot + a] (doubles). */
+int amx_mt_seed(void* states, int n_states, const int32_t* slots, const uint32_t* seeds, int n);
+int amx_mt_policy_noise(void* states, int n_states, const int32_t* slots, int n, int steps, int A,
+                        double* out, long long ld_step, long long ld_slot);
 
 #ifdef __cplusplus
 }

@@ -35,8 +35,10 @@ def _work(i):
 
 def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers: int | None = None,
         samples: int = 20000, horizon: int = 300, expert_rows: int = 50000, feature_dim: int = 512,
-        lambda_b: float = 0.0025, seed: int = 100, relabel: bool = True) -> dict:
-    """Returns env-steps/s of the CPU sampler alone and (relabel=True) of sampler + relabel."""
+        lambda_b: float = 0.0025, seed: int = 100, relabel: bool = True, relabel_threads: int | None = None) -> dict:
+    """Returns env-steps/s of the CPU sampler alone and (relabel=True) of sampler + relabel.
+    The relabel runs in this process with `relabel_threads` torch threads (default: the
+    worker count); the reference's relabel is one process with torch's default threading."""
     from amp_extensions_amd import synthetic as syn
 
     torch.set_num_threads(1)
@@ -58,7 +60,8 @@ def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers:
     if not relabel:
         return dict(samples=n, paths=len(paths), workers=workers, sampler_s=t1 - t0, sampler_steps_per_s=n / (t1 - t0))
     # host relabel with the reference's batching (thread count restored for the relabel)
-    torch.set_num_threads(workers)
+    threads = relabel_threads or workers
+    torch.set_num_threads(threads)
     expert = torch.from_numpy(syn.expert(expert_rows, S, 3))
     cost = R.RBFLinearCostRef(expert, feature_dim=feature_dim, bw_quantile=0.1, lambda_b=lambda_b, seed=seed)
     thr = R.compute_threshold(ens, norms, torch.from_numpy(s).float()[:4096], torch.from_numpy(a).float()[:4096])
@@ -67,5 +70,6 @@ def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers:
     R.relabel_mmd(paths, cost, disc_fn, thr)
     t3 = time.perf_counter()
     torch.set_num_threads(1)
-    return dict(samples=n, paths=len(paths), workers=workers, sampler_s=t1 - t0, relabel_s=t3 - t2,
+    return dict(samples=n, paths=len(paths), workers=workers, relabel_threads=threads, sampler_s=t1 - t0,
+                relabel_s=t3 - t2,
                 sampler_steps_per_s=n / (t1 - t0), end_to_end_steps_per_s=n / ((t1 - t0) + (t3 - t2)))

@@ -234,3 +234,31 @@ def test_deepmimic_arg_file_parsing_and_reset_args(tmp_path):
             SE.check_reset_args(dict(RUN_PY_RESET_ARGS, **bad))
     with pytest.raises(FileNotFoundError):
         SE.motion_from_args(None, str(tmp_path / "missing_args.txt"))
+
+
+def test_host_policy_noise_matches_numpy_legacy_stream(lib):
+    """amx_mt_seed / amx_mt_policy_noise (the sampler's per-lane policy noise) reproduce numpy's
+    legacy RandomState bit for bit as mjrl MLP.get_action draws it after np.random.seed(s)
+    (gaussian_mlp.py:99-102: np.random.uniform(), then np.random.randn(A), per step), carried
+    across calls (the polar method's cached normal included: odd A), for the full seed range."""
+    for A in (36, 7):
+        L, K = 6, 5
+        st = np.zeros((L, _native.AMX_MT_STATE_BYTES), np.uint8)
+        slots = np.array([0, 2, 5, 3], np.int32)
+        seeds = np.array([12345, 12345 + 100 * 3 + 7, 0, 2 ** 32 - 1], np.uint32)
+        assert lib.amx_mt_seed(st.ctypes.data, L, slots.ctypes.data, seeds.ctypes.data, 4) == 0
+        rss = [np.random.RandomState(int(x)) for x in seeds]
+        out = np.full((K, L, A), np.nan)
+        for rep in range(3):
+            sub = slots[rep % 2:]  # not every lane advances in every chunk
+            assert lib.amx_mt_policy_noise(st.ctypes.data, L, sub.ctypes.data, sub.size, K, A, out.ctypes.data,
+                                           L * A, A) == 0
+            for lane in sub:
+                i = list(slots).index(lane)
+                want = np.empty((K, A))
+                for k in range(K):
+                    rss[i].uniform()
+                    want[k] = rss[i].randn(A)
+                np.testing.assert_array_equal(out[:, lane], want)
+    bad = np.array([L], np.int32)
+    assert lib.amx_mt_seed(st.ctypes.data, L, bad.ctypes.data, seeds.ctypes.data, 1) != 0

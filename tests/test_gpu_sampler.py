@@ -81,17 +81,22 @@ def test_sample_points_reproduces_reference_g8(setup, golden):
 
 
 @pytest.mark.parametrize("mode,N,horizon,chunk", [("samples", 400, 40, 8), ("samples", 257, 25, 5),
-                                                  ("trajectories", 9, 30, 8)])
-def test_sample_points_matches_oracle(setup, mode, N, horizon, chunk):
+                                                  ("trajectories", 9, 30, 8), ("samples", 900, 30, 4)])
+@pytest.mark.parametrize("speculate,graph", [(True, True), (False, False), (True, False)])
+def test_sample_points_matches_oracle(setup, mode, N, horizon, chunk, speculate, graph):
     """W=2 and W=3 workers vs the oracle's sequential get_samples with the same seeds, on a
-    standing reset table (long trajectories: several chunks, mid-chunk ends, refills)."""
+    standing reset table (long trajectories: several chunks, mid-chunk ends, refills), with the
+    speculative admission (surplus trajectories run and are dropped) and the chunk HIP graph on
+    and off: the same paths either way."""
     amx, ens, ens_w, norms, pw, log_std, pol = setup
     from amp_extensions_amd.synthetic import reset_table
     table = reset_table(256, S, 1)
     table[::7, 2] = -2.0  # root below the ground: these reset poses fall at once (length-1 trajectories)
+    table[1::3, 2] = -0.3  # these fall after a few steps: short trajectories drive the speculation
     for W in (2, 3):
         env = amx.BatchedSimEnv(ens, table, lanes=512, horizon=horizon, record_means=True)
-        paths = amx.sample_points(env, pol, num_to_collect=N, base_seed=7, num_workers=W, mode=mode, chunk=chunk)
+        paths = amx.sample_points(env, pol, num_to_collect=N, base_seed=7, num_workers=W, mode=mode, chunk=chunk,
+                                  speculate=speculate, graph=graph)
         per = math.ceil(N / W)
         ref = []
         for i in range(W):
