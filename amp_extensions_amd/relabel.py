@@ -15,6 +15,26 @@ from .costs import GAILCost, RBFLinearCost, cost_input
 from .dist import feature_mean
 
 
+def _rows(paths, key: str) -> np.ndarray:
+    """np.concatenate([p[key] for p in paths]) -- without the copy when the paths' arrays are
+    consecutive views of one buffer (sample_points returns them so)."""
+    arrs = [p[key] for p in paths]
+    a0 = arrs[0]
+    base = a0.base
+    if base is not None and all(a.base is base and a.flags.c_contiguous and a.dtype == a0.dtype for a in arrs):
+        row = a0.strides[0]
+        start = a0.__array_interface__["data"][0]
+        off = start
+        for a in arrs:
+            if a.__array_interface__["data"][0] != off or a.shape[1:] != a0.shape[1:]:
+                break
+            off += a.shape[0] * row
+        else:
+            n = sum(a.shape[0] for a in arrs)
+            return np.lib.stride_tricks.as_strided(a0, shape=(n,) + a0.shape[1:], strides=a0.strides)
+    return np.concatenate(arrs)
+
+
 def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", allreduce=None) -> dict:
     """`cost_input_type` builds the fit_cost input ('ss' or 'sa', batch_reinforce.py:107-110);
     the per-sample rewards use reward_func's own input_type (get_bonus_costs).  With
@@ -26,9 +46,9 @@ def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", all
         raise NotImplementedError(f"cost_input_type {cost_input_type!r}: batch_reinforce builds only 'ss' / 'sa'")
     dev = reward_func.ctx.device
     lens = [len(p["observations"]) for p in paths]
-    obs = torch.from_numpy(np.concatenate([p["observations"] for p in paths])).float().to(dev)
-    nxt = torch.from_numpy(np.concatenate([p["next_observations"] for p in paths])).float().to(dev)
-    act = torch.from_numpy(np.concatenate([p["actions"] for p in paths])).float().to(dev)
+    obs = torch.from_numpy(_rows(paths, "observations")).to(dev).float()
+    nxt = torch.from_numpy(_rows(paths, "next_observations")).to(dev).float()
+    act = torch.from_numpy(_rows(paths, "actions")).to(dev).float()
     bonus_v = ipm_v = None
     if isinstance(reward_func, RBFLinearCost):
         if ensemble is None:

@@ -115,7 +115,11 @@ class _HostNoise:
     def __init__(self, lib, L: int, K: int, A: int):
         self.lib, self.L, self.K, self.A = lib, L, K, A
         self.states = np.zeros((L, N.AMX_MT_STATE_BYTES), np.uint8)
-        self.host = torch.zeros(K, L, A, dtype=torch.float64, pin_memory=torch.cuda.is_available())
+        # two pinned buffers: the next chunk's noise is drawn into one while the other's upload
+        # and the current chunk's steps run on the GPU
+        pin = torch.cuda.is_available()
+        self.bufs = [torch.zeros(K, L, A, dtype=torch.float64, pin_memory=pin) for _ in range(2)]
+        self.cur = 0
 
     def seed(self, lanes: np.ndarray, seeds: np.ndarray) -> None:
         sl = np.ascontiguousarray(lanes, np.int32)
@@ -123,12 +127,13 @@ class _HostNoise:
         N.check(self.lib.amx_mt_seed(self.states.ctypes.data, self.L, sl.ctypes.data, sd.ctypes.data, sl.size),
                 "amx_mt_seed")
 
-    def draw(self, lanes: np.ndarray) -> torch.Tensor:
+    def draw(self, lanes: np.ndarray, buf: torch.Tensor) -> torch.Tensor:
+        """The next K steps' noise of `lanes` into their slots of `buf` (other slots untouched)."""
         sl = np.ascontiguousarray(lanes, np.int32)
         N.check(self.lib.amx_mt_policy_noise(self.states.ctypes.data, self.L, sl.ctypes.data, sl.size, self.K,
-                                             self.A, self.host.data_ptr(), self.L * self.A, self.A),
+                                             self.A, buf.data_ptr(), self.L * self.A, self.A),
                 "amx_mt_policy_noise")
-        return self.host
+        return buf
 
 
 class _ChunkGraph:
@@ -148,12 +153,15 @@ class _ChunkGraph:
         t0 = eng.t
         with torch.cuda.stream(side):
             eng._capturing = True
+            # capture_begin/end directly: torch.cuda.graph's context manager also synchronises,
+            # garbage-collects and empties the allocator cache (13 ms per sample_points call)
+            self.g.capture_begin(capture_error_mode="thread_local")
             try:
-                with torch.cuda.graph(self.g, stream=side, capture_error_mode="thread_local"):
-                    for k in range(K):
-                        eng.step(noise=None if noise_dev is None else noise_dev[k])
-                    N.check(c.lib.amx_counter_add(c.h, eng.dev_step.data_ptr(), K, c.stream), "amx_counter_add")
+                for k in range(K):
+                    eng.step(noise=None if noise_dev is None else noise_dev[k])
+                N.check(c.lib.amx_counter_add(c.h, eng.dev_step.data_ptr(), K, c.stream), "amx_counter_add")
             finally:
+                self.g.capture_end()
                 eng._capturing = False
         torch.cuda.current_stream(c.device).wait_stream(side)
         eng.t, eng.step_counter = t0, eng.step_counter - K  # the captured steps did not run
@@ -196,7 +204,16 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     ref_noise = rng == "reference" and not eval_mode
     hn = _HostNoise(c.lib, L, K, A) if ref_noise else None
     noise_dev = torch.zeros(K, L, A, dtype=torch.float64, device=dev) if ref_noise else None
+    pin = torch.cuda.is_available()
+    # per-chunk reset inputs: staged in pinned memory, uploaded without a host wait
+    mask_h = torch.zeros(L, dtype=torch.uint8, pin_memory=pin)
+    counts_h = torch.zeros(L, dtype=torch.int32, pin_memory=pin)
+    rows_h = torch.zeros(L, dtype=torch.float64 if motion is not None else torch.int32, pin_memory=pin)
     mask_dev = torch.empty(L, dtype=torch.uint8, device=dev)
+    counts_dev = torch.empty(L, dtype=torch.int32, device=dev)
+    rows_dev = torch.empty(L, dtype=rows_h.dtype, device=dev)
+    mask_np, counts_np, rows_np = mask_h.numpy(), counts_h.numpy(), rows_h.numpy()
+    pre_drawn = False
     ended_sum, ended_n = 0, 0
     chunk_graph = None
     chunks, budget = 0, 4 * (W * quota + W) * (R + K) // K + 64
@@ -209,7 +226,9 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
 
     while True:
         # ---- per worker: drop the unneeded, detect completion, admit (round-robin) ----
-        lhat = (ended_sum / ended_n) if (speculate and ended_n >= 4) else float(R)
+        # speculation: 2x the worst-case concurrency until lengths are known (lanes are nearly free
+        # at these counts: the step time is latency-bound), then the mean ended length
+        lhat = float(R) if not speculate else (ended_sum / ended_n if ended_n >= 4 else 0.5 * R)
         for w in range(W):
             if done_w[w]:
                 continue
@@ -259,27 +278,30 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
             raise RuntimeError("sample_points: step budget exhausted (trajectories longer than the horizon?)")
         # ---- resets: the new trajectories (reset counter j-1 -> member j mod M) and the idle lanes ----
         eng.begin_rollout()
-        mask = np.ones(L, np.uint8)
-        mask[active] = 0
-        counts = np.zeros(L, np.int32)
-        rows = np.zeros(L, np.float64 if motion is not None else np.int32)
+        mask_np.fill(1)
+        mask_np[active] = 0
+        counts_np.fill(0)
         new_lanes = np.array([tr.lane for tr in new], np.int64)
         for tr in new:
-            mask[tr.lane] = 1
-            counts[tr.lane] = tr.j - 1
+            mask_np[tr.lane] = 1
+            counts_np[tr.lane] = tr.j - 1
             if rng == "reference":
                 t = _gym_np_random(tr.seed).uniform(low=0, high=time_max)  # seed_env + reset (sim_env.py:132,276)
-                rows[tr.lane] = t if motion is not None else int(np.floor(t))
-        if hn is not None and new:
-            hn.seed(new_lanes, np.array([tr.seed for tr in new]))  # np.random.seed (sampler.py:39)
-        sel = torch.from_numpy(np.nonzero(mask)[0]).to(dev)
-        eng.reset_count.index_copy_(0, sel, torch.from_numpy(counts[mask != 0]).to(dev))
-        mask_dev.copy_(torch.from_numpy(mask))
-        rows_dev = torch.from_numpy(rows).to(dev) if rng == "reference" else None
-        eng.reset_lanes(mask_dev, rows_dev)
+                rows_np[tr.lane] = t if motion is not None else int(np.floor(t))
+        mask_dev.copy_(mask_h, non_blocking=True)
+        counts_dev.copy_(counts_h, non_blocking=True)
+        # reset lanes restart their counter at j - 1 (idle lanes at 0); the reset kernel adds one
+        torch.where(mask_dev.bool(), counts_dev, eng.reset_count, out=eng.reset_count)
+        if rng == "reference":
+            rows_dev.copy_(rows_h, non_blocking=True)
+        eng.reset_lanes(mask_dev, rows_dev if rng == "reference" else None)
         # ---- K synchronous steps ----
         if hn is not None:
-            noise_dev.copy_(hn.draw(active), non_blocking=True)
+            if new:
+                hn.seed(new_lanes, np.array([tr.seed for tr in new]))  # np.random.seed (sampler.py:39)
+            buf = hn.bufs[hn.cur]
+            hn.draw(new_lanes if pre_drawn else active, buf)  # (the continuing lanes' noise is drawn)
+            noise_dev.copy_(buf, non_blocking=True)
         if graph and chunk_graph is None and chunks >= 2:  # (the first chunk allocates the workspaces)
             eng.begin_rollout()
             chunk_graph = _ChunkGraph(eng, K, noise_dev)
@@ -288,6 +310,10 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
         else:
             for k in range(K):
                 eng.step(noise=None if noise_dev is None else noise_dev[k])
+        if hn is not None:  # the next chunk's noise of the lanes in flight, while the GPU steps
+            hn.cur ^= 1
+            hn.draw(active, hn.bufs[hn.cur])
+            pre_drawn = True
         done = eng.done[:K].cpu().numpy().astype(bool)  # [K, L]: the chunk's one host sync
         # ---- compact the in-flight lanes' transitions into the store (vectorised) ----
         d = done[:, active]

@@ -530,7 +530,7 @@ def main():
                                 if strong else
                                 f"dp{world} (lane-sharded, {args.samples_per_gpu} samples per rank, 1 all-reduce "
                                 f"per rollout)"),
-                "termination_rate": round(term_rate, 5), "threshold": thr,
+                "termination_rate": None if term_rate is None else round(term_rate, 5), "threshold": thr,
                 "gemm": gi["desc"],
             },
             "roofline": {
