@@ -45,10 +45,20 @@ struct Tile {
 
 
 // LDS of the RFF epilogue: the staged BM x (BN + 4) f32 tile and BM row-validity flags
-constexpr size_t rff_epi_lds(int bm, int bn) { return ((size_t)bm * (bn + 4) + bm) * 4; }
+constexpr size_t rff_epi_lds(int bm, int bn) { return (size_t)bm * (bn + 4) * 4; }
 
 // ---- epilogue (shared by the f32 and the bf16x6 main loops: the 32x32 C/D register map
 // is dtype-independent on gfx950) ---------------------------------------------------------
+// Row validity of `n` <= 64 consecutive rows from `row0` (row < n_valid and row_mask[row] != 0)
+// as a wave-uniform bit mask: lane l tests row row0 + l, a ballot gathers the bits.  The RFF
+// epilogues test bit i per row from this mask instead of reading a per-row flag from LDS, so
+// no LDS address is read by every lane of a wave at once.
+__device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, int n) {
+  const int l = threadIdx.x & 63, row = row0 + l;
+  const bool v = l < n && row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
+  return __ballot(v);
+}
+
 template <int EPI, class TL>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], int g, int tm, int tn) {
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN;
@@ -109,7 +119,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
     // valid rows in fixed row order, the PARTS part sums added in part order (deterministic;
     // 2 parts at BN 128, 4 at BN 64).
     constexpr int CLD = BN + 4, PARTS = 256 / BN, PR = BM / PARTS;
-    float* Cs = smem;  // [BM][CLD] + BM row flags (rff_epi_lds), reuses the stage buffers (last barrier passed)
+    float* Cs = smem;  // [BM][CLD] (rff_epi_lds), reuses the stage buffers (last barrier passed)
 #pragma unroll
     for (int n = 0; n < TN; ++n)
 #pragma unroll
@@ -119,15 +129,11 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
           const int r = wm * TM * 32 + m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
           Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
         }
-    // the tile's row validity (n_valid, row_mask) once per row, beside the staged tile: the
-    // column loop reads it from LDS (one broadcast per row) instead of a global load per row
-    int* vf = reinterpret_cast<int*>(smem + BM * CLD);
-    if (t < BM) {
-      const int row = tm * BM + t;
-      vf[t] = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
-    }
+    const int c = t & (BN - 1), part = t / BN;  // part is wave-uniform (BN >= 64)
+    // the validity (n_valid, row_mask) of the wave's PR <= 64 rows as one wave-uniform bit mask:
+    // lane l loads row part*PR + l (lane-distinct, coalesced), a ballot forms the mask
+    const uint64_t vmask = row_valid_mask(a, tm * BM + part * PR, PR);
     __syncthreads();
-    const int c = t & (BN - 1), part = t / BN;
     const int col = tn * BN + c;
     const float bv = a.bias[col];
     double csum = 0.0;
@@ -139,7 +145,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
       const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
       Cg[(long long)row * a.ldc + col] = phi;
-      csum += vf[r] ? (double)phi : 0.0;
+      csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
     }
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);  // [PARTS][BN]
@@ -609,13 +615,9 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           Cs[(lrow0 + m * 16 + 4 * lq + j) * CLD + wn * TL::WCOLS + n * 16 + lc] = acc[m][n][j];
-    int* vf = reinterpret_cast<int*>(Cs + 128 * CLD);  // row validity, as the 32x32 path's epilogue
-    if (threadIdx.x < 128) {
-      const int row = tm * 128 + threadIdx.x;
-      vf[threadIdx.x] = row < a.n_valid && (a.row_mask == nullptr || a.row_mask[row] != 0);
-    }
-    __syncthreads();
     const int t = threadIdx.x, c = t & 127, half = t >> 7;
+    const uint64_t vmask = row_valid_mask(a, tm * 128 + half * 64, 64);  // as the 32x32 path's epilogue
+    __syncthreads();
     const int col = tn * 128 + c;
     const float bv = a.bias[col];
     double csum = 0.0;
@@ -626,7 +628,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
       const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
       a.C[(long long)row * a.ldc + col] = phi;
-      csum += vf[r] ? (double)phi : 0.0;
+      csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
     }
     __syncthreads();
     double* red = reinterpret_cast<double*>(smem);

@@ -468,6 +468,10 @@ def main():
     per_fwd = ctx.L + 1  # GEMM launches per forward
     launches = n_fwd * per_fwd
     flops_per_fwd = ens.mlp_flops_per_sample() * B
+    if args.mode == "paths":
+        # the sampler's forwards run at its own lane counts (chunks of idle-padded lanes): count
+        # the algorithmic FLOPs of the samples it returned over the forwards' measured time
+        flops_per_fwd = ens.mlp_flops_per_sample() * samples / max(n_fwd, 1)
     achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
     ens.gemm_events = None
 
