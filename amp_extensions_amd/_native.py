@@ -73,6 +73,7 @@ SIGNATURES = {
     "amx_set_gemm_timer": (c_int, [vp, vp]),
     "amx_split_workspace_floats": (c_ll, [vp, c_int, c_int, ip]),
     "amx_set_split_workspace": (c_int, [vp, vp, c_ll, vp, c_int]),
+    "amx_set_out_tile": (c_int, [vp, c_int]),
     "amx_policy_blob_floats": (c_ll, [vp, c_int, c_int]),
     "amx_policy_pack": (c_int, [vp, vp, vp, c_int, vp, vp, c_int, vp, vp, vp, vp]),
     "amx_rff_features": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_flt, vp, c_int,

@@ -73,6 +73,11 @@ class AmxContext:
         N.check(self.lib.amx_set_gemm_timer(self.h, self._timer.data_ptr()), "amx_set_gemm_timer")
         return self._timer
 
+    def set_out_tile(self, tile: int) -> None:
+        """Output-layer tile of the f16x3 forward (amx_set_out_tile): 0 default (= 1, the
+        register-staged tiles), 2 LDS-DMA ring with 16-row waves, 3 ring with 32 x 112 waves."""
+        N.check(self.lib.amx_set_out_tile(self.h, int(tile)), "amx_set_out_tile")
+
     @property
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream

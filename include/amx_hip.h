@@ -369,6 +369,14 @@ int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf);
  * context (counters zeroed by the caller once; each launch leaves them zero); without it the
  * layer runs on row-block tiles.  One launch at a time per context. */
 long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters);
+
+/* Output-layer tile of the f16x3 forward (amx_gemm_out_unnorm_h3), for A/B measurement:
+ * 0 = default = 1, the register-staged 128 x 224 / row-block / 128 x 256 tiles; 2 = the
+ * LDS-DMA ring tile (both operands by global_load_lds into a 3-slot ring, two K-tiles ahead)
+ * with 8 waves of 16 x 16*ceil(S/16) (S in 193..240), 3 = the ring tile with 8 waves of
+ * 32 x 112 (S in 193..224); other S fall back to 1.  Identical bits: the ring issues the same
+ * limb products per 16 x 16 block in the same K order over the same stream-K segments. */
+int amx_set_out_tile(amx_ctx* ctx, int tile);
 int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
                             int n_counters);
 
