@@ -1,4 +1,4 @@
-// Victim kernels for the cross-process interference seen on gfx950 (DESIGN.md §5): each mode
+// Victim kernels for the cross-process interference seen on gfx950 (DESIGN.md §5.3): each mode
 // computes a deterministic result; the reference is taken before the co-runner starts (the
 // program sleeps 4 s after it), then the kernel is re-run for ~6 s and every result is
 // compared bit for bit; mismatching lanes are reported by their lane index within the wave.
