@@ -61,6 +61,10 @@ SIGNATURES = {
     "amx_step_rexp": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, c_int, vp]),
     "amx_step_reset": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, vp, c_int, vp,
                                c_u64, vp, vp, vp, vp, vp, c_ll, vp, c_int, vp]),
+    "amx_step_reset_act": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, vp, c_int, vp,
+                                   c_u64, vp, vp, vp, vp, vp, vp, c_int, c_int, vp, c_u64, c_u64, vp, c_int, vp, vp,
+                                   vp, c_ll, c_int, vp, c_ll, c_ll, c_int, c_int, vp]),
+    "amx_set_step_act_occupancy": (c_int, [vp, c_int]),
     "amx_rff_features_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, vp, vp, vp, c_flt, vp, c_int,
                                     vp, vp, vp]),
     "amx_disagreement": (c_int, [vp, vp, c_int, c_ll, vp, c_int, vp]),

@@ -49,6 +49,7 @@ struct amx_ctx {
   uint32_t* split_cnt;       //   and its per-tile arrival counters (zero when idle)
   int split_ncnt;
   int out_tile;              // amx_set_out_tile: output-layer tile of the f16x3 forward (0 = default)
+  int step_act_w8;           // amx_set_step_act_occupancy: k_step_act at two workgroups per CU (A/B)
   double* d_npg_scratch;     // amx_npg_reduce's run sums
   size_t npg_scratch_bytes;
 };

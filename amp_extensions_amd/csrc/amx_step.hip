@@ -188,11 +188,10 @@ struct StepArgs {
 // MM4: the MILO ensemble (M = 4): all four members' rows are loaded in the first phase and
 // the disagreement is formed from registers (one memory round trip instead of two; the same
 // per-lane j order as lane_disagreement, so the same bits).
+// srow (nullable, LDS): the float32 of the lane's next observation obs[t+1] (ob', or its reset
+// row), written lane-distinctly -- the input row of the fused policy (k_step_act)
 template <int NIT, bool MM4>
-__global__ __launch_bounds__(256) void k_step(StepArgs a) {
-  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (b >= a.B) return;  // wave-uniform
+__device__ __forceinline__ void step_lane(const StepArgs& a, int b, int lane, float* srow) {
   const amx_termination& T = a.term;
   const int S = a.S;
   const int k = a.model_idx[b];
@@ -336,7 +335,10 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
 #pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const int j = lane + 64 * it;
-        if (j < S) oo[j] = x[it];
+        if (j < S) {
+          oo[j] = x[it];
+          if (srow) srow[j] = (float)x[it];  // np.float32(observation)
+        }
       }
       if (lane == 0 && a.row_out) a.row_out[b] = -1;
     } else {
@@ -350,7 +352,11 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
         row = (int)((((uint64_t)r.y << 32) | r.x) % (uint64_t)a.R);
       }
       const double* src = a.table + (long long)row * S;
-      for (int j = lane; j < S; j += 64) oo[j] = src[j];
+      for (int j = lane; j < S; j += 64) {
+        const double v = src[j];
+        oo[j] = v;
+        if (srow) srow[j] = (float)v;
+      }
       if (lane == 0) {
         a.reset_count[b] = rc;
         a.model_idx_out[b] = rc % a.M;  // :282-283
@@ -367,6 +373,14 @@ __global__ __launch_bounds__(256) void k_step(StepArgs a) {
     if (a.disc) a.disc[b] = d;
     if (a.nonfinite) a.nonfinite[b] = nf ? 1 : 0;
   }
+}
+
+template <int NIT, bool MM4>
+__global__ __launch_bounds__(256) void k_step(StepArgs a) {
+  const int b = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (b >= a.B) return;  // wave-uniform
+  step_lane<NIT, MM4>(a, b, lane, nullptr);
 }
 
 // ---- reset ---------------------------------------------------------------------------------
@@ -561,8 +575,11 @@ __device__ inline void pol_combine(const float* __restrict__ part, int N, int nc
   }
 }
 
-__global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float psm[];
+// The policy of one workgroup's 16 lanes once its LDS is staged (k_policy; k_step_act): the
+// lanes' float32 observations in `so`, the weight image at psm.  Only threads < 256 (the first
+// four waves) work: k_step_act's other twelve waves take part in the barriers only, so the work
+// decomposition -- and every bit of the result -- is k_policy's.
+__device__ __forceinline__ void policy_core(const PolicyArgs& p, float* psm, int b0, int img_floats) {
   const int S = p.S, A = p.A, H1 = p.H1, H2 = p.H2;
   const int s1 = pol_stride(S), s2 = pol_stride(H1), s3 = pol_stride(H2);
   float* w1 = psm;                       // [H1][s1]   (packed image, amx_policy_pack)
@@ -571,35 +588,26 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   float* bb1 = w3 + A * s3;
   float* bb2 = bb1 + H1;
   float* bb3 = bb2 + H2;
-  const int nblob = pol_blob_floats(S, H1, H2, A);
-  float* so = psm + nblob;               // [16][s1]
+  float* so = psm + img_floats;          // [16][s1] (after the weight image's LDS slot)
   float* h1 = so + POL_LANES * s1;       // [16][s2]
   float* h2 = h1 + POL_LANES * s2;       // [16][s3]
   float* mo = h2 + POL_LANES * s3;       // [16][A] policy means
   float* xa_s = mo + POL_LANES * A;      // [16][A] float32 actions for the fused assembly
   float* part = xa_s + POL_LANES * A;    // layer partial sums (pol_part_floats)
   const int t = threadIdx.x;
-  const int b0 = blockIdx.x * POL_LANES;
-  // staging: the packed weight image (pads already zero) and the block's observation rows;
-  // the observation pads / rows of lanes >= B are zeroed (they take part in the MFMAs)
-  const int nl = (p.B - b0) < POL_LANES ? (p.B - b0) : POL_LANES;  // valid lanes of this block
-  pol_zero_pads(so, s1, S, nl);
-  for (int i = t + nl * s1; i < POL_LANES * s1; i += 256) so[i] = 0.f;
-  pol_stage_all(psm, p.blob, nblob >> 2, so, s1, p.ob + (long long)b0 * S, nl * S, S);
-  for (int i = t; i < POL_LANES * (s2 + s3); i += 256) h1[i] = 0.f;  // pads of h1/h2
-  __syncthreads();
+  const bool on = t < 256;               // wave-uniform
   const int nc1 = (S + 3) >> 2, nc2 = (H1 + 3) >> 2, nc3 = (H2 + 3) >> 2;
-  pol_mfma_layer(so, s1, nc1, w1, s1, H1, part);
+  if (on) pol_mfma_layer(so, s1, nc1, w1, s1, H1, part);
   __syncthreads();
-  pol_combine(part, H1, nc1, bb1, true, h1, s2);
+  if (on) pol_combine(part, H1, nc1, bb1, true, h1, s2);
   __syncthreads();
-  pol_mfma_layer(h1, s2, nc2, w2, s2, H2, part);
+  if (on) pol_mfma_layer(h1, s2, nc2, w2, s2, H2, part);
   __syncthreads();
-  pol_combine(part, H2, nc2, bb2, true, h2, s3);
+  if (on) pol_combine(part, H2, nc2, bb2, true, h2, s3);
   __syncthreads();
-  pol_mfma_layer(h2, s3, nc3, w3, s3, A, part);
+  if (on) pol_mfma_layer(h2, s3, nc3, w3, s3, A, part);
   __syncthreads();
-  pol_combine(part, A, nc3, bb3, false, mo, A);  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
+  if (on) pol_combine(part, A, nc3, bb3, false, mo, A);  // FCNetwork out_scale = 1, out_shift = 0 (fc_network.py:54)
   __syncthreads();
   // actions: one thread per (lane, pair u = 2pr, 2pr + 1): Box-Muller on one Philox block gives
   // both normals of the pair (gaussian_mlp.py:102-103: float32 mean + float64 noise)
@@ -610,7 +618,7 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
     ctr_lo = (uint32_t)cv;
     ctr_hi = (uint32_t)(cv >> 32);
   }
-  for (int e = t; e < POL_LANES * npairs; e += 256) {
+  for (int e = t; on && e < POL_LANES * npairs; e += 256) {
     const int l = e / npairs, pr = e - l * npairs;
     const int b = b0 + l;
     if (b >= p.B) continue;
@@ -644,6 +652,7 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
   }
   if (!p.x0) return;
   __syncthreads();
+  if (!on) return;  // (after the last barrier)
   // fused amx_assemble_input[_rexp] (dynamics.py:225-227): 16 threads per row (one DPP row of
   // the wave; columns c0 + 16q), the block's POL_LANES rows of x0 (once when stride_m is 0: the
   // f16x3 GEMMs read every model's x0 slice from model 0's rows, else for every model), and
@@ -704,6 +713,66 @@ __global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
     const int v = sl == 0 ? e : -100;
     for (int mm = 0; mm < p.M; ++mm) p.row_exp[mm * p.stride_rexp + sl * p.slot_stride + bb] = v;
   }
+}
+
+
+__global__ __launch_bounds__(256) void k_policy(PolicyArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float psm[];
+  const int S = p.S, s1 = pol_stride(S), s2 = pol_stride(p.H1), s3 = pol_stride(p.H2);
+  const int nblob = pol_blob_floats(S, p.H1, p.H2, p.A);
+  float* so = psm + nblob;               // [16][s1]
+  float* h1 = so + POL_LANES * s1;       // [16][s2], then h2 [16][s3]
+  const int t = threadIdx.x;
+  const int b0 = blockIdx.x * POL_LANES;
+  // staging: the packed weight image (pads already zero) and the block's observation rows;
+  // the observation pads / rows of lanes >= B are zeroed (they take part in the MFMAs)
+  const int nl = (p.B - b0) < POL_LANES ? (p.B - b0) : POL_LANES;  // valid lanes of this block
+  pol_zero_pads(so, s1, S, nl);
+  for (int i = t + nl * s1; i < POL_LANES * s1; i += 256) so[i] = 0.f;
+  pol_stage_all(psm, p.blob, nblob >> 2, so, s1, p.ob + (long long)b0 * S, nl * S, S);
+  for (int i = t; i < POL_LANES * (s2 + s3); i += 256) h1[i] = 0.f;  // pads of h1/h2
+  __syncthreads();
+  policy_core(p, psm, b0, nblob);
+}
+
+// ---- fused step + next action --------------------------------------------------------------
+// One workgroup = 16 waves = the 16 lanes of one policy block: wave w runs step t of lane
+// b0 + w (step_lane, amx_step_reset's fused form: update, termination, disagreement, cost row,
+// table reset) and leaves the float32 of the lane's obs[t+1] in its LDS row, then the block
+// runs the policy of step t + 1 on those rows (policy_core: actions, means, and the fused x0 +
+// row-exponent assembly of step t + 1's ensemble forward) -- the same values and bits as
+// amx_step_reset followed by amx_policy_act on obs[t+1], in one launch with the observation
+// rows kept on chip.  The weight image arrives by LDS-DMA (global_load_lds, whole 1-KiB pieces:
+// amx_policy_blob_floats rounds the image up to them) issued before the step's loads, so it is
+// in flight under the step phase without holding registers.
+__host__ __device__ inline int pol_image_lds_floats(int S, int H1, int H2, int A) {
+  return (pol_blob_floats(S, H1, H2, A) + 255) & ~255;
+}
+
+// W8: two workgroups per CU (<= 64 VGPRs, 8 waves per SIMD) instead of one
+template <int NIT, bool MM4, bool W8>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(W8 ? 8 : 1))) void k_step_act(StepArgs a,
+                                                                                                    PolicyArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float psm[];
+  const int S = p.S, s1 = pol_stride(S), s2 = pol_stride(p.H1), s3 = pol_stride(p.H2);
+  const int nimg = pol_image_lds_floats(S, p.H1, p.H2, p.A);
+  float* so = psm + nimg;                // [16][s1]
+  float* h1 = so + POL_LANES * s1;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int b0 = blockIdx.x * POL_LANES, b = b0 + wave;
+  for (int q = wave; q < (nimg >> 8); q += POL_LANES)  // 256 floats = one 1-KiB piece per wave-instruction
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.blob + q * 256 + 4 * lane),
+                                     (__attribute__((address_space(3))) void*)(psm + q * 256), 16, 0, 0);
+  float* srow = so + wave * s1;
+  if (b < a.B) {  // wave-uniform
+    step_lane<NIT, MM4>(a, b, lane, srow);
+    for (int j = S + lane; j < s1; j += 64) srow[j] = 0.f;
+  } else {
+    for (int j = lane; j < s1; j += 64) srow[j] = 0.f;
+  }
+  for (int i = t; i < POL_LANES * (s2 + s3); i += 1024) h1[i] = 0.f;  // pads of h1/h2
+  __syncthreads();  // (waits for the image's DMA: vmcnt(0) before the barrier)
+  policy_core(p, psm, b0, nimg);
 }
 
 // amx_policy_pack: nn.Linear weights -> the zero-padded LDS image (one thread per float).
@@ -792,6 +861,58 @@ extern "C" int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void*
                   slot_stride, n_slots, stream);
 }
 
+// PolicyArgs of amx_policy_act[_dev] / amx_step_reset_act (ob: null for the fused form, whose
+// input rows come from the step kernel), with their argument checks
+static int make_policy_args(const char* fn, amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
+                            const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
+                            const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
+                            long long stride_m, int ldk, int* row_exp, long long stride_rexp, long long slot_stride,
+                            int n_slots, PolicyArgs& p) {
+  AMX_CHECK_ARG(ctx && blob && act, "%s: null pointer", fn);
+  AMX_CHECK_ARG(amx::aligned16(blob), "%s: blob must be 16-byte aligned", fn);
+  AMX_CHECK_ARG(eval_mode || noise_scale, "%s: noise_scale required unless eval_mode", fn);
+  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH && ctx->S <= POL_MAXH,
+                "%s: S=%d H1=%d H2=%d A=%d (max %d)", fn, ctx->S, H1, H2, ctx->A, POL_MAXH);
+  AMX_CHECK_ARG(B >= 0, "%s: B=%d", fn, B);
+  AMX_CHECK_ARG(!x0_buf || ctx->k0_pad <= POL_X0_COLS, "%s: fused assembly needs k0_pad <= %d (%d)", fn,
+                POL_X0_COLS, ctx->k0_pad);
+  AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
+                            (ctx->M == 1 || stride_m == 0 || stride_m >= (long long)ldk * B)),
+                "%s: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B", fn);
+  AMX_CHECK_ARG(!row_exp || (x0_buf && n_slots >= 1 && n_slots <= 64 && slot_stride >= B &&
+                             (ctx->M == 1 || stride_rexp >= (long long)n_slots * slot_stride)),
+                "%s: row_exp needs x0_buf, 1 <= n_slots <= 64, slot_stride >= B, stride_rexp", fn);
+  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
+  AMX_CHECK_ARG(lds <= 160 * 1024, "%s: S/H too large for LDS staging (%zu B)", fn, lds);
+  p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;
+  p.nscale = noise_scale; p.noise = noise;
+  p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32); p.ctr_lo = (uint32_t)counter;
+  p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode; p.ctr_dev = counter_dev;
+  p.act = act; p.mean_out = mean;
+  p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
+  p.row_exp = row_exp; p.stride_rexp = stride_rexp; p.slot_stride = slot_stride; p.n_slots = n_slots;
+  p.S = ctx->S; p.A = ctx->A; p.B = B;
+  return AMX_OK;
+}
+
+static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
+                      const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
+                      const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
+                      long long stride_m, int ldk, int* row_exp, long long stride_rexp, long long slot_stride,
+                      int n_slots, void* stream) {
+  AMX_CHECK_ARG(ob, "amx_policy_act: null ob");
+  PolicyArgs p;
+  const int rc = make_policy_args("amx_policy_act", ctx, ob, B, blob, H1, H2, noise_scale, noise, seed, counter,
+                                  counter_dev, eval_mode, act, mean, x0_buf, stride_m, ldk, row_exp, stride_rexp,
+                                  slot_stride, n_slots, p);
+  if (rc) return rc;
+  if (B == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_policy, dim3((B + POL_LANES - 1) / POL_LANES), dim3(256), pol_lds_bytes(ctx->S, H1, H2, ctx->A),
+                     (hipStream_t)stream, p);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
 struct ResetArgs {  // amx_step_reset's reset half (amx_reset_lanes' arguments)
   const double* table; int R; const int32_t* rows; uint64_t seed; double* ob_out; int32_t* model_idx;
   int32_t* reset_count; int32_t* row_out; int32_t* steps0_out;
@@ -801,7 +922,7 @@ struct ResetArgs {  // amx_step_reset's reset half (amx_reset_lanes' arguments)
 static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long strideP, const int32_t* model_idx,
                      const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
                      float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, int B, void* stream,
-                     const ResetArgs* rs = nullptr) {
+                     const ResetArgs* rs = nullptr, const PolicyArgs* pa = nullptr) {
   AMX_CHECK_ARG(ctx && ctx->have_term, "amx_step: context has no termination config");
   AMX_CHECK_ARG(preds && model_idx && ob && ob_next && num_steps && done, "amx_step: null pointer");
   AMX_CHECK_ARG(ldp >= ctx->S && B >= 0, "amx_step: ldp=%d B=%d", ldp, B);
@@ -831,6 +952,29 @@ static int step_impl(amx_ctx* ctx, const float* preds, int ldp, long long stride
     a.counter = rs->counter; a.counter_delta = rs->counter_delta; a.ob_rec = rs->ob_rec;
   }
   const int nit = (ctx->S + 63) / 64;
+  if (pa) {  // k_step_act: step t + the policy (and x0 assembly) of step t + 1 on obs[t+1]
+    AMX_CHECK_ARG(rs && !rs->counter && !pa->noise && pa->B == B && nit <= 4,
+                  "amx_step_reset_act: needs the table reset, no counter advance, no injected noise, S <= 256");
+    const size_t lds = pol_lds_bytes(ctx->S, pa->H1, pa->H2, ctx->A) +
+                       (size_t)(pol_image_lds_floats(ctx->S, pa->H1, pa->H2, ctx->A) -
+                                pol_blob_floats(ctx->S, pa->H1, pa->H2, ctx->A)) * sizeof(float);
+    AMX_CHECK_ARG(lds <= 160 * 1024, "amx_step_reset_act: S/H too large for LDS staging (%zu B)", lds);
+    const dim3 grid((B + POL_LANES - 1) / POL_LANES);
+    switch (nit) {
+#define AMX_STEP_ACT_CASE(N)                                                                                       \
+  case N:                                                                                                          \
+    if (ctx->M == 4 && ctx->step_act_w8) hipLaunchKernelGGL((k_step_act<N, true, true>), grid, dim3(1024), lds,     \
+                                                           (hipStream_t)stream, a, *pa);                          \
+    else if (ctx->M == 4) hipLaunchKernelGGL((k_step_act<N, true, false>), grid, dim3(1024), lds, (hipStream_t)stream, \
+                                             a, *pa);                                                              \
+    else hipLaunchKernelGGL((k_step_act<N, false, false>), grid, dim3(1024), lds, (hipStream_t)stream, a, *pa);   \
+    break;
+      AMX_STEP_ACT_CASE(1) AMX_STEP_ACT_CASE(2) AMX_STEP_ACT_CASE(3) AMX_STEP_ACT_CASE(4)
+#undef AMX_STEP_ACT_CASE
+    }
+    AMX_CHECK_LAUNCH();
+    return AMX_OK;
+  }
   switch (nit) {
 #define AMX_STEP_CASE(N)                                                                                 \
   case N:                                                                                                \
@@ -874,6 +1018,27 @@ extern "C" int amx_step_reset(amx_ctx* ctx, const float* preds, int ldp, long lo
                    nonfinite, B, stream, &rs);
 }
 
+extern "C" int amx_step_reset_act(amx_ctx* ctx, const float* preds, int ldp, long long strideP, int32_t* model_idx,
+                                  const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                                  float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, const double* table,
+                                  int R, const int32_t* rows, uint64_t seed, double* ob_out, int32_t* reset_count,
+                                  int32_t* row_out, int32_t* steps0_out, double* ob_rec, const float* blob, int H1,
+                                  int H2, const double* noise_scale, uint64_t policy_seed, uint64_t counter,
+                                  const uint64_t* counter_dev, int eval_mode, double* act, float* mean,
+                                  float* x0_buf, long long stride_m, int ldk, int* row_exp, long long stride_rexp,
+                                  long long slot_stride, int n_slots, int B, void* stream) {
+  AMX_CHECK_ARG(!cost_rexp || cost_in, "amx_step_reset_act: cost_rexp needs cost_in");
+  PolicyArgs p;
+  int rc = make_policy_args("amx_step_reset_act", ctx, nullptr, B, blob, H1, H2, noise_scale, nullptr, policy_seed,
+                            counter, counter_dev, eval_mode, act, mean, x0_buf, stride_m, ldk, row_exp, stride_rexp,
+                            slot_stride, n_slots, p);
+  if (rc) return rc;
+  const ResetArgs rs = {table, R, rows, seed, ob_out, model_idx, reset_count, row_out, steps0_out, nullptr, 0,
+                        ob_rec};
+  return step_impl(ctx, preds, ldp, strideP, model_idx, ob, ob_next, num_steps, done, disc, cost_in, ldc, cost_rexp,
+                   nonfinite, B, stream, &rs, &p);
+}
+
 extern "C" int amx_disagreement(amx_ctx* ctx, const float* preds, int ldp, long long strideP, float* disc, int B,
                                 void* stream) {
   AMX_CHECK_ARG(ctx && preds && disc, "amx_disagreement: null pointer");
@@ -902,7 +1067,7 @@ extern "C" int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* 
 
 extern "C" long long amx_policy_blob_floats(const amx_ctx* ctx, int H1, int H2) {
   if (!ctx || H1 <= 0 || H2 <= 0) return -1;
-  return pol_blob_floats(ctx->S, H1, H2, ctx->A);
+  return pol_image_lds_floats(ctx->S, H1, H2, ctx->A);  // whole 1-KiB pieces (k_step_act's LDS-DMA)
 }
 
 extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, int H1, const float* W2,
@@ -915,42 +1080,6 @@ extern "C" int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, i
   const int n = pol_blob_floats(ctx->S, H1, H2, ctx->A);
   hipLaunchKernelGGL(k_policy_pack, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, W1, b1, H1, W2, b2,
                      H2, W3, b3, ctx->S, ctx->A, blob);
-  AMX_CHECK_LAUNCH();
-  return AMX_OK;
-}
-
-static int policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
-                      const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
-                      const uint64_t* counter_dev, int eval_mode, double* act, float* mean, float* x0_buf,
-                      long long stride_m, int ldk, int* row_exp, long long stride_rexp, long long slot_stride,
-                      int n_slots, void* stream) {
-  AMX_CHECK_ARG(ctx && ob && blob && act, "amx_policy_act: null pointer");
-  AMX_CHECK_ARG(amx::aligned16(blob), "amx_policy_act: blob must be 16-byte aligned");
-  AMX_CHECK_ARG(eval_mode || noise_scale, "amx_policy_act: noise_scale required unless eval_mode");
-  AMX_CHECK_ARG(H1 > 0 && H1 <= POL_MAXH && H2 > 0 && H2 <= POL_MAXH && ctx->A <= POL_MAXH && ctx->S <= POL_MAXH,
-                "amx_policy_act: S=%d H1=%d H2=%d A=%d (max %d)", ctx->S, H1, H2, ctx->A, POL_MAXH);
-  AMX_CHECK_ARG(B >= 0, "amx_policy_act: B=%d", B);
-  AMX_CHECK_ARG(!x0_buf || ctx->k0_pad <= POL_X0_COLS, "amx_policy_act: fused assembly needs k0_pad <= %d (%d)",
-                POL_X0_COLS, ctx->k0_pad);
-  AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
-                            (ctx->M == 1 || stride_m == 0 || stride_m >= (long long)ldk * B)),
-                "amx_policy_act: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B");
-  AMX_CHECK_ARG(!row_exp || (x0_buf && n_slots >= 1 && n_slots <= 64 && slot_stride >= B &&
-                             (ctx->M == 1 || stride_rexp >= (long long)n_slots * slot_stride)),
-                "amx_policy_act: row_exp needs x0_buf, 1 <= n_slots <= 64, slot_stride >= B, stride_rexp");
-  if (B == 0) return AMX_OK;
-  const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
-  AMX_CHECK_ARG(lds <= 160 * 1024, "amx_policy_act: S/H too large for LDS staging (%zu B)", lds);
-  PolicyArgs p;
-  p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;
-  p.nscale = noise_scale; p.noise = noise;
-  p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32); p.ctr_lo = (uint32_t)counter;
-  p.ctr_hi = (uint32_t)(counter >> 32); p.eval_mode = eval_mode; p.ctr_dev = counter_dev;
-  p.act = act; p.mean_out = mean;
-  p.x0 = x0_buf; p.stride_m = stride_m; p.ldk = ldk; p.k0_pad = ctx->k0_pad; p.M = ctx->M; p.norm = ctx->d_norm;
-  p.row_exp = row_exp; p.stride_rexp = stride_rexp; p.slot_stride = slot_stride; p.n_slots = n_slots;
-  p.S = ctx->S; p.A = ctx->A; p.B = B;
-  hipLaunchKernelGGL(k_policy, dim3((B + POL_LANES - 1) / POL_LANES), dim3(256), lds, (hipStream_t)stream, p);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -976,7 +1105,7 @@ extern "C" int amx_policy_act_dev(amx_ctx* ctx, const double* ob, int B, const f
 
 __global__ void k_counter_add(uint64_t* c, long long d) { c[0] += (uint64_t)d; }
 
-// the GPU's constant 100 MHz realtime counter at the point the stream reaches this launch
+// *counter += delta when the stream reaches this launch (a captured rollout's policy counter)
 extern "C" int amx_counter_add(amx_ctx* ctx, uint64_t* counter, long long delta, void* stream) {
   AMX_CHECK_ARG(ctx && counter, "amx_counter_add: null pointer");
   hipLaunchKernelGGL(k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter, delta);
@@ -991,5 +1120,11 @@ extern "C" int amx_philox(amx_ctx* ctx, uint64_t seed, uint32_t ctr1, uint32_t c
   hipLaunchKernelGGL(k_philox, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, (uint32_t)seed,
                      (uint32_t)(seed >> 32), ctr1, ctr2, ctr3, out, n);
   AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_set_step_act_occupancy(amx_ctx* ctx, int two_per_cu) {
+  AMX_CHECK_ARG(ctx, "amx_set_step_act_occupancy: null ctx");
+  ctx->step_act_w8 = two_per_cu ? 1 : 0;
   return AMX_OK;
 }

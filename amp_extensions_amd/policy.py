@@ -56,7 +56,7 @@ class DevicePolicy:
         n = int(c.lib.amx_policy_blob_floats(c.h, self.H1, self.H2))
         if n <= 0:
             raise ValueError("amx_policy_blob_floats failed")
-        self.blob = torch.empty(n, dtype=torch.float32, device=dev)
+        self.blob = torch.zeros(n, dtype=torch.float32, device=dev)  # (the tail past the image: LDS-DMA padding)
         N.check(c.lib.amx_policy_pack(c.h, self.W[0].data_ptr(), self.b[0].data_ptr(), self.H1, self.W[1].data_ptr(),
                                       self.b[1].data_ptr(), self.H2, self.W[2].data_ptr(), self.b[2].data_ptr(),
                                       self.blob.data_ptr(), c.stream), "amx_policy_pack")

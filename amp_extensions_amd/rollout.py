@@ -61,6 +61,12 @@ class RolloutEngine:
         # off: with the MFMA policy and a 16-threads-per-row tail the fused launch takes 28-31 us
         # against 21 + 7 us for policy + separate assembly, no gain; bench --fuse-assembly on)
         self.fuse_assembly = False
+        # rollout(): step t's kernel also runs the policy (+ x0 assembly) of step t + 1 on the
+        # observations it produces (amx_step_reset_act: bit-identical to the separate launches,
+        # tested); needs the fused table reset and the f16x3 shared x0 slice.  Off: measured no
+        # faster than the separate launches (47-56 vs 48 us per step at 8192 lanes)
+        self.fuse_step_act = False
+        self._act_ready = -1      # step whose action + x0 the previous step kernel already wrote
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = c.device
         from .motion import ReferenceMotion
@@ -193,17 +199,27 @@ class RolloutEngine:
         self._scored = 0
 
     def step(self, actions: torch.Tensor | None = None, reset_rows: torch.Tensor | None = None,
-             noise: torch.Tensor | None = None) -> int:
+             noise: torch.Tensor | None = None, act_next: bool = False) -> int:
         """One synchronous step of all lanes; returns the slot index t it was recorded in.
         `actions` [B, A] f64 on device replaces the policy; `noise` [B, A] f64 replaces the
         policy's Philox noise; `reset_rows` [B] i32 forces the rows of lanes that reset.
+        `act_next` (rollout()): the step kernel also computes step t + 1's policy action and
+        ensemble input (amx_step_reset_act) when the configuration allows it.
         A relabel left pending by rollout_overlapped runs between the first step's ensemble
         forward and its step kernel (the forward hides the all-reduce it waits for)."""
         front = self._step_front(actions, noise)
         if front[0] == 0 and self._pending is not None:
             pending, self._pending = self._pending, None
             pending()
-        return self._step_back(front, reset_rows)
+        fuse = act_next and actions is None and noise is None and reset_rows is None and self._can_act_next()
+        return self._step_back(front, reset_rows, act_next=fuse)
+
+    def _can_act_next(self) -> bool:
+        """amx_step_reset_act applies: policy-driven steps, the fused table reset, the f16x3 GEMM's
+        shared x0 slice (the kernel writes x0 once, into model 0's rows), S <= 256."""
+        return (self.fuse_step_act and self.policy is not None and self.auto_reset and self.motion is None
+                and self.fuse_reset and self.ens.W2 is not None and self.ens.shared_x0 and self.ctx.S <= 256
+                and self.t + 1 < self.K)
 
     def _step_front(self, actions, noise):
         """Policy + ensemble forward of step t (everything before the step kernel)."""
@@ -220,9 +236,15 @@ class RolloutEngine:
         self._carry = 0
         ob, ob_next, act = self.obs[src], self.next_obs[t], self.acts[t]
         x0_ready = False
-        if actions is not None:
+        if self._act_ready == t and actions is None and noise is None:
+            # the previous step kernel already wrote this step's action, means and x0
+            x0_ready = True
+            self._act_ready = -1
+        elif actions is not None:
+            self._act_ready = -1
             act.copy_(actions)
         else:
+            self._act_ready = -1
             if self.policy is None:
                 raise RuntimeError("no policy and no actions given")
             if self._graph_ahead and not self._capturing:  # continue after graph replays
@@ -241,13 +263,33 @@ class RolloutEngine:
         preds = self.ens.forward_preds(ob, act, B, x0_ready=x0_ready)
         return t, src, preds
 
-    def _step_back(self, front, reset_rows) -> int:
-        """Step kernel (fp64 update, termination, disagreement, cost row, reset) of step t."""
+    def _step_back(self, front, reset_rows, act_next: bool = False) -> int:
+        """Step kernel (fp64 update, termination, disagreement, cost row, reset) of step t;
+        with act_next also step t + 1's policy action, means and x0 (amx_step_reset_act)."""
         c, B, s = self.ctx, self.B, self.ctx.stream
         t, src, preds = front
         fused = self.auto_reset and self.motion is None and self.fuse_reset
         ob, ob_next = self.obs[src], self.next_obs[t]
-        if fused:  # step + table reset in one pass (amx_step_reset)
+        if fused and act_next:  # step t + policy(t+1) + x0(t+1) in one launch
+            ss = self.cost_type == "ss"
+            pol, ws = self.policy, self.ens.workspace(B)
+            rx = ws["rexp"]
+            N.check(c.lib.amx_step_reset_act(
+                c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(), ob.data_ptr(),
+                ob_next.data_ptr(), self.num_steps.data_ptr(), self.done[t].data_ptr(),
+                self.disc[t].data_ptr() if c.M >= 2 else None, self.cost_in[t].data_ptr() if ss else None, self.kc,
+                self.cost_rexp[t].data_ptr() if ss and self.cost_rexp is not None else None,
+                self.nonfinite[t].data_ptr(), self.table.data_ptr(), self.table.shape[0], None, self.seed,
+                self.obs[t + 1].data_ptr(), self.reset_count.data_ptr(), self.reset_rows[t].data_ptr(),
+                self.steps0.data_ptr() if t == 0 else None, self.obs[0].data_ptr() if src != t else None,
+                pol.blob.data_ptr(), pol.H1, pol.H2, pol.noise_scale.data_ptr(), pol.seed,
+                (t + 1) if self._capturing else (self.step_counter + 1) & 0xFFFFFFFFFFFFFFFF,
+                self.dev_step.data_ptr() if self._capturing else None, int(self.eval_mode), self.acts[t + 1].data_ptr(),
+                None if self.means is None else self.means[t + 1].data_ptr(), ws["act"].data_ptr(), 0, c.ldk,
+                rx.data_ptr(), rx.stride(0), rx.stride(1), rx.shape[1], B, s), "amx_step_reset_act")
+            self._ctr_folded = False
+            self._act_ready = t + 1
+        elif fused:  # step + table reset in one pass (amx_step_reset)
             ss = self.cost_type == "ss"
             # a captured rollout's last step also advances the device policy counter by T
             # (amx_counter_add folded into the step kernel: one graph node fewer)
@@ -321,8 +363,9 @@ class RolloutEngine:
         Returns K*B transitions."""
         K = self.K if K is None else K
         self._rollout_begin()
-        for _ in range(K):
-            self.step()
+        self._act_ready = -1
+        for t in range(K):
+            self.step(act_next=t + 1 < K)
         self.score()
         return K * self.B
 

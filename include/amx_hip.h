@@ -302,6 +302,28 @@ int amx_step_reset(amx_ctx* ctx, const float* preds, int ldp, long long strideP,
                    int32_t* row_out, int32_t* steps0_out, uint64_t* counter, long long counter_delta,
                    double* ob_rec, int B, void* stream);
 
+/* amx_step_reset of step t (no counter advance) fused with the policy of step t + 1 on the
+ * observations it produces (obs[t+1] = ob_out): one launch runs the step of 16 lanes, keeps the
+ * float32 of their obs[t+1] rows on chip and runs amx_policy_act on them (Philox noise with
+ * policy_seed and counter / counter_dev as amx_policy_act[_dev]; no injected noise), writing
+ * act [B][A], mean and the fused x0 / row-exponent assembly exactly as amx_policy_act.  The
+ * results are bit-identical to amx_step_reset followed by amx_policy_act on ob_out (the same
+ * workgroup decomposition of the policy).  Replaces, per rollout step t + 1 > 0, the reference's
+ * get_action call after env.step (mjrl/mjrl/samplers/core.py via milo/milo/sampler.py:48-65).
+ * S <= 256 and a policy image of at most 16384 floats. */
+int amx_step_reset_act(amx_ctx* ctx, const float* preds, int ldp, long long strideP, int32_t* model_idx,
+                       const double* ob, double* ob_next, int32_t* num_steps, uint8_t* done, float* disc,
+                       float* cost_in, int ldc, int* cost_rexp, uint8_t* nonfinite, const double* table,
+                       int R, const int32_t* rows, uint64_t seed, double* ob_out, int32_t* reset_count,
+                       int32_t* row_out, int32_t* steps0_out, double* ob_rec, const float* blob, int H1,
+                       int H2, const double* noise_scale, uint64_t policy_seed, uint64_t counter,
+                       const uint64_t* counter_dev, int eval_mode, double* act, float* mean,
+                       float* x0_buf, long long stride_m, int ldk, int* row_exp, long long stride_rexp,
+                       long long slot_stride, int n_slots, int B, void* stream);
+/* amx_step_reset_act's occupancy, for A/B measurement: 0 (default) one 1024-thread workgroup
+ * per CU at the kernel's natural register count, 1 two per CU (registers capped at 64). */
+int amx_set_step_act_occupancy(amx_ctx* ctx, int two_per_cu);
+
 /* Disagreement only (DynamicsEnsemble.get_action_discrepancy / compute_threshold,
  * milo/milo/dynamics.py:145-165). */
 int amx_disagreement(amx_ctx* ctx, const float* preds, int ldp, long long strideP, float* disc,

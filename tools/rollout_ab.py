@@ -4,7 +4,8 @@ interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
 usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
 variants: "base" (defaults); "s0": one x0 copy per member (DeviceEnsemble.shared_x0 off);
 "r0": separate step + reset launches (RolloutEngine.fuse_reset off); "f0"/"f1": layer-by-layer GEMM launches /
-the fused ensemble forward (DeviceEnsemble.fused).
+the fused ensemble forward (DeviceEnsemble.fused); "a0": separate step and policy launches (RolloutEngine.fuse_step_act
+off); "w8": the fused step + action at two workgroups per CU (amx_set_step_act_occupancy).
 """
 import math
 import os
@@ -43,6 +44,8 @@ def setv(v):
     s = str(v)
     ens.shared_x0 = s != "s0"
     eng.fuse_reset = s != "r0"
+    eng.fuse_step_act = s != "a0"
+    ctx.lib.amx_set_step_act_occupancy(ctx.h, int(s == "w8"))
     if hasattr(ens, "fused"):
         ens.fused = s == "f1" or (s != "f0" and ens.fused_default)
 
