@@ -5,7 +5,8 @@ usage: python tools/rollout_ab.py [lanes] [variants, comma-separated]
 variants: "base" (defaults); "s0": one x0 copy per member (DeviceEnsemble.shared_x0 off);
 "r0": separate step + reset launches (RolloutEngine.fuse_reset off); "f0"/"f1": layer-by-layer GEMM launches /
 the fused ensemble forward (DeviceEnsemble.fused); "a0": separate step and policy launches (RolloutEngine.fuse_step_act
-off); "w8": the fused step + action at two workgroups per CU (amx_set_step_act_occupancy).
+off); "w8": the fused step + action at two workgroups per CU (amx_set_step_act_occupancy); "x1": the policy launch
+writes the ensemble's x0 (RolloutEngine.fuse_assembly).
 """
 import math
 import os
@@ -44,7 +45,8 @@ def setv(v):
     s = str(v)
     ens.shared_x0 = s != "s0"
     eng.fuse_reset = s != "r0"
-    eng.fuse_step_act = s != "a0"
+    eng.fuse_step_act = s in ("a1", "w8")
+    eng.fuse_assembly = s == "x1"
     ctx.lib.amx_set_step_act_occupancy(ctx.h, int(s == "w8"))
     if hasattr(ens, "fused"):
         ens.fused = s == "f1" or (s != "f0" and ens.fused_default)
