@@ -6,7 +6,8 @@ variants: "base" (defaults); "s0": one x0 copy per member (DeviceEnsemble.shared
 "r0": separate step + reset launches (RolloutEngine.fuse_reset off); "f0"/"f1": layer-by-layer GEMM launches /
 the fused ensemble forward (DeviceEnsemble.fused); "a0": separate step and policy launches (RolloutEngine.fuse_step_act
 off); "w8": the fused step + action at two workgroups per CU (amx_set_step_act_occupancy); "x1": the policy launch
-writes the ensemble's x0 (RolloutEngine.fuse_assembly).
+writes the ensemble's x0 (RolloutEngine.fuse_assembly); "t1": the f16x3 forwards time themselves (amx_set_gemm_timer,
+as bench.py's timed region).
 """
 import math
 import os
@@ -47,6 +48,10 @@ def setv(v):
     eng.fuse_reset = s != "r0"
     eng.fuse_step_act = s in ("a1", "w8")
     eng.fuse_assembly = s == "x1"
+    if s == "t1":
+        ctx.gemm_timer()
+    else:
+        ctx.gemm_timer(False)
     ctx.lib.amx_set_step_act_occupancy(ctx.h, int(s == "w8"))
     if hasattr(ens, "fused"):
         ens.fused = s == "f1" or (s != "f0" and ens.fused_default)
