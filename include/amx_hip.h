@@ -392,6 +392,9 @@ int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf);
  * layer runs on row-block tiles.  One launch at a time per context. */
 long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters);
 
+int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
+                            int n_counters);
+
 /* Output-layer tile of the f16x3 forward (amx_gemm_out_unnorm_h3), for A/B measurement:
  * 0 = default = 1, the register-staged 128 x 224 / row-block / 128 x 256 tiles; 2 = the
  * LDS-DMA ring tile (both operands by global_load_lds into a 3-slot ring, two K-tiles ahead)
@@ -399,11 +402,11 @@ long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, i
  * 32 x 112 (S in 193..224); other S fall back to 1.  Identical bits: the ring issues the same
  * limb products per 16 x 16 block in the same K order over the same stream-K segments. */
 int amx_set_out_tile(amx_ctx* ctx, int tile);
-int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
-                            int n_counters);
 
-/* Floats of the packed policy weight image for hidden widths H1, H2 (host query; -1 on a
- * bad argument). */
+/* Floats to allocate for the packed policy weight image for hidden widths H1, H2 (host query;
+ * -1 on a bad argument): the image rounded up to whole 1-KiB pieces, which
+ * amx_step_reset_act copies into LDS by LDS-DMA (amx_policy_pack writes the image, the tail is
+ * never read as weights). */
 long long amx_policy_blob_floats(const amx_ctx* ctx, int H1, int H2);
 
 /* Pack the policy's three nn.Linear layers (W [out][in] row-major f32, b [out]; the
