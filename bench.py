@@ -98,11 +98,15 @@ def parse():
                    help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward (valid "
                         "only while consecutive rollouts share the policy: fixed-policy collection / evaluation; "
                         "a trainer updates the policy between iterations, so the default is the serial order)")
-    p.add_argument("--mode", choices=["engine", "paths"], default="engine",
+    p.add_argument("--mode", choices=["engine", "paths", "train"], default="engine",
                    help="engine: persistent lanes x synchronous steps + device relabel (throughput); paths: the "
                         "reference's semantics through the drop-in surfaces -- sample_points(num_to_collect, "
                         "num_workers=--workers): complete exact-seeded trajectories per worker quota, path dicts "
-                        "on the host -- then relabel_paths (batch_reinforce.py:88-169)")
+                        "on the host -- then relabel_paths (batch_reinforce.py:88-169); train: the engine rollout + "
+                        "relabel followed by the learner half of BatchREINFORCE.train_step on the device -- MLP "
+                        "baseline values, GAE, whitening and the NPG update (10-step CG, kl_dist 0.05) with the "
+                        "sampler's policy refreshed (batch_reinforce.py:170-200, npg_cg.py:113-199); the baseline's "
+                        "Adam fit stays with the caller and is not timed; one rank")
     p.add_argument("--workers", type=int, default=4, help="--mode paths: sampler workers (run.py --num_cpu, default 4)")
     p.add_argument("--motion", default=None, help="--cost amp: character + clip bundle (tools/pack_motion.py)")
     p.add_argument("--dry-run", action="store_true",
@@ -367,6 +371,26 @@ def main():
         return T * B
 
     paths_info = {}
+    if args.mode == "train":
+        # MILO's learner settings (milo/milo/arguments.py:100-122): critic [128, 128], gamma 0.995,
+        # gae_lambda 0.97, cg_iter 10, cg_damping 1e-4, kl_dist 0.05, hvp_sample_frac 1
+        if world > 1:
+            raise SystemExit("bench.py --mode train: one rank (the device NPG reduces over one process's samples)")
+        from amp_extensions_amd.gae import init_mlp_baseline_params
+        baseline = amx.DeviceMLPBaseline(ctx, init_mlp_baseline_params(S, (128, 128), seed=7))
+        npg = amx.DeviceNPG(ctx, pw, log_std, kl_dist=0.05, FIM_invert_args={"iters": 10, "damping": 1e-4},
+                            policy=pol)
+
+        def one_rollout():
+            eng.rollout(T)
+            eng.relabel(allreduce)
+            if args.cost == "mmd":
+                cost.get_expert_cost()
+            adv = eng.advantages(baseline, gamma=0.995, gae_lambda=0.97)["advantages"]
+            info = npg.train_from_engine(eng, adv)
+            paths_info.update(kl=info["kl_dist"], alpha=info["alpha"])
+            return T * B
+
     if args.mode == "paths":
         # the reference's call sequence (batch_reinforce.py:88-90, 103-169): sample_points with W
         # workers' exact-seeded trajectories (path dicts on the host), then the relabel of those
@@ -447,7 +471,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    term_rate = float(eng.done[:T].float().mean().item()) if args.mode == "engine" else None
+    term_rate = float(eng.done[:T].float().mean().item()) if args.mode != "paths" else None
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -516,7 +540,12 @@ def main():
                 "samples_per_rollout": T * B * world, "samples_per_rollout_per_gpu": T * B,
                 "lanes_per_gpu": B, "sync_steps": T,
                 "launch": "eager" if graph is None else "HIP graph replay of the whole rollout",
-                **({} if args.mode == "engine" else {
+                **({} if args.mode != "train" else {
+                    "mode": ("train: rollout + relabel + MLP-baseline values + GAE + whitening + NPG update "
+                             "(VPG, 10-step CG on the Fisher, step, surrogate/KL) + policy refresh per step, all on "
+                             "the device; the baseline's Adam fit is the caller's and is not timed"),
+                    "npg_kl_last": round(float(paths_info.get("kl", 0.0)), 5)}),
+                **({} if args.mode != "paths" else {
                     "mode": (f"reference semantics: sample_points(num_to_collect={per_rank}, num_workers="
                              f"{args.workers}) -> complete exact-seeded trajectories (per-worker quota "
                              f"ceil(N/W)), host path dicts -> relabel_paths; chunks of 8 steps replayed as "
