@@ -15,27 +15,52 @@
 //        log_std block, a diagonal constant, and the damping are added by the caller);
 //   EVAL mean(LR * adv) and mean_kl of new vs old parameters (surr_after, kl_old_new,
 //        npg_cg.py:181-183).
-// Rows are processed in chunks of 32 staged in LDS with the weights; every thread owns a
-// fixed set of gradient entries and accumulates its chunk sums in fp64 registers.
 // Hidden widths are fixed at 32 (MILO's actor_model_hidden, milo/milo/arguments.py:95).
+//
+// Layout (round 3): a block of 8 waves walks its rows in chunks of 32.  Every product is a
+// 16x16 tile on the f32 matrix pipe (v_mfma_f32_16x16x4_f32, an exact f32 fma chain):
+//   * forward layer 1 (K = S, most of the flops): wave w owns the tile (rows 16 (w & 1),
+//     units 16 ((w >> 1) & 1), parameter set w >> 2) and keeps that tile's W1 (or tangent V1)
+//     rows in registers for the whole kernel (16 float4 per lane at S = 256); the chunk's
+//     observations are the only K-long operand in LDS, read as float4s;
+//   * layers 2 / 3 and the back-propagated deltas are 16x16 tiles over K = 32 / A, dealt
+//     over the waves; the tanh derivative of a JVP is applied as its operand is loaded;
+//   * the weight gradients (K = the chunk's rows) are tiles each wave owns across chunks,
+//     summed per chunk in fp32 and accumulated in fp64 registers (as round 2's per-thread
+//     sums); the bias gradients come out of the same tiles through a column of ones next to
+//     the layer's input (x[S] = 1, h[32] = 1: grad b = sum_r delta_r * 1);
+//   * the next chunk's observations / actions / advantages are loaded into registers while
+//     the current chunk computes.
+// Round 2's kernel (scalar LDS FMA loops, 4 waves, 1 chunk-sum per thread) took 431 us per
+// pass at 40960 x 197; see DESIGN.md section 6 for this one's time.
 #include "amx_common.h"
 
 namespace {
 
-constexpr int NH = 32;     // hidden width (both layers)
-constexpr int RC = 32;     // rows per chunk
-constexpr int NT = 256;    // threads per block
-constexpr int MAXS = 256;  // max state dim
-constexpr int MAXA = 64;   // max action dim
-constexpr int HP = NH + 1; // padded row of the [RC][NH] activation tiles
+constexpr int NH = 32;                 // hidden width (both layers)
+constexpr int RC = 32;                 // rows per chunk
+constexpr int NT = 512;                // threads per block: 8 waves, 2 per SIMD
+constexpr int NW = NT / 64;
+constexpr int MAXS = 256;              // max state dim
+constexpr int MAXA = 64;               // max action dim
+constexpr int HS = 52;                 // H1/H2 row stride: 32 units | 1 (ones column) | 0 to 48 | pad
+constexpr int DS = 36;                 // D1/D2 (JVP, then delta) row stride
+constexpr int WS = 36;                 // W2 / W3 LDS row stride
+constexpr int MAXJJ = MAXS / 16;       // float4 W1 fragments per lane
+constexpr int G1SLOTS = (2 * ((MAXS + 16) / 16) + NW - 1) / NW;  // gW1 tiles per wave
+constexpr int G3SLOTS = (3 * (MAXA / 16) + NW - 1) / NW;         // gW3 tiles per wave
+constexpr int XU = MAXS / 16;          // observation values per thread per chunk (16 threads a row)
+constexpr int AU = MAXA / 16;          // action values per thread per chunk
 
 enum { NPG_VPG = 0, NPG_FVP = 1, NPG_EVAL = 2 };
 
+typedef float pf4 __attribute__((ext_vector_type(4)));
+
 struct NpgArgs {
-  int mode, N, S, A, SP;     // SP: odd LDS row stride of W1 / X (conflict-free column reads)
+  int mode, N, S, A;
   int rows_per_block;
-  const void* obs; int obs_f64; long long ldo;
-  const void* act; int act_f64; long long lda;
+  const void* obs; long long ldo;
+  const void* act; long long lda;
   const double* adv;         // VPG / EVAL (whitened advantages)
   const float* theta;        // packed parameters (old, for EVAL)
   const float* vec;          // FVP: tangent; EVAL: new parameters
@@ -50,314 +75,479 @@ struct Lay {  // offsets into the packed parameter vector
   }
 };
 
-// LDS image of one parameter set: W1 [NH][SP], b1, W2 [NH][HP], b2, W3 [A][HP], b3, ls
-struct PSet {
-  float *w1, *b1, *w2, *b2, *w3, *b3, *ls;
+__host__ __device__ inline int npg_stride(int k) {  // LDS row stride (floats) of a [*][k] tile
+  const int r = (k + 3) & ~3;
+  return (r % 8 == 0) ? r + 4 : r;
+}
+
+struct Geo {
+  int S, A, A16, nA, SW, nS, XS, GS, JJ;
+  __host__ __device__ Geo(int S_, int A_) : S(S_), A(A_) {
+    A16 = (A + 15) & ~15;
+    nA = A16 / 16;
+    SW = (S + 16) & ~15;   // gW1 columns: S inputs, the ones column (-> b1), zeros to 16
+    nS = SW / 16;
+    XS = npg_stride(SW);
+    GS = npg_stride(A16);
+    JJ = (S + 15) / 16;    // layer-1 K steps of 16 (one float4 per lane each)
+  }
 };
+
+// LDS image of one parameter set's small part (W1 lives in registers)
+struct Small {
+  float *w2, *b2, *w3, *b3, *b1, *ls;
+};
+
+__host__ __device__ inline int r4(int n) { return (n + 3) & ~3; }
+
+__host__ __device__ inline int small_floats(const Geo& g) {
+  return r4(NH * WS) + r4(NH) + r4(g.A16 * WS) + r4(g.A16) + r4(NH) + r4(g.A16);
+}
 
 __device__ inline float* carve(float*& p, int n) {
   float* r = p;
-  p += (n + 3) & ~3;
+  p += r4(n);
   return r;
 }
 
-__device__ inline void load_params(const float* __restrict__ src, const Lay& L, int S, int A, int SP, PSet& d) {
-  for (int e = threadIdx.x; e < NH * S; e += NT) d.w1[(e / S) * SP + e % S] = src[L.w1 + e];
-  for (int e = threadIdx.x; e < NH * NH; e += NT) d.w2[(e / NH) * HP + e % NH] = src[L.w2 + e];
-  for (int e = threadIdx.x; e < A * NH; e += NT) d.w3[(e / NH) * HP + e % NH] = src[L.w3 + e];
+__device__ inline Small carve_small(float*& p, const Geo& g) {
+  Small s;
+  s.w2 = carve(p, NH * WS); s.b2 = carve(p, NH); s.w3 = carve(p, g.A16 * WS);
+  s.b3 = carve(p, g.A16); s.b1 = carve(p, NH); s.ls = carve(p, g.A16);
+  return s;
+}
+
+__device__ inline void load_small(const float* __restrict__ src, const Lay& L, const Geo& g, const Small& d) {
+  for (int e = threadIdx.x; e < NH * NH; e += NT) d.w2[(e >> 5) * WS + (e & 31)] = src[L.w2 + e];
+  for (int e = threadIdx.x; e < g.A16 * NH; e += NT) {
+    const int r = e >> 5;
+    d.w3[r * WS + (e & 31)] = r < g.A ? src[L.w3 + e] : 0.f;
+  }
   for (int e = threadIdx.x; e < NH; e += NT) {
     d.b1[e] = src[L.b1 + e];
     d.b2[e] = src[L.b2 + e];
   }
-  for (int e = threadIdx.x; e < A; e += NT) {
-    d.b3[e] = src[L.b3 + e];
-    d.ls[e] = src[L.ls + e];
+  for (int e = threadIdx.x; e < g.A16; e += NT) {
+    d.b3[e] = e < g.A ? src[L.b3 + e] : 0.f;
+    d.ls[e] = e < g.A ? src[L.ls + e] : 0.f;
   }
 }
 
-// out[r][j] = act(b[j] + sum_k W[j][k] in[r][k]) for r < RC, j < NH; thread: j = t&31,
-// rows rg + 8q.  in row stride ldi, W row stride ldw.  Returns the pre-activation sums via
-// the callback order used by the caller.
-__device__ inline void dense_nh(const float* W, int ldw, const float* b, const float* in, int ldi, int K, float (&acc)[4]) {
-  const int j = threadIdx.x & 31, rg = threadIdx.x >> 5;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = b ? b[j] : 0.f;
-  for (int k = 0; k < K; ++k) {
-    const float w = W[j * ldw + k];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = fmaf(w, in[(rg + 8 * q) * ldi + k], acc[q]);
-  }
+__device__ __forceinline__ pf4 mma(float a, float b, pf4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+template <int MODE, typename TO, typename TA>
 __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  const int S = a.S, A = a.A, SP = a.SP, t = threadIdx.x;
-  const Lay L(S, A);
+  const Geo g(a.S, a.A);
+  const Lay L(a.S, a.A);
+  const int S = g.S, A = g.A;
+  constexpr int mode = MODE;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = lane & 15, kq = lane >> 4;
+  const bool two = mode != NPG_VPG;
   float* p = sm;
-  PSet th, tv;
-  th.w1 = carve(p, NH * SP); th.b1 = carve(p, NH); th.w2 = carve(p, NH * HP); th.b2 = carve(p, NH);
-  th.w3 = carve(p, A * HP); th.b3 = carve(p, A); th.ls = carve(p, A);
-  const bool two = a.mode != NPG_VPG;
-  if (two) {
-    tv.w1 = carve(p, NH * SP); tv.b1 = carve(p, NH); tv.w2 = carve(p, NH * HP); tv.b2 = carve(p, NH);
-    tv.w3 = carve(p, A * HP); tv.b3 = carve(p, A); tv.ls = carve(p, A);
+  const Small th = carve_small(p, g);
+  Small tv = th;
+  if (two) tv = carve_small(p, g);
+  float* X = carve(p, RC * g.XS);     // [32][XS]: S observations | 1 | zeros
+  float* H1 = carve(p, RC * HS);      // tanh activations | 1 | zeros
+  float* H2 = carve(p, RC * HS);
+  float* D1 = carve(p, RC * DS);      // FVP: tangent pre-activation (V1 x + vb1); EVAL: new h1; then delta
+  float* D2 = carve(p, RC * DS);
+  float* M = carve(p, RC * g.GS);     // mean (EVAL), z (VPG)
+  float* G = carve(p, RC * g.GS);     // output-layer gradient (VPG / FVP), new mean (EVAL)
+  float* ACT = carve(p, RC * A);
+  double* ADV = reinterpret_cast<double*>(carve(p, 2 * RC));
+  float* CF = carve(p, g.A16);        // FVP: 2 / (2 sigma^2 + 1e-8)
+
+  load_small(a.theta, L, g, th);
+  if (two) load_small(a.vec, L, g, tv);
+  {
+    const int xp = g.XS - S;
+    for (int e = t; e < RC * xp; e += NT) {
+      const int r = e / xp, c = S + e % xp;
+      X[r * g.XS + c] = c == S ? 1.f : 0.f;
+    }
+    for (int e = t; e < RC * (HS - NH); e += NT) {
+      const int r = e / (HS - NH), c = NH + e % (HS - NH);
+      H1[r * HS + c] = c == NH ? 1.f : 0.f;
+      H2[r * HS + c] = c == NH ? 1.f : 0.f;
+    }
+    if (mode == NPG_FVP)
+      for (int e = t; e < g.A16; e += NT) {
+        const float sd = e < A ? expf(a.theta[L.ls + e]) : 1.f;
+        CF[e] = 2.f / (2.f * sd * sd + 1e-8f);
+      }
   }
-  float* X = carve(p, RC * SP);
-  float* H1 = carve(p, RC * HP);
-  float* H2 = carve(p, RC * HP);
-  float* D1 = carve(p, RC * HP);   // FVP: JVP of layer 1, then the backward delta
-  float* D2 = carve(p, RC * HP);
-  float* G = carve(p, RC * MAXA);  // output-layer gradient (or, EVAL: new mean)
-  float* M = carve(p, RC * MAXA);  // mean (or JVP of the mean)
-  double* red = reinterpret_cast<double*>(carve(p, 2 * 2 * NT));
 
-  load_params(a.theta, L, S, A, SP, th);
-  if (two) load_params(a.vec, L, S, A, SP, tv);
+  // this wave's layer-1 tile: rows 16 rb1, units 16 cb1, parameter set mat1 (VPG: waves 0-3)
+  const int n1 = two ? 8 : 4;
+  const bool f1 = wave < n1;
+  const int rb1 = wave & 1, cb1 = (wave >> 1) & 1, mat1 = wave >> 2;
+  pf4 wf[MAXJJ];
+  {
+    const float* wrow = ((f1 && mat1) ? a.vec : a.theta) + L.w1 + (cb1 * 16 + i) * S;
+#pragma unroll
+    for (int jj = 0; jj < MAXJJ; ++jj) {
+      pf4 v = {0.f, 0.f, 0.f, 0.f};
+      if (f1 && jj < g.JJ) {
+        const int k0 = 4 * (kq + 4 * jj);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (k0 + e < S) v[e] = wrow[k0 + e];
+      }
+      wf[jj] = v;
+    }
+  }
 
-  // gradient accumulators owned by this thread (fp64)
-  double gw1[MAXS / 8], gw2[NH * NH / NT], gw3[MAXA * NH / NT], gb = 0.0;
+  // next chunk's inputs, held in registers while the current chunk computes: thread t stages
+  // row t / 16, columns t % 16 + 16 u (affine in u: one address register per array)
+  TO xv[XU];
+  TA av[AU];
+  double dv = 0.0;
+  const int pr = t >> 4, pc = t & 15;
+  const bool need_act = mode != NPG_FVP;
+  auto prefetch = [&](int c0, int nr) {
+    const bool rv = pr < nr;
+    const TO* xs = static_cast<const TO*>(a.obs) + (long long)(c0 + (rv ? pr : 0)) * a.ldo + pc;
 #pragma unroll
-  for (int m = 0; m < MAXS / 8; ++m) gw1[m] = 0.0;
+    for (int u = 0; u < XU; ++u) xv[u] = (rv && pc + 16 * u < S) ? xs[16 * u] : TO(0);
+    if (need_act) {
+      const TA* as = static_cast<const TA*>(a.act) + (long long)(c0 + (rv ? pr : 0)) * a.lda + pc;
 #pragma unroll
-  for (int m = 0; m < NH * NH / NT; ++m) gw2[m] = 0.0;
+      for (int u = 0; u < AU; ++u) av[u] = (rv && pc + 16 * u < A) ? as[16 * u] : TA(0);
+      if (t < RC) dv = t < nr ? a.adv[c0 + t] : 0.0;
+    }
+  };
+  auto stash = [&]() {
+    float* xd = X + pr * g.XS + pc;
 #pragma unroll
-  for (int m = 0; m < MAXA * NH / NT; ++m) gw3[m] = 0.0;
-  double ev_surr = 0.0, ev_kl = 0.0;
+    for (int u = 0; u < XU; ++u)
+      if (pc + 16 * u < S) xd[16 * u] = (float)xv[u];  // np.float32(observation)
+    if (need_act) {
+      float* ad = ACT + pr * A + pc;
+#pragma unroll
+      for (int u = 0; u < AU; ++u)
+        if (pc + 16 * u < A) ad[16 * u] = (float)av[u];
+      if (t < RC) ADV[t] = dv;
+    }
+  };
+
+  double g1[G1SLOTS][4], g3[G3SLOTS][4], g2[4], gls = 0.0, ev_surr = 0.0, ev_kl = 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int s = 0; s < G1SLOTS; ++s) g1[s][r] = 0.0;
+#pragma unroll
+    for (int s = 0; s < G3SLOTS; ++s) g3[s][r] = 0.0;
+    g2[r] = 0.0;
+  }
   const double invN = 1.0 / (double)a.N;
-
   const int r0 = blockIdx.x * a.rows_per_block;
   const int r1 = min(a.N, r0 + a.rows_per_block);
+  if (r0 < r1) prefetch(r0, min(RC, r1 - r0));
+
   for (int c0 = r0; c0 < r1; c0 += RC) {
+    // per-chunk opaque copies of the lane indices and strides: keeps the compiler from hoisting
+    // every chunk-invariant LDS address out of the loop (hundreds of registers held live)
+    int i_ = i, kq_ = kq, xs_ = g.XS, gs_ = g.GS;
+    asm volatile("" : "+v"(i_), "+v"(kq_));
+    asm volatile("" : "+s"(xs_), "+s"(gs_));
+    const int i = i_, kq = kq_, XS = xs_, GS = gs_;
     const int nr = min(RC, r1 - c0);
-    __syncthreads();  // previous chunk's tiles are consumed (and the parameters are loaded)
-    for (int e = t; e < RC * S; e += NT) {
-      const int r = e / S, k = e % S;
-      float v = 0.f;
-      if (r < nr) {
-        const long long off = (long long)(c0 + r) * a.ldo + k;
-        v = a.obs_f64 ? (float)static_cast<const double*>(a.obs)[off] : static_cast<const float*>(a.obs)[off];
+    __syncthreads();  // the previous chunk is consumed (first chunk: parameters and pads are stored)
+    stash();
+    if (c0 + RC < r1) prefetch(c0 + RC, min(RC, r1 - c0 - RC));
+    __syncthreads();
+
+    // ---- layer 1: H1 = tanh(X W1^T + b1); FVP: D1 = X V1^T + vb1; EVAL: D1 = tanh(X V1n^T + b1n)
+    if (f1) {
+      const float* xr = X + (rb1 * 16 + i) * XS + 4 * kq;
+      pf4 ca = {0.f, 0.f, 0.f, 0.f}, cb = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int jj = 0; jj < MAXJJ; ++jj) {
+        if (jj < g.JJ) {
+          const pf4 x = *reinterpret_cast<const pf4*>(xr + 16 * jj);
+          ca = mma(x.x, wf[jj].x, ca);
+          cb = mma(x.y, wf[jj].y, cb);
+          ca = mma(x.z, wf[jj].z, ca);
+          cb = mma(x.w, wf[jj].w, cb);
+        }
       }
-      X[r * SP + k] = v;
-    }
-    __syncthreads();
-    // ---- forward (and, FVP, the tangent) of the two tanh layers --------------------------
-    const int j = t & 31, rg = t >> 5;
-    float acc[4], dac[4];
-    dense_nh(th.w1, SP, th.b1, X, SP, S, acc);
-    if (a.mode == NPG_FVP) dense_nh(tv.w1, SP, tv.b1, X, SP, S, dac);
+      const int col = cb1 * 16 + i;
+      const float bias = (mat1 ? tv.b1 : th.b1)[col];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float h = tanhf(acc[q]);
-      H1[(rg + 8 * q) * HP + j] = h;
-      if (a.mode == NPG_FVP) D1[(rg + 8 * q) * HP + j] = dac[q] * (1.f - h * h);
-    }
-    if (a.mode == NPG_EVAL) {  // second forward with the new parameters into D1
-      dense_nh(tv.w1, SP, tv.b1, X, SP, S, dac);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) D1[(rg + 8 * q) * HP + j] = tanhf(dac[q]);
-    }
-    __syncthreads();
-    dense_nh(th.w2, HP, th.b2, H1, HP, NH, acc);
-    if (a.mode == NPG_FVP) {
-      float d2[4], d3[4];
-      dense_nh(tv.w2, HP, tv.b2, H1, HP, NH, d2);     // vW2 h1 + vb2
-      dense_nh(th.w2, HP, nullptr, D1, HP, NH, d3);   // W2 dh1
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dac[q] = d2[q] + d3[q];
-    } else if (a.mode == NPG_EVAL) {
-      dense_nh(tv.w2, HP, tv.b2, D1, HP, NH, dac);
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float h = tanhf(acc[q]);
-      H2[(rg + 8 * q) * HP + j] = h;
-      if (a.mode == NPG_FVP) D2[(rg + 8 * q) * HP + j] = dac[q] * (1.f - h * h);
-      if (a.mode == NPG_EVAL) D2[(rg + 8 * q) * HP + j] = tanhf(dac[q]);
-    }
-    __syncthreads();
-    // ---- output layer: mean (M); FVP: JVP of the mean (M); EVAL: new mean (G) ---------------
-    for (int e = t; e < RC * A; e += NT) {
-      const int r = e / A, d = e % A;
-      float m = th.b3[d];
-      for (int k = 0; k < NH; ++k) m = fmaf(th.w3[d * HP + k], H2[r * HP + k], m);
-      if (a.mode == NPG_FVP) {
-        float v1 = tv.b3[d], v2 = 0.f;
-        for (int k = 0; k < NH; ++k) v1 = fmaf(tv.w3[d * HP + k], H2[r * HP + k], v1);
-        for (int k = 0; k < NH; ++k) v2 = fmaf(th.w3[d * HP + k], D2[r * HP + k], v2);
-        m = v1 + v2;
-      } else if (a.mode == NPG_EVAL) {
-        float mn = tv.b3[d];
-        for (int k = 0; k < NH; ++k) mn = fmaf(tv.w3[d * HP + k], D2[r * HP + k], mn);
-        G[r * MAXA + d] = mn;
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb1 * 16 + 4 * kq + r;
+        const float z = (ca[r] + cb[r]) + bias;
+        if (!mat1) H1[row * HS + col] = tanhf(z);
+        else D1[row * DS + col] = mode == NPG_EVAL ? tanhf(z) : z;  // FVP: tanh' applied on use
       }
-      M[r * MAXA + d] = m;
     }
     __syncthreads();
-    if (a.mode == NPG_EVAL) {
+
+    // ---- layer 2 (same tile per wave): H2 = tanh(H1 W2^T + b2);
+    //      FVP: D2 = H1 V2^T + (D1 (1 - H1^2)) W2^T + vb2; EVAL: D2 = tanh(D1 V2n^T + b2n)
+    if (f1) {
+      const int rowA = rb1 * 16 + i, u = cb1 * 16 + i;
+      pf4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+      if (!mat1) {
+#pragma unroll
+        for (int s = 0; s < NH / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(H1[rowA * HS + k], th.w2[u * WS + k], acc);
+        }
+      } else if (mode == NPG_FVP) {
+#pragma unroll
+        for (int s = 0; s < NH / 4; ++s) {
+          const int k = 4 * s + kq;
+          const float h = H1[rowA * HS + k];
+          acc = mma(h, tv.w2[u * WS + k], acc);
+          acc2 = mma(D1[rowA * DS + k] * (1.f - h * h), th.w2[u * WS + k], acc2);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < NH / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(D1[rowA * DS + k], tv.w2[u * WS + k], acc);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb1 * 16 + 4 * kq + r;
+        if (!mat1) H2[row * HS + u] = tanhf(acc[r] + th.b2[u]);
+        else if (mode == NPG_FVP) D2[row * DS + u] = (acc[r] + acc2[r]) + tv.b2[u];
+        else D2[row * DS + u] = tanhf(acc[r] + tv.b2[u]);
+      }
+    }
+    __syncthreads();
+
+    // ---- output layer: VPG mean -> G (and z -> M); FVP JVP of the mean -> G; EVAL M, new mean G
+    {
+      const int n3 = mode == NPG_EVAL ? 4 * g.nA : 2 * g.nA;
+      for (int it = wave; it < n3; it += NW) {
+        const int rb = it & 1, cbk = (it >> 1) % g.nA, mat = it / (2 * g.nA);
+        const int rowA = rb * 16 + i, u = cbk * 16 + i;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+        if (mode == NPG_FVP) {
+#pragma unroll
+          for (int s = 0; s < NH / 4; ++s) {
+            const int k = 4 * s + kq;
+            const float h = H2[rowA * HS + k];
+            acc = mma(h, tv.w3[u * WS + k], acc);
+            acc2 = mma(D2[rowA * DS + k] * (1.f - h * h), th.w3[u * WS + k], acc2);
+          }
+        } else if (!mat) {
+#pragma unroll
+          for (int s = 0; s < NH / 4; ++s) {
+            const int k = 4 * s + kq;
+            acc = mma(H2[rowA * HS + k], th.w3[u * WS + k], acc);
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < NH / 4; ++s) {
+            const int k = 4 * s + kq;
+            acc = mma(D2[rowA * DS + k], tv.w3[u * WS + k], acc);
+          }
+        }
+        const int d = u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * kq + r;
+          const bool ok = row < nr && d < A;
+          if (mode == NPG_FVP) {
+            const float m = (acc[r] + acc2[r]) + tv.b3[d];
+            G[row * GS + d] = ok ? (float)((double)(m * CF[d]) * invN) : 0.f;
+          } else if (mode == NPG_VPG) {
+            const float m = acc[r] + th.b3[d];
+            float gg = 0.f, z = 0.f;
+            if (ok) {
+              const float sd = expf(th.ls[d]);
+              z = (ACT[row * A + d] - m) / sd;
+              gg = (float)(ADV[row] * invN) * (z / sd);
+            }
+            G[row * GS + d] = gg;
+            M[row * GS + d] = z;
+          } else {
+            (mat ? G : M)[row * GS + d] = acc[r] + (mat ? tv.b3 : th.b3)[d];
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    if (mode == NPG_EVAL) {
       // per row: LL_new - LL_old and sample_kl (gaussian_mlp.py:110-155), one thread per row
       if (t < nr) {
         const int r = t;
-        const long long ro = (long long)(c0 + r);
         float dll = 0.f, kl = 0.f, sls_o = 0.f, sls_n = 0.f;
         for (int d = 0; d < A; ++d) {
-          const float ac = a.act_f64 ? (float)static_cast<const double*>(a.act)[ro * a.lda + d]
-                                     : static_cast<const float*>(a.act)[ro * a.lda + d];
+          const float ac = ACT[r * A + d];
+          const float mo = M[r * GS + d], mn = G[r * GS + d];
           const float so = expf(th.ls[d]), sn = expf(tv.ls[d]);
-          const float zo = (ac - M[r * MAXA + d]) / so, zn = (ac - G[r * MAXA + d]) / sn;
+          const float zo = (ac - mo) / so, zn = (ac - mn) / sn;
           dll += -0.5f * zn * zn - (-0.5f * zo * zo);
           sls_o += th.ls[d];
           sls_n += tv.ls[d];
-          const float dm = M[r * MAXA + d] - G[r * MAXA + d];
+          const float dm = mo - mn;
           const float Nr = dm * dm + so * so - sn * sn, Dr = 2.f * sn * sn + 1e-8f;
           kl += Nr / Dr + tv.ls[d] - th.ls[d];
         }
         dll += -sls_n + sls_o;
-        ev_surr += (double)(expf(dll) * (float)a.adv[ro]);
+        ev_surr += (double)(expf(dll) * (float)ADV[r]);
         ev_kl += (double)kl;
       }
       continue;
     }
-    // ---- output-layer gradient G [RC][A] ---------------------------------------------------
-    for (int e = t; e < RC * A; e += NT) {
-      const int r = e / A, d = e % A;
-      float g = 0.f;
-      if (r < nr) {
-        const float sd = expf(th.ls[d]);
-        if (a.mode == NPG_VPG) {
-          const long long ro = (long long)(c0 + r);
-          const float ac = a.act_f64 ? (float)static_cast<const double*>(a.act)[ro * a.lda + d]
-                                     : static_cast<const float*>(a.act)[ro * a.lda + d];
-          const float z = (ac - M[r * MAXA + d]) / sd;
-          g = (float)(a.adv[ro] * invN) * (z / sd);
-        } else {
-          const float c = 2.f / (2.f * sd * sd + 1e-8f);
-          g = (float)((double)(M[r * MAXA + d] * c) * invN);
+
+    // ---- back-propagation, output layer: gW3 | b3 (owned tiles, K = rows);
+    //      D2 = (G W3)(1 - H2^2) (tiles from the last wave down); VPG: log_std sums (wave 3)
+#pragma unroll
+    for (int sl = 0; sl < G3SLOTS; ++sl) {
+      const int q = wave + NW * sl;
+      if (q < 3 * g.nA) {
+        const int mb = q / 3, nb = q % 3;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < RC / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(G[k * GS + mb * 16 + i], H2[k * HS + nb * 16 + i], acc);
         }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g3[sl][r] += (double)acc[r];
       }
-      G[r * MAXA + d] = g;
     }
-    // log_std gradient (VPG): sum_r adv/N (z^2 - 1), threads [128, 128 + A)
-    if (a.mode == NPG_VPG && t >= 128 && t < 128 + A) {
-      const int d = t - 128;
-      const float sd = expf(th.ls[d]);
+    if (NW - 1 - wave < 4) {
+      const int it = NW - 1 - wave, rb = it & 1, cbk = it >> 1;
+      const int rowA = rb * 16 + i, col = cbk * 16 + i;
+      pf4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < g.A16 / 4; ++s) {
+        const int k = 4 * s + kq;
+        acc = mma(G[rowA * GS + k], th.w3[k * WS + col], acc);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * 16 + 4 * kq + r;
+        const float h = H2[row * HS + col];
+        D2[row * DS + col] = acc[r] * (1.f - h * h);
+      }
+    }
+    if (mode == NPG_VPG && t >= 192 && t < 192 + A) {
+      const int d = t - 192;
       for (int r = 0; r < nr; ++r) {
-        const long long ro = (long long)(c0 + r);
-        const float ac = a.act_f64 ? (float)static_cast<const double*>(a.act)[ro * a.lda + d]
-                                   : static_cast<const float*>(a.act)[ro * a.lda + d];
-        const float z = (ac - M[r * MAXA + d]) / sd;
-        gb += a.adv[ro] * invN * (double)(z * z - 1.f);
+        const float z = M[r * GS + d];
+        gls += ADV[r] * invN * (double)(z * z - 1.f);
       }
     }
     __syncthreads();
-    // ---- backward ------------------------------------------------------------------------
-    // gW3[d][k] += sum_r G[r][d] H2[r][k]; entries e = t + NT*m (d = e>>5, k = e&31)
+
+    // ---- layer 2: gW2 | b2 (waves 0-5); D1 = (D2 W2)(1 - H1^2) (waves 7-4)
+    if (wave < 6) {
+      const int mb = wave / 3, nb = wave % 3;
+      pf4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int m = 0; m < MAXA * NH / NT; ++m) {
-      const int e = t + NT * m, d = e >> 5, k = e & 31;
-      if (d < A) {
-        float s = 0.f;
-        for (int r = 0; r < nr; ++r) s = fmaf(G[r * MAXA + d], H2[r * HP + k], s);
-        gw3[m] += (double)s;
+      for (int s = 0; s < RC / 4; ++s) {
+        const int k = 4 * s + kq;
+        acc = mma(D2[k * DS + mb * 16 + i], H1[k * HS + nb * 16 + i], acc);
       }
-    }
-    if (t >= 64 && t < 64 + A) {  // gb3
-      float s = 0.f;
-      for (int r = 0; r < nr; ++r) s += G[r * MAXA + (t - 64)];
-      gb += (double)s;
-    }
-    // D2[r][j] = (sum_d G[r][d] W3[d][j]) (1 - H2^2)
-    {
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int d = 0; d < A; ++d) {
-        const float w = th.w3[d * HP + j];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s[q] = fmaf(G[(rg + 8 * q) * MAXA + d], w, s[q]);
+      for (int r = 0; r < 4; ++r) g2[r] += (double)acc[r];
+    }
+    if (NW - 1 - wave < 4) {
+      const int it = NW - 1 - wave, rb = it & 1, cbk = it >> 1;
+      const int rowA = rb * 16 + i, col = cbk * 16 + i;
+      pf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NH / 4; ++s) {
+        const int k = 4 * s + kq;
+        acc = mma(D2[rowA * DS + k], th.w2[k * WS + col], acc);
       }
-      __syncthreads();  // D2 (JVP) was read by the output layer above
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float h = H2[(rg + 8 * q) * HP + j];
-        D2[(rg + 8 * q) * HP + j] = s[q] * (1.f - h * h);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < NH * NH / NT; ++m) {  // gW2[jj][i] += sum_r D2[r][jj] H1[r][i]
-      const int e = t + NT * m, jj = e >> 5, i = e & 31;
-      float s = 0.f;
-      for (int r = 0; r < nr; ++r) s = fmaf(D2[r * HP + jj], H1[r * HP + i], s);
-      gw2[m] += (double)s;
-    }
-    if (t >= 32 && t < 64) {  // gb2
-      float s = 0.f;
-      for (int r = 0; r < nr; ++r) s += D2[r * HP + (t - 32)];
-      gb += (double)s;
-    }
-    {  // D1[r][i] = (sum_jj D2[r][jj] W2[jj][i]) (1 - H1^2)
-      float s[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int jj = 0; jj < NH; ++jj) {
-        const float w = th.w2[jj * HP + j];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) s[q] = fmaf(D2[(rg + 8 * q) * HP + jj], w, s[q]);
-      }
-      __syncthreads();  // D1 (JVP) was read by layer 2 above
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float h = H1[(rg + 8 * q) * HP + j];
-        D1[(rg + 8 * q) * HP + j] = s[q] * (1.f - h * h);
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * 16 + 4 * kq + r;
+        const float h = H1[row * HS + col];
+        D1[row * DS + col] = acc[r] * (1.f - h * h);
       }
     }
     __syncthreads();
+
+    // ---- layer 1: gW1 | b1 (owned tiles)
 #pragma unroll
-    for (int m = 0; m < MAXS / 8; ++m) {  // gW1[i][k] += sum_r D1[r][i] X[r][k], i = t&31, k = rg + 8m
-      const int k = rg + 8 * m;
-      if (k < S) {
-        float s = 0.f;
-        for (int r = 0; r < nr; ++r) s = fmaf(D1[r * HP + j], X[r * SP + k], s);
-        gw1[m] += (double)s;
+    for (int sl = 0; sl < G1SLOTS; ++sl) {
+      const int q = wave + NW * sl;
+      if (q < 2 * g.nS) {
+        const int mb = q & 1, nb = q >> 1;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < RC / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(D1[k * DS + mb * 16 + i], X[k * XS + nb * 16 + i], acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) g1[sl][r] += (double)acc[r];
       }
-    }
-    if (t < 32) {  // gb1
-      float s = 0.f;
-      for (int r = 0; r < nr; ++r) s += D1[r * HP + t];
-      gb += (double)s;
     }
   }
 
-  if (a.mode == NPG_EVAL) {
+  if (mode == NPG_EVAL) {
     // block sums of (surr, kl) in fixed order
+    __syncthreads();
+    double* red = reinterpret_cast<double*>(H1);  // the activation tiles are free now
     red[t] = ev_surr;
     red[NT + t] = ev_kl;
     __syncthreads();
     if (t == 0) {
       double s0 = 0.0, s1 = 0.0;
-      for (int i = 0; i < NT; ++i) {
-        s0 += red[i];
-        s1 += red[NT + i];
+      for (int e = 0; e < NT; ++e) {
+        s0 += red[e];
+        s1 += red[NT + e];
       }
       a.partials[2LL * blockIdx.x] = s0;
       a.partials[2LL * blockIdx.x + 1] = s1;
     }
     return;
   }
+  // tile element (row 16 mb + 4 kq + r, column 16 nb + i); the ones column is the bias
   double* out = a.partials + (long long)blockIdx.x * a.P;
-  const int j = t & 31, rg = t >> 5;
 #pragma unroll
-  for (int m = 0; m < MAXS / 8; ++m) {
-    const int k = rg + 8 * m;
-    if (k < S) out[L.w1 + j * S + k] = gw1[m];
+  for (int sl = 0; sl < G1SLOTS; ++sl) {
+    const int q = wave + NW * sl;
+    if (q < 2 * g.nS) {
+      const int mb = q & 1, nb = q >> 1, k = nb * 16 + i;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = mb * 16 + 4 * kq + r;
+        if (k < S) out[L.w1 + j * S + k] = g1[sl][r];
+        else if (k == S) out[L.b1 + j] = g1[sl][r];
+      }
+    }
+  }
+  if (wave < 6) {
+    const int mb = wave / 3, nb = wave % 3, k = nb * 16 + i;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = mb * 16 + 4 * kq + r;
+      if (k < NH) out[L.w2 + j * NH + k] = g2[r];
+      else if (k == NH) out[L.b2 + j] = g2[r];
+    }
   }
 #pragma unroll
-  for (int m = 0; m < NH * NH / NT; ++m) out[L.w2 + t + NT * m] = gw2[m];
+  for (int sl = 0; sl < G3SLOTS; ++sl) {
+    const int q = wave + NW * sl;
+    if (q < 3 * g.nA) {
+      const int mb = q / 3, nb = q % 3, k = nb * 16 + i;
 #pragma unroll
-  for (int m = 0; m < MAXA * NH / NT; ++m) {
-    const int e = t + NT * m;
-    if ((e >> 5) < A) out[L.w3 + e] = gw3[m];
+      for (int r = 0; r < 4; ++r) {
+        const int d = mb * 16 + 4 * kq + r;
+        if (d < A) {
+          if (k < NH) out[L.w3 + d * NH + k] = g3[sl][r];
+          else if (k == NH) out[L.b3 + d] = g3[sl][r];
+        }
+      }
+    }
   }
-  if (t < 32) out[L.b1 + t] = gb;
-  else if (t < 64) out[L.b2 + t - 32] = gb;
-  else if (t < 64 + A) out[L.b3 + t - 64] = gb;
-  else if (t >= 128 && t < 128 + A) out[L.ls + t - 128] = a.mode == NPG_VPG ? gb : 0.0;
+  if (t >= 192 && t < 192 + A) out[L.ls + t - 192] = mode == NPG_VPG ? gls : 0.0;
 }
 
 // out[c] = sum_b partials[b][c] in a fixed order (deterministic): stage 1 sums runs of RB
@@ -380,11 +570,10 @@ __global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, dou
 }
 
 size_t npg_lds_bytes(int S, int A, int mode) {
-  const int SP = (S | 1);
-  auto r4 = [](int n) { return (size_t)((n + 3) & ~3); };
-  const size_t pset = r4(NH * SP) + r4(NH) + r4(NH * HP) + r4(NH) + r4(A * HP) + r4(A) + r4(A);
-  return sizeof(float) * (pset * (mode == NPG_VPG ? 1 : 2) + r4(RC * SP) + 4 * r4(RC * HP) + 2 * r4(RC * MAXA) +
-                          r4(4 * NT));
+  const Geo g(S, A);
+  const size_t fl = (size_t)small_floats(g) * (mode == NPG_VPG ? 1 : 2) + r4(RC * g.XS) + 2 * r4(RC * HS) +
+                    2 * r4(RC * DS) + 2 * r4(RC * g.GS) + r4(RC * A) + r4(2 * RC) + r4(g.A16);
+  return fl * sizeof(float);
 }
 
 }  // namespace
@@ -408,15 +597,25 @@ extern "C" int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int 
                 mode);
   AMX_CHECK_ARG(ldo >= S && lda >= A, "amx_npg_pass: ldo=%lld lda=%lld", ldo, lda);
   NpgArgs a = {};
-  a.mode = mode; a.N = N; a.S = S; a.A = A; a.SP = S | 1; a.rows_per_block = rows_per_block;
-  a.obs = obs; a.obs_f64 = obs_dtype == AMX_IN_F64; a.ldo = ldo;
-  a.act = act; a.act_f64 = act_dtype == AMX_IN_F64; a.lda = lda;
+  a.mode = mode; a.N = N; a.S = S; a.A = A; a.rows_per_block = rows_per_block;
+  a.obs = obs; a.ldo = ldo;
+  a.act = act; a.lda = lda;
   a.adv = adv; a.theta = theta; a.vec = vec; a.partials = partials;
   a.P = (int)amx_npg_param_count(S, A);
   const size_t lds = npg_lds_bytes(S, A, mode);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_npg_pass: %zu B of LDS", lds);
   const int blocks = (N + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL(k_npg, dim3(blocks), dim3(NT), lds, (hipStream_t)stream, a);
+  const bool of64 = obs_dtype == AMX_IN_F64, af64 = act_dtype == AMX_IN_F64;
+  void (*kern)(NpgArgs) = nullptr;
+  if (mode == NPG_FVP)  // actions are not read
+    kern = of64 ? k_npg<NPG_FVP, double, float> : k_npg<NPG_FVP, float, float>;
+  else if (mode == NPG_VPG)
+    kern = of64 ? (af64 ? k_npg<NPG_VPG, double, double> : k_npg<NPG_VPG, double, float>)
+                : (af64 ? k_npg<NPG_VPG, float, double> : k_npg<NPG_VPG, float, float>);
+  else
+    kern = of64 ? (af64 ? k_npg<NPG_EVAL, double, double> : k_npg<NPG_EVAL, double, float>)
+                : (af64 ? k_npg<NPG_EVAL, float, double> : k_npg<NPG_EVAL, float, float>);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(NT), lds, (hipStream_t)stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
