@@ -57,6 +57,8 @@ SIGNATURES = {
     "amx_npg_param_count": (c_ll, [c_int, c_int]),
     "amx_npg_pass": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp]),
     "amx_npg_reduce": (c_int, [vp, vp, c_int, c_int, vp, vp]),
+    "amx_npg_cg_init": (c_int, [vp, c_int, vp, vp, vp, vp, vp, vp, vp]),
+    "amx_npg_cg_step": (c_int, [vp, c_int, c_int, vp, vp, c_dbl, c_dbl, vp, vp, vp, vp, vp, vp]),
     "amx_step": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_int, vp]),
     "amx_step_rexp": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, c_int, vp]),
     "amx_step_reset": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, vp, c_int, vp,

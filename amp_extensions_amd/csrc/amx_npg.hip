@@ -35,6 +35,27 @@
 // pass at 40960 x 197; see DESIGN.md section 6 for this one's time.
 #include "amx_common.h"
 
+// Phase mask for timing experiments (tools/npg_phase.py builds variants with -DNPG_PHASES=m):
+// 1 layer 1, 2 layer 2, 4 output layer, 8 / 16 / 32 back-propagation of layers 3 / 2 / 1,
+// 64 the chunk loads.  The library is always built with every phase.
+#ifndef NPG_PHASES
+#define NPG_PHASES 0x7f
+#endif
+// -DNPG_TRACE (tools/npg_phase.py trace): thread 0 of blocks 0, 64, 128, 255 stamps the device
+// realtime clock (100 MHz) at the kernel's phase boundaries into npg_trace_buf.
+#ifdef NPG_TRACE
+__device__ unsigned long long npg_trace_buf[4][64];
+#define NPG_STAMP(slot)                                                                        \
+  do {                                                                                         \
+    const int tb_ = blockIdx.x == 0 ? 0 : blockIdx.x == 64 ? 1 : blockIdx.x == 128 ? 2 : blockIdx.x == 255 ? 3 : -1; \
+    if (threadIdx.x == 0 && tb_ >= 0 && (slot) < 64) npg_trace_buf[tb_][(slot)] = wall_clock64();   \
+  } while (0)
+#else
+#define NPG_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 
 constexpr int NH = 32;                 // hidden width (both layers)
@@ -133,6 +154,10 @@ __device__ inline void load_small(const float* __restrict__ src, const Lay& L, c
   }
 }
 
+// Workgroup barrier for LDS hand-offs: waits for this wave's LDS traffic only, so the next
+// chunk's global loads stay in flight across it (__syncthreads' fence waits for them too).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ pf4 mma(float a, float b, pf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -159,8 +184,9 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   float* G = carve(p, RC * g.GS);     // output-layer gradient (VPG / FVP), new mean (EVAL)
   float* ACT = carve(p, RC * A);
   double* ADV = reinterpret_cast<double*>(carve(p, 2 * RC));
-  float* CF = carve(p, g.A16);        // FVP: 2 / (2 sigma^2 + 1e-8)
+  float* TAB = carve(p, 2 * g.A16);   // per action: FVP 2 / (2 sigma^2 + 1e-8); VPG sigma; EVAL sigma_old | sigma_new
 
+  NPG_STAMP(0);
   load_small(a.theta, L, g, th);
   if (two) load_small(a.vec, L, g, tv);
   {
@@ -174,11 +200,11 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       H1[r * HS + c] = c == NH ? 1.f : 0.f;
       H2[r * HS + c] = c == NH ? 1.f : 0.f;
     }
-    if (mode == NPG_FVP)
-      for (int e = t; e < g.A16; e += NT) {
-        const float sd = e < A ? expf(a.theta[L.ls + e]) : 1.f;
-        CF[e] = 2.f / (2.f * sd * sd + 1e-8f);
-      }
+    for (int e = t; e < g.A16; e += NT) {
+      const float sd = e < A ? expf(a.theta[L.ls + e]) : 1.f;
+      TAB[e] = mode == NPG_FVP ? 2.f / (2.f * sd * sd + 1e-8f) : sd;
+      if (mode == NPG_EVAL) TAB[g.A16 + e] = e < A ? expf(a.vec[L.ls + e]) : 1.f;
+    }
   }
 
   // this wave's layer-1 tile: rows 16 rb1, units 16 cb1, parameter set mat1 (VPG: waves 0-3)
@@ -199,6 +225,10 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       }
       wf[jj] = v;
     }
+    // the fragments' loads complete here, outside the chunk loop (otherwise the loop's first
+    // use waits on vmcnt(0), i.e. on the next chunk's prefetch as well)
+#pragma unroll
+    for (int jj = 0; jj < MAXJJ; ++jj) asm volatile("" ::"v"(wf[jj]));
   }
 
   // next chunk's inputs, held in registers while the current chunk computes: thread t stages
@@ -248,32 +278,39 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   const int r1 = min(a.N, r0 + a.rows_per_block);
   if (r0 < r1) prefetch(r0, min(RC, r1 - r0));
 
-  for (int c0 = r0; c0 < r1; c0 += RC) {
+  for (int c0 = r0, ci = 0; c0 < r1; c0 += RC, ++ci) {
     // per-chunk opaque copies of the lane indices and strides: keeps the compiler from hoisting
     // every chunk-invariant LDS address out of the loop (hundreds of registers held live)
-    int i_ = i, kq_ = kq, xs_ = g.XS, gs_ = g.GS;
+    int i_ = i, kq_ = kq, xs_ = g.XS, gs_ = g.GS, jj_ = g.JJ;
     asm volatile("" : "+v"(i_), "+v"(kq_));
-    asm volatile("" : "+s"(xs_), "+s"(gs_));
-    const int i = i_, kq = kq_, XS = xs_, GS = gs_;
+    asm volatile("" : "+s"(xs_), "+s"(gs_), "+s"(jj_));
+    const int i = i_, kq = kq_, XS = xs_, GS = gs_, JJ = jj_;
     const int nr = min(RC, r1 - c0);
-    __syncthreads();  // the previous chunk is consumed (first chunk: parameters and pads are stored)
-    stash();
-    if (c0 + RC < r1) prefetch(c0 + RC, min(RC, r1 - c0 - RC));
-    __syncthreads();
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 0);  // the previous chunk is consumed (first chunk: parameters and pads are stored)
+    if (NPG_PHASES & 64) stash();
+    if ((NPG_PHASES & 64) && c0 + RC < r1) prefetch(c0 + RC, min(RC, r1 - c0 - RC));
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 1);
 
     // ---- layer 1: H1 = tanh(X W1^T + b1); FVP: D1 = X V1^T + vb1; EVAL: D1 = tanh(X V1n^T + b1n)
-    if (f1) {
+    if ((NPG_PHASES & 1) && f1) {
       const float* xr = X + (rb1 * 16 + i) * XS + 4 * kq;
       pf4 ca = {0.f, 0.f, 0.f, 0.f}, cb = {0.f, 0.f, 0.f, 0.f};
+      // branch-free and software-pipelined (step jj + 2's operand is read while step jj
+      // multiplies); steps past JJ re-read the last step's columns against zero weights,
+      // adding exact zeros
+      pf4 xq[2];
+      xq[0] = *reinterpret_cast<const pf4*>(xr);
+      xq[1] = *reinterpret_cast<const pf4*>(xr + 16 * min(1, JJ - 1));
 #pragma unroll
       for (int jj = 0; jj < MAXJJ; ++jj) {
-        if (jj < g.JJ) {
-          const pf4 x = *reinterpret_cast<const pf4*>(xr + 16 * jj);
-          ca = mma(x.x, wf[jj].x, ca);
-          cb = mma(x.y, wf[jj].y, cb);
-          ca = mma(x.z, wf[jj].z, ca);
-          cb = mma(x.w, wf[jj].w, cb);
-        }
+        const pf4 x = xq[jj & 1];
+        if (jj + 2 < MAXJJ) xq[jj & 1] = *reinterpret_cast<const pf4*>(xr + 16 * min(jj + 2, JJ - 1));
+        ca = mma(x.x, wf[jj].x, ca);
+        cb = mma(x.y, wf[jj].y, cb);
+        ca = mma(x.z, wf[jj].z, ca);
+        cb = mma(x.w, wf[jj].w, cb);
       }
       const int col = cb1 * 16 + i;
       const float bias = (mat1 ? tv.b1 : th.b1)[col];
@@ -285,11 +322,12 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         else D1[row * DS + col] = mode == NPG_EVAL ? tanhf(z) : z;  // FVP: tanh' applied on use
       }
     }
-    __syncthreads();
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 2);
 
     // ---- layer 2 (same tile per wave): H2 = tanh(H1 W2^T + b2);
     //      FVP: D2 = H1 V2^T + (D1 (1 - H1^2)) W2^T + vb2; EVAL: D2 = tanh(D1 V2n^T + b2n)
-    if (f1) {
+    if ((NPG_PHASES & 2) && f1) {
       const int rowA = rb1 * 16 + i, u = cb1 * 16 + i;
       pf4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
       if (!mat1) {
@@ -321,10 +359,11 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         else D2[row * DS + u] = tanhf(acc[r] + tv.b2[u]);
       }
     }
-    __syncthreads();
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 3);
 
     // ---- output layer: VPG mean -> G (and z -> M); FVP JVP of the mean -> G; EVAL M, new mean G
-    {
+    if (NPG_PHASES & 4) {
       const int n3 = mode == NPG_EVAL ? 4 * g.nA : 2 * g.nA;
       for (int it = wave; it < n3; it += NW) {
         const int rb = it & 1, cbk = (it >> 1) % g.nA, mat = it / (2 * g.nA);
@@ -358,12 +397,12 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
           const bool ok = row < nr && d < A;
           if (mode == NPG_FVP) {
             const float m = (acc[r] + acc2[r]) + tv.b3[d];
-            G[row * GS + d] = ok ? (float)((double)(m * CF[d]) * invN) : 0.f;
+            G[row * GS + d] = ok ? (float)((double)(m * TAB[d]) * invN) : 0.f;
           } else if (mode == NPG_VPG) {
             const float m = acc[r] + th.b3[d];
             float gg = 0.f, z = 0.f;
             if (ok) {
-              const float sd = expf(th.ls[d]);
+              const float sd = TAB[d];
               z = (ACT[row * A + d] - m) / sd;
               gg = (float)(ADV[row] * invN) * (z / sd);
             }
@@ -375,32 +414,36 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 4);
 
     if (mode == NPG_EVAL) {
-      // per row: LL_new - LL_old and sample_kl (gaussian_mlp.py:110-155), one thread per row
-      if (t < nr) {
-        const int r = t;
-        float dll = 0.f, kl = 0.f, sls_o = 0.f, sls_n = 0.f;
-        for (int d = 0; d < A; ++d) {
-          const float ac = ACT[r * A + d];
-          const float mo = M[r * GS + d], mn = G[r * GS + d];
-          const float so = expf(th.ls[d]), sn = expf(tv.ls[d]);
-          const float zo = (ac - mo) / so, zn = (ac - mn) / sn;
-          dll += -0.5f * zn * zn - (-0.5f * zo * zo);
-          sls_o += th.ls[d];
-          sls_n += tv.ls[d];
-          const float dm = mo - mn;
-          const float Nr = dm * dm + so * so - sn * sn, Dr = 2.f * sn * sn + 1e-8f;
-          kl += Nr / Dr + tv.ls[d] - th.ls[d];
-        }
-        dll += -sls_n + sls_o;
-        ev_surr += (double)(expf(dll) * (float)ADV[r]);
+      // per row: LL_new - LL_old and sample_kl (gaussian_mlp.py:110-155); 16 threads per row
+      // (actions pc + 16 u), combined over the 16 by butterfly shuffles
+      float dll = 0.f, kl = 0.f;
+      for (int d = pc; d < A; d += 16) {
+        const float ac = ACT[pr * A + d];
+        const float mo = M[pr * GS + d], mn = G[pr * GS + d];
+        const float so = TAB[d], sn = TAB[g.A16 + d];
+        const float zo = (ac - mo) / so, zn = (ac - mn) / sn;
+        dll += -0.5f * zn * zn - (-0.5f * zo * zo) + (th.ls[d] - tv.ls[d]);
+        const float dm = mo - mn;
+        const float Nr = dm * dm + so * so - sn * sn, Dr = 2.f * sn * sn + 1e-8f;
+        kl += Nr / Dr + tv.ls[d] - th.ls[d];
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        dll += __shfl_xor(dll, o);
+        kl += __shfl_xor(kl, o);
+      }
+      if (pc == 0 && pr < nr) {
+        ev_surr += (double)(expf(dll) * (float)ADV[pr]);
         ev_kl += (double)kl;
       }
       continue;
     }
 
+    if (NPG_PHASES & 8) {
     // ---- back-propagation, output layer: gW3 | b3 (owned tiles, K = rows);
     //      D2 = (G W3)(1 - H2^2) (tiles from the last wave down); VPG: log_std sums (wave 3)
 #pragma unroll
@@ -440,8 +483,11 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         gls += ADV[r] * invN * (double)(z * z - 1.f);
       }
     }
-    __syncthreads();
+    }
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 5);
 
+    if (NPG_PHASES & 16) {
     // ---- layer 2: gW2 | b2 (waves 0-5); D1 = (D2 W2)(1 - H1^2) (waves 7-4)
     if (wave < 6) {
       const int mb = wave / 3, nb = wave % 3;
@@ -470,45 +516,64 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         D1[row * DS + col] = acc[r] * (1.f - h * h);
       }
     }
-    __syncthreads();
+    }
+    lds_barrier();
+    NPG_STAMP(2 + 8 * ci + 6);
 
-    // ---- layer 1: gW1 | b1 (owned tiles)
+    if (NPG_PHASES & 32) {
+    // ---- layer 1: gW1 | b1 (owned tiles: mb = wave & 1 for every slot, so the D1 operand is
+    //      shared; the slots' chains interleave branch-free, a slot past the tiles is discarded)
+    {
+      const int mb = wave & 1;
+      pf4 acc[G1SLOTS];
 #pragma unroll
-    for (int sl = 0; sl < G1SLOTS; ++sl) {
-      const int q = wave + NW * sl;
-      if (q < 2 * g.nS) {
-        const int mb = q & 1, nb = q >> 1;
-        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < G1SLOTS; ++sl) acc[sl] = pf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < RC / 4; ++s) {
-          const int k = 4 * s + kq;
-          acc = mma(D1[k * DS + mb * 16 + i], X[k * XS + nb * 16 + i], acc);
+      for (int s = 0; s < RC / 4; ++s) {
+        const int k = 4 * s + kq;
+        const float d = D1[k * DS + mb * 16 + i];
+        float xb[G1SLOTS];
+#pragma unroll
+        for (int sl = 0; sl < G1SLOTS; ++sl) {
+          const int nb = min((wave >> 1) + (NW / 2) * sl, g.nS - 1);
+          xb[sl] = X[k * XS + nb * 16 + i];
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) g1[sl][r] += (double)acc[r];
+        for (int sl = 0; sl < G1SLOTS; ++sl) acc[sl] = mma(d, xb[sl], acc[sl]);  // (unowned slots: discarded)
       }
+#pragma unroll
+      for (int sl = 0; sl < G1SLOTS; ++sl)
+        if (wave + NW * sl < 2 * g.nS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) g1[sl][r] += (double)acc[sl][r];
+        }
     }
+    }
+    NPG_STAMP(2 + 8 * ci + 7);
   }
 
   if (mode == NPG_EVAL) {
-    // block sums of (surr, kl) in fixed order
+    // block sums of (surr, kl): fixed-order tree
     __syncthreads();
     double* red = reinterpret_cast<double*>(H1);  // the activation tiles are free now
     red[t] = ev_surr;
     red[NT + t] = ev_kl;
     __syncthreads();
-    if (t == 0) {
-      double s0 = 0.0, s1 = 0.0;
-      for (int e = 0; e < NT; ++e) {
-        s0 += red[e];
-        s1 += red[NT + e];
+    for (int h = NT / 2; h > 0; h >>= 1) {
+      if (t < h) {
+        red[t] += red[t + h];
+        red[NT + t] += red[NT + t + h];
       }
-      a.partials[2LL * blockIdx.x] = s0;
-      a.partials[2LL * blockIdx.x + 1] = s1;
+      __syncthreads();
+    }
+    if (t == 0) {
+      a.partials[2LL * blockIdx.x] = red[0];
+      a.partials[2LL * blockIdx.x + 1] = red[NT];
     }
     return;
   }
   // tile element (row 16 mb + 4 kq + r, column 16 nb + i); the ones column is the bias
+  NPG_STAMP(1);
   double* out = a.partials + (long long)blockIdx.x * a.P;
 #pragma unroll
   for (int sl = 0; sl < G1SLOTS; ++sl) {
@@ -548,6 +613,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     }
   }
   if (t >= 192 && t < 192 + A) out[L.ls + t - 192] = mode == NPG_VPG ? gls : 0.0;
+  NPG_STAMP(63);
 }
 
 // out[c] = sum_b partials[b][c] in a fixed order (deterministic): stage 1 sums runs of RB
@@ -569,10 +635,105 @@ __global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, dou
   out[c] = s;
 }
 
+// ---- conjugate gradient (cg_solve.py:3-23) ---------------------------------------------
+constexpr int CGT = 1024;
+constexpr int CGE = 16;  // elements per thread: P <= CGT * CGE
+
+// sum over the workgroup in a fixed order (per-thread sums, wave butterflies, waves in order)
+__device__ double cg_block_sum(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < CGT / 64; ++w) s += red[w];
+  __syncthreads();  // red is reused by the next sum
+  return s;
+}
+
+__global__ __launch_bounds__(CGT) void k_npg_cg_init(int P, const double* __restrict__ b, double* __restrict__ x,
+                                                     double* __restrict__ r, double* __restrict__ p,
+                                                     float* __restrict__ p32, double* __restrict__ state) {
+  __shared__ double red[CGT / 64];
+  double rr = 0.0;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = threadIdx.x + u * CGT;
+    if (e < P) {
+      const double bv = b[e];
+      x[e] = 0.0;
+      r[e] = bv;
+      p[e] = bv;
+      p32[e] = (float)bv;
+      rr += bv * bv;
+    }
+  }
+  rr = cg_block_sum(rr, red);
+  if (threadIdx.x == 0) {
+    state[0] = rr;
+    state[1] = 1.0;
+  }
+}
+
+__global__ __launch_bounds__(CGT) void k_npg_cg_step(int P, int A, const double* __restrict__ h,
+                                                     const double* __restrict__ curv, double damping, double tol,
+                                                     double* __restrict__ x, double* __restrict__ r,
+                                                     double* __restrict__ p, float* __restrict__ p32,
+                                                     double* __restrict__ state) {
+  __shared__ double red[CGT / 64];
+  if (state[1] == 0.0) return;  // the solve has stopped (uniform)
+  const double rdotr = state[0];
+  double zl[CGE], pl[CGE], pz = 0.0;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = threadIdx.x + u * CGT;
+    zl[u] = pl[u] = 0.0;
+    if (e < P) {
+      const double pv = p[e];
+      double z = h[e];
+      if (e >= P - A) z += curv[e - (P - A)] * (double)p32[e];
+      z += damping * pv;
+      zl[u] = z;
+      pl[u] = pv;
+      pz += pv * z;
+    }
+  }
+  pz = cg_block_sum(pz, red);
+  const double v = rdotr / pz;
+  double rl[CGE], rr = 0.0;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = threadIdx.x + u * CGT;
+    rl[u] = 0.0;
+    if (e < P) {
+      x[e] += v * pl[u];
+      const double rv = r[e] - v * zl[u];
+      r[e] = rv;
+      rl[u] = rv;
+      rr += rv * rv;
+    }
+  }
+  rr = cg_block_sum(rr, red);
+  const double mu = rr / rdotr;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = threadIdx.x + u * CGT;
+    if (e < P) {
+      const double pn = rl[u] + mu * pl[u];
+      p[e] = pn;
+      p32[e] = (float)pn;
+    }
+  }
+  if (threadIdx.x == 0) {
+    state[0] = rr;
+    state[1] = rr < tol ? 0.0 : 1.0;
+  }
+}
+
 size_t npg_lds_bytes(int S, int A, int mode) {
   const Geo g(S, A);
   const size_t fl = (size_t)small_floats(g) * (mode == NPG_VPG ? 1 : 2) + r4(RC * g.XS) + 2 * r4(RC * HS) +
-                    2 * r4(RC * DS) + 2 * r4(RC * g.GS) + r4(RC * A) + r4(2 * RC) + r4(g.A16);
+                    2 * r4(RC * DS) + 2 * r4(RC * g.GS) + r4(RC * A) + r4(2 * RC) + r4(2 * g.A16);
   return fl * sizeof(float);
 }
 
@@ -649,3 +810,29 @@ extern "C" int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, 
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
+
+extern "C" int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, double* r, double* p, float* p32,
+                               double* state, void* stream) {
+  AMX_CHECK_ARG(ctx && b && x && r && p && p32 && state, "amx_npg_cg_init: null argument");
+  AMX_CHECK_ARG(P > 0 && P <= CGT * CGE, "amx_npg_cg_init: P=%d (<= %d)", P, CGT * CGE);
+  hipLaunchKernelGGL(k_npg_cg_init, dim3(1), dim3(CGT), 0, (hipStream_t)stream, P, b, x, r, p, p32, state);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_npg_cg_step(amx_ctx* ctx, int P, int A, const double* h, const double* curv, double damping,
+                               double residual_tol, double* x, double* r, double* p, float* p32, double* state,
+                               void* stream) {
+  AMX_CHECK_ARG(ctx && h && curv && x && r && p && p32 && state, "amx_npg_cg_step: null argument");
+  AMX_CHECK_ARG(P > 0 && P <= CGT * CGE && A > 0 && A <= P, "amx_npg_cg_step: P=%d A=%d", P, A);
+  hipLaunchKernelGGL(k_npg_cg_step, dim3(1), dim3(CGT), 0, (hipStream_t)stream, P, A, h, curv, damping,
+                     residual_tol, x, r, p, p32, state);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+#ifdef NPG_TRACE
+extern "C" int amx_npg_trace_read(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(npg_trace_buf), sizeof(unsigned long long) * 4 * 64) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -87,13 +87,28 @@ class DeviceNPG:
         return self.theta.cpu().numpy().copy()
 
     def set_param_values(self, new_params) -> None:
-        """MLP.set_param_values (gaussian_mlp.py:71-94): float32, log_std clamped at min_log_std."""
-        t = torch.as_tensor(np.asarray(new_params), dtype=torch.float32).to(self.ctx.device).clone()
+        """MLP.set_param_values (gaussian_mlp.py:71-94): float32, log_std clamped at min_log_std.
+        A device tensor stays on the device (no host round trip)."""
+        if isinstance(new_params, torch.Tensor):
+            t = new_params.detach().to(self.ctx.device, torch.float32).clone()
+        else:
+            t = torch.as_tensor(np.asarray(new_params), dtype=torch.float32).to(self.ctx.device).clone()
         t[-self.A:] = torch.clamp(t[-self.A:], min=self.min_log_std)
         self.theta = t.contiguous()
         if self.policy is not None:
-            layers, ls = unpack_policy(self.theta.cpu().numpy(), self.S, self.A)
-            self.policy.sync_from(layers, ls)
+            self.policy.sync_from(*self._layers_view())
+
+    def _layers_view(self):
+        """([(W, b)] * 3, log_std) as device views of theta (reference flat order)."""
+        sizes = (self.S, 32, 32, self.A)
+        layers, i = [], 0
+        for k in range(3):
+            o, n = sizes[k + 1], sizes[k]
+            W = self.theta[i:i + o * n].view(o, n)
+            i += o * n
+            layers.append((W, self.theta[i:i + o]))
+            i += o
+        return layers, self.theta[i:i + self.A]
 
     # ---- passes --------------------------------------------------------------------------
     def _rows_per_block(self, n: int) -> int:
@@ -164,22 +179,25 @@ class DeviceNPG:
         return h + regu * v32.double()
 
     def cg_solve(self, obs, act, b: torch.Tensor) -> torch.Tensor:
-        """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol)."""
-        x = torch.zeros_like(b)
-        r = b.clone()
-        p = r.clone()
-        rdotr = torch.dot(r, r)
+        """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with
+        NPG.HVP as the operator.  Each iteration is one Fisher-vector pass + reduce and one
+        single-workgroup vector step (amx_npg_cg_step); the early stop is the step's device-side
+        `live` flag (a finished solve leaves x unchanged), so no host sync between iterations."""
+        c = self.ctx
+        P = self.P
+        dev = c.device
+        b = b.to(torch.float64).contiguous()
+        x, r, p = (torch.empty(P, dtype=torch.float64, device=dev) for _ in range(3))
+        p32 = torch.empty(P, dtype=torch.float32, device=dev)
+        state = torch.empty(2, dtype=torch.float64, device=dev)
+        curv = self._ls_curvature().contiguous()
+        N.check(c.lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
+                                      p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_init")
         for _ in range(self.cg_iters):
-            z = self._hvp(obs, act, p)
-            v = rdotr / torch.dot(p, z)
-            x += v * p
-            r -= v * z
-            newrdotr = torch.dot(r, r)
-            mu = newrdotr / rdotr
-            p = r + mu * p
-            rdotr = newrdotr
-            if float(rdotr) < self.residual_tol:
-                break
+            h = self._pass(NPG_FVP, obs, act, None, p32)
+            N.check(c.lib.amx_npg_cg_step(c.h, P, self.A, h.data_ptr(), curv.data_ptr(), self.damping,
+                                          self.residual_tol, x.data_ptr(), r.data_ptr(), p.data_ptr(),
+                                          p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_step")
         return x
 
     def surrogate_kl(self, obs, act, adv_w, new_theta) -> tuple[float, float]:
@@ -198,19 +216,22 @@ class DeviceNPG:
             adv = (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-6)
         vpg = self._pass(NPG_VPG, obs, act, adv, None)
         npg = self.cg_solve(obs, act, vpg)
-        gdot = float(torch.dot(vpg, npg))
+        gdot = torch.dot(vpg, npg)
         if self.alpha is not None:
-            alpha = self.alpha
+            alpha = torch.full((), float(self.alpha), dtype=torch.float64, device=gdot.device)
             n_step_size = alpha ** 2 * gdot
         else:
-            n_step_size = self.n_step_size
-            alpha = math.sqrt(abs(self.n_step_size / (gdot + 1e-20)))
+            n_step_size = torch.full((), float(self.n_step_size), dtype=torch.float64, device=gdot.device)
+            alpha = torch.sqrt(torch.abs(n_step_size / (gdot + 1e-20)))
         new = (self.theta.double() + alpha * npg).to(torch.float32)
         new[-self.A:] = torch.clamp(new[-self.A:], min=self.min_log_std)
-        surr_after, kl = self.surrogate_kl(obs, act, adv, new)
-        self.set_param_values(new.cpu().numpy())
-        return {"vpg_grad": vpg, "npg_grad": npg, "alpha": alpha, "delta": n_step_size, "surr_before": 0.0,
-                "surr_after": surr_after, "kl_dist": kl, "advantages": adv}
+        n = obs.shape[0]
+        tot = self._pass(NPG_EVAL, obs, act, adv, new.contiguous())
+        self.set_param_values(new)
+        # the update's one host sync: the reference's infos are python floats
+        alpha_h, delta_h, surr_h, kl_h = torch.stack([alpha, n_step_size, tot[0], tot[1]]).tolist()
+        return {"vpg_grad": vpg, "npg_grad": npg, "alpha": alpha_h, "delta": delta_h, "surr_before": 0.0,
+                "surr_after": surr_h / n, "kl_dist": kl_h / n, "advantages": adv}
 
     def train_from_paths(self, paths, infos: dict | None = None):
         """Reference surface: mjrl path dicts (observations, actions, advantages, rewards) ->

@@ -264,6 +264,20 @@ int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, 
                  const float* vec, int rows_per_block, double* partials, void* stream);
 int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, void* stream);
 
+/* The conjugate-gradient solve of NPG (mjrl/mjrl/utils/cg_solve.py:3-23) on the device, one
+ * workgroup per call, fixed-order fp64 reductions, no host round trip between iterations.
+ * amx_npg_cg_init: x = 0, r = p = b, p32 = float32(p), state = {r.r, 1 (live)}.
+ * amx_npg_cg_step, after h = amx_npg_reduce(amx_npg_pass(FVP, vec = p32)):
+ *   z = h + [log_std block: curv * p32] + damping * p   (NPG.HVP's return, npg_cg.py:105)
+ *   v = rdotr / p.z; x += v p; r -= v z; rr = r.r; p = r + (rr / rdotr) p; rdotr = rr;
+ *   live = rdotr >= residual_tol (cg_solve's break: a finished solve leaves x/r/p unchanged);
+ *   p32 = float32(p) for the next product.  curv [A]: d^2 mean_kl / d log_std^2.  P <= 16384. */
+int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, double* r, double* p, float* p32,
+                    double* state, void* stream);
+int amx_npg_cg_step(amx_ctx* ctx, int P, int A, const double* h, const double* curv, double damping,
+                    double residual_tol, double* x, double* r, double* p, float* p32, double* state,
+                    void* stream);
+
 /* ---- step + termination ------------------------------------------------------- */
 
 /* One batched SimEnv.step after the forward (gym-simenv/gym_simenv/envs/sim_env.py:140-173):
