@@ -26,14 +26,16 @@
 //   * layers 2 / 3 and the back-propagated deltas are 16x16 tiles over K = 32 / A, dealt
 //     over the waves; the tanh derivative of a JVP is applied as its operand is loaded;
 //   * the weight gradients (K = the chunk's rows) are tiles each wave owns across chunks,
-//     summed per chunk in fp32 and accumulated in fp64 registers (as round 2's per-thread
-//     sums); the bias gradients come out of the same tiles through a column of ones next to
+//     accumulated on the matrix pipe in fp32 over the block's rows (fp64 across blocks in
+//     amx_npg_reduce); the bias gradients come out of the same tiles through a column of ones next to
 //     the layer's input (x[S] = 1, h[32] = 1: grad b = sum_r delta_r * 1);
 //   * the next chunk's observations / actions / advantages are loaded into registers while
 //     the current chunk computes.
 // Round 2's kernel (scalar LDS FMA loops, 4 waves, 1 chunk-sum per thread) took 431 us per
 // pass at 40960 x 197; see DESIGN.md section 6 for this one's time.
 #include "amx_common.h"
+
+#include <type_traits>
 
 // Phase mask for timing experiments (tools/npg_phase.py builds variants with -DNPG_PHASES=m):
 // 1 layer 1, 2 layer 2, 4 output layer, 8 / 16 / 32 back-propagation of layers 3 / 2 / 1,
@@ -138,20 +140,41 @@ __device__ inline Small carve_small(float*& p, const Geo& g) {
   return s;
 }
 
-__device__ inline void load_small(const float* __restrict__ src, const Lay& L, const Geo& g, const Small& d) {
-  for (int e = threadIdx.x; e < NH * NH; e += NT) d.w2[(e >> 5) * WS + (e & 31)] = src[L.w2 + e];
-  for (int e = threadIdx.x; e < g.A16 * NH; e += NT) {
-    const int r = e >> 5;
-    d.w3[r * WS + (e & 31)] = r < g.A ? src[L.w3 + e] : 0.f;
-  }
-  for (int e = threadIdx.x; e < NH; e += NT) {
-    d.b1[e] = src[L.b1 + e];
-    d.b2[e] = src[L.b2 + e];
-  }
-  for (int e = threadIdx.x; e < g.A16; e += NT) {
-    d.b3[e] = e < g.A ? src[L.b3 + e] : 0.f;
-    d.ls[e] = e < g.A ? src[L.ls + e] : 0.f;
-  }
+// The small image as one flat index space: W2 [32][32] | W3 [A16][32] | b1 | b2 | b3 [A16] |
+// ls [A16].  small_src: the packed-parameter index of element e (-1: a zero pad row);
+// small_dst: its offset in the LDS image (carve_small's layout).
+constexpr int SMU = (NH * NH + MAXA * NH + 2 * NH + 2 * MAXA + NT - 1) / NT;  // elements per thread
+
+__host__ __device__ inline int small_count(const Geo& g) { return NH * NH + g.A16 * NH + 2 * NH + 2 * g.A16; }
+
+__device__ inline int small_src(int e, const Lay& L, const Geo& g) {
+  if (e < NH * NH) return L.w2 + e;
+  e -= NH * NH;
+  if (e < g.A16 * NH) return (e >> 5) < g.A ? L.w3 + e : -1;
+  e -= g.A16 * NH;
+  if (e < NH) return L.b1 + e;
+  e -= NH;
+  if (e < NH) return L.b2 + e;
+  e -= NH;
+  if (e < g.A16) return e < g.A ? L.b3 + e : -1;
+  e -= g.A16;
+  return e < g.A ? L.ls + e : -1;
+}
+
+__device__ inline int small_dst(int e, const Geo& g) {  // offsets as carve_small: w2, b2, w3, b3, b1, ls
+  const int o_b2 = r4(NH * WS), o_w3 = o_b2 + r4(NH), o_b3 = o_w3 + r4(g.A16 * WS), o_b1 = o_b3 + r4(g.A16),
+            o_ls = o_b1 + r4(NH);
+  if (e < NH * NH) return (e >> 5) * WS + (e & 31);
+  e -= NH * NH;
+  if (e < g.A16 * NH) return o_w3 + (e >> 5) * WS + (e & 31);
+  e -= g.A16 * NH;
+  if (e < NH) return o_b1 + e;
+  e -= NH;
+  if (e < NH) return o_b2 + e;
+  e -= NH;
+  if (e < g.A16) return o_b3 + e;
+  e -= g.A16;
+  return o_ls + e;
 }
 
 // Workgroup barrier for LDS hand-offs: waits for this wave's LDS traffic only, so the next
@@ -187,27 +210,10 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   float* TAB = carve(p, 2 * g.A16);   // per action: FVP 2 / (2 sigma^2 + 1e-8); VPG sigma; EVAL sigma_old | sigma_new
 
   NPG_STAMP(0);
-  load_small(a.theta, L, g, th);
-  if (two) load_small(a.vec, L, g, tv);
-  {
-    const int xp = g.XS - S;
-    for (int e = t; e < RC * xp; e += NT) {
-      const int r = e / xp, c = S + e % xp;
-      X[r * g.XS + c] = c == S ? 1.f : 0.f;
-    }
-    for (int e = t; e < RC * (HS - NH); e += NT) {
-      const int r = e / (HS - NH), c = NH + e % (HS - NH);
-      H1[r * HS + c] = c == NH ? 1.f : 0.f;
-      H2[r * HS + c] = c == NH ? 1.f : 0.f;
-    }
-    for (int e = t; e < g.A16; e += NT) {
-      const float sd = e < A ? expf(a.theta[L.ls + e]) : 1.f;
-      TAB[e] = mode == NPG_FVP ? 2.f / (2.f * sd * sd + 1e-8f) : sd;
-      if (mode == NPG_EVAL) TAB[g.A16 + e] = e < A ? expf(a.vec[L.ls + e]) : 1.f;
-    }
-  }
-
-  // this wave's layer-1 tile: rows 16 rb1, units 16 cb1, parameter set mat1 (VPG: waves 0-3)
+  // Setup issues every global load before the first store (one memory round trip, not one per
+  // array): this wave's W1 fragments, the small parameter images, the log_std table and the
+  // first chunk's inputs, in that order (the fragments' and images' waits leave the chunk
+  // loads in flight).
   const int n1 = two ? 8 : 4;
   const bool f1 = wave < n1;
   const int rb1 = wave & 1, cb1 = (wave >> 1) & 1, mat1 = wave >> 2;
@@ -225,10 +231,27 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       }
       wf[jj] = v;
     }
-    // the fragments' loads complete here, outside the chunk loop (otherwise the loop's first
-    // use waits on vmcnt(0), i.e. on the next chunk's prefetch as well)
+  }
+  NPG_STAMP(50);
+  const int nsmall = small_count(g);
+  float sv0[SMU], sv1[SMU];
 #pragma unroll
-    for (int jj = 0; jj < MAXJJ; ++jj) asm volatile("" ::"v"(wf[jj]));
+  for (int u = 0; u < SMU; ++u) {
+    const int e = t + u * NT;
+    sv0[u] = sv1[u] = 0.f;
+    if (e < nsmall) {
+      const int src = small_src(e, L, g);
+      if (src >= 0) {
+        sv0[u] = a.theta[src];
+        if (two) sv1[u] = a.vec[src];
+      }
+    }
+  }
+  NPG_STAMP(51);
+  float lso = 0.f, lsn = 0.f;
+  if (t < g.A16 && t < A) {
+    lso = a.theta[L.ls + t];
+    if (mode == NPG_EVAL) lsn = a.vec[L.ls + t];
   }
 
   // next chunk's inputs, held in registers while the current chunk computes: thread t stages
@@ -263,20 +286,55 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       if (t < RC) ADV[t] = dv;
     }
   };
-
-  double g1[G1SLOTS][4], g3[G3SLOTS][4], g2[4], gls = 0.0, ev_surr = 0.0, ev_kl = 0.0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-#pragma unroll
-    for (int s = 0; s < G1SLOTS; ++s) g1[s][r] = 0.0;
-#pragma unroll
-    for (int s = 0; s < G3SLOTS; ++s) g3[s][r] = 0.0;
-    g2[r] = 0.0;
-  }
-  const double invN = 1.0 / (double)a.N;
   const int r0 = blockIdx.x * a.rows_per_block;
   const int r1 = min(a.N, r0 + a.rows_per_block);
+  NPG_STAMP(52);
   if (r0 < r1) prefetch(r0, min(RC, r1 - r0));
+  NPG_STAMP(53);
+
+  // stores: parameter images, constant pads, the per-action table
+#pragma unroll
+  for (int u = 0; u < SMU; ++u) {
+    const int e = t + u * NT;
+    if (e < nsmall) {
+      const int o = small_dst(e, g);
+      sm[o] = sv0[u];
+      if (two) sm[small_floats(g) + o] = sv1[u];
+    }
+  }
+  {
+    const int xp = g.XS - S;
+    for (int e = t; e < RC * xp; e += NT) {
+      const int r = e / xp, c = S + e % xp;
+      X[r * g.XS + c] = c == S ? 1.f : 0.f;
+    }
+    for (int e = t; e < RC * (HS - NH); e += NT) {
+      const int r = e / (HS - NH), c = NH + e % (HS - NH);
+      H1[r * HS + c] = c == NH ? 1.f : 0.f;
+      H2[r * HS + c] = c == NH ? 1.f : 0.f;
+    }
+    if (t < g.A16) {
+      const float sd = t < A ? expf(lso) : 1.f;
+      TAB[t] = mode == NPG_FVP ? 2.f / (2.f * sd * sd + 1e-8f) : sd;
+      if (mode == NPG_EVAL) TAB[g.A16 + t] = t < A ? expf(lsn) : 1.f;
+    }
+  }
+  NPG_STAMP(54);
+  // the fragments' loads complete here, outside the chunk loop (otherwise the loop's first
+  // use waits on vmcnt(0), i.e. on the next chunk's prefetch as well)
+#pragma unroll
+  for (int jj = 0; jj < MAXJJ; ++jj) asm volatile("" ::"v"(wf[jj]));
+
+  NPG_STAMP(55);
+  // the owned weight-gradient tiles: MFMA accumulators carried across the block's chunks
+  // (fp32 over the block's rows, fp64 across blocks in amx_npg_reduce)
+  pf4 g1[G1SLOTS], g3[G3SLOTS], g2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < G1SLOTS; ++s) g1[s] = pf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < G3SLOTS; ++s) g3[s] = pf4{0.f, 0.f, 0.f, 0.f};
+  double gls = 0.0, ev_surr = 0.0, ev_kl = 0.0;
+  const double invN = 1.0 / (double)a.N;
 
   for (int c0 = r0, ci = 0; c0 < r1; c0 += RC, ++ci) {
     // per-chunk opaque copies of the lane indices and strides: keeps the compiler from hoisting
@@ -297,9 +355,8 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     if ((NPG_PHASES & 1) && f1) {
       const float* xr = X + (rb1 * 16 + i) * XS + 4 * kq;
       pf4 ca = {0.f, 0.f, 0.f, 0.f}, cb = {0.f, 0.f, 0.f, 0.f};
-      // branch-free and software-pipelined (step jj + 2's operand is read while step jj
-      // multiplies); steps past JJ re-read the last step's columns against zero weights,
-      // adding exact zeros
+      // software-pipelined: step jj + 2's operand is read while step jj multiplies (clamped to
+      // the last step: a read past JJ is never used)
       pf4 xq[2];
       xq[0] = *reinterpret_cast<const pf4*>(xr);
       xq[1] = *reinterpret_cast<const pf4*>(xr + 16 * min(1, JJ - 1));
@@ -307,10 +364,12 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       for (int jj = 0; jj < MAXJJ; ++jj) {
         const pf4 x = xq[jj & 1];
         if (jj + 2 < MAXJJ) xq[jj & 1] = *reinterpret_cast<const pf4*>(xr + 16 * min(jj + 2, JJ - 1));
-        ca = mma(x.x, wf[jj].x, ca);
-        cb = mma(x.y, wf[jj].y, cb);
-        ca = mma(x.z, wf[jj].z, ca);
-        cb = mma(x.w, wf[jj].w, cb);
+        if (jj < JJ) {  // uniform
+          ca = mma(x.x, wf[jj].x, ca);
+          cb = mma(x.y, wf[jj].y, cb);
+          ca = mma(x.z, wf[jj].z, ca);
+          cb = mma(x.w, wf[jj].w, cb);
+        }
       }
       const int col = cb1 * 16 + i;
       const float bias = (mat1 ? tv.b1 : th.b1)[col];
@@ -451,14 +510,13 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       const int q = wave + NW * sl;
       if (q < 3 * g.nA) {
         const int mb = q / 3, nb = q % 3;
-        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+        pf4 acc = g3[sl];
 #pragma unroll
         for (int s = 0; s < RC / 4; ++s) {
           const int k = 4 * s + kq;
           acc = mma(G[k * GS + mb * 16 + i], H2[k * HS + nb * 16 + i], acc);
         }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) g3[sl][r] += (double)acc[r];
+        g3[sl] = acc;
       }
     }
     if (NW - 1 - wave < 4) {
@@ -491,14 +549,13 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     // ---- layer 2: gW2 | b2 (waves 0-5); D1 = (D2 W2)(1 - H1^2) (waves 7-4)
     if (wave < 6) {
       const int mb = wave / 3, nb = wave % 3;
-      pf4 acc = {0.f, 0.f, 0.f, 0.f};
+      pf4 acc = g2;
 #pragma unroll
       for (int s = 0; s < RC / 4; ++s) {
         const int k = 4 * s + kq;
         acc = mma(D2[k * DS + mb * 16 + i], H1[k * HS + nb * 16 + i], acc);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) g2[r] += (double)acc[r];
+      g2 = acc;
     }
     if (NW - 1 - wave < 4) {
       const int it = NW - 1 - wave, rb = it & 1, cbk = it >> 1;
@@ -521,32 +578,39 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     NPG_STAMP(2 + 8 * ci + 6);
 
     if (NPG_PHASES & 32) {
-    // ---- layer 1: gW1 | b1 (owned tiles: mb = wave & 1 for every slot, so the D1 operand is
-    //      shared; the slots' chains interleave branch-free, a slot past the tiles is discarded)
+    // ---- layer 1: gW1 | b1 (owned tiles q = wave + 8 sl: mb = wave & 1 for every slot, so the
+    //      D1 operand is shared and the slots' chains interleave; the slot count is the block's
+    //      ceil(2 nS / 8), a slot past this wave's tiles computes and is discarded)
     {
-      const int mb = wave & 1;
-      pf4 acc[G1SLOTS];
+      auto bp1 = [&](auto nsl_c) {
+        constexpr int NSL = decltype(nsl_c)::value;
+        const int mb = wave & 1;
+        pf4 acc[NSL];
 #pragma unroll
-      for (int sl = 0; sl < G1SLOTS; ++sl) acc[sl] = pf4{0.f, 0.f, 0.f, 0.f};
+        for (int sl = 0; sl < NSL; ++sl) acc[sl] = g1[sl];
 #pragma unroll
-      for (int s = 0; s < RC / 4; ++s) {
-        const int k = 4 * s + kq;
-        const float d = D1[k * DS + mb * 16 + i];
-        float xb[G1SLOTS];
+        for (int s = 0; s < RC / 4; ++s) {
+          const int k = 4 * s + kq;
+          const float d = D1[k * DS + mb * 16 + i];
+          float xb[NSL];
 #pragma unroll
-        for (int sl = 0; sl < G1SLOTS; ++sl) {
-          const int nb = min((wave >> 1) + (NW / 2) * sl, g.nS - 1);
-          xb[sl] = X[k * XS + nb * 16 + i];
+          for (int sl = 0; sl < NSL; ++sl) {
+            const int nb = min((wave >> 1) + (NW / 2) * sl, g.nS - 1);
+            xb[sl] = X[k * XS + nb * 16 + i];
+          }
+#pragma unroll
+          for (int sl = 0; sl < NSL; ++sl) acc[sl] = mma(d, xb[sl], acc[sl]);
         }
 #pragma unroll
-        for (int sl = 0; sl < G1SLOTS; ++sl) acc[sl] = mma(d, xb[sl], acc[sl]);  // (unowned slots: discarded)
+        for (int sl = 0; sl < NSL; ++sl) g1[sl] = acc[sl];
+      };
+      switch ((2 * g.nS + NW - 1) / NW) {
+        case 1: bp1(std::integral_constant<int, 1>{}); break;
+        case 2: bp1(std::integral_constant<int, 2>{}); break;
+        case 3: bp1(std::integral_constant<int, 3>{}); break;
+        case 4: bp1(std::integral_constant<int, 4>{}); break;
+        default: bp1(std::integral_constant<int, G1SLOTS>{}); break;
       }
-#pragma unroll
-      for (int sl = 0; sl < G1SLOTS; ++sl)
-        if (wave + NW * sl < 2 * g.nS) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) g1[sl][r] += (double)acc[sl][r];
-        }
     }
     }
     NPG_STAMP(2 + 8 * ci + 7);
@@ -583,8 +647,8 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int j = mb * 16 + 4 * kq + r;
-        if (k < S) out[L.w1 + j * S + k] = g1[sl][r];
-        else if (k == S) out[L.b1 + j] = g1[sl][r];
+        if (k < S) out[L.w1 + j * S + k] = (double)g1[sl][r];
+        else if (k == S) out[L.b1 + j] = (double)g1[sl][r];
       }
     }
   }
@@ -593,8 +657,8 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = mb * 16 + 4 * kq + r;
-      if (k < NH) out[L.w2 + j * NH + k] = g2[r];
-      else if (k == NH) out[L.b2 + j] = g2[r];
+      if (k < NH) out[L.w2 + j * NH + k] = (double)g2[r];
+      else if (k == NH) out[L.b2 + j] = (double)g2[r];
     }
   }
 #pragma unroll
@@ -606,8 +670,8 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       for (int r = 0; r < 4; ++r) {
         const int d = mb * 16 + 4 * kq + r;
         if (d < A) {
-          if (k < NH) out[L.w3 + d * NH + k] = g3[sl][r];
-          else if (k == NH) out[L.b3 + d] = g3[sl][r];
+          if (k < NH) out[L.w3 + d * NH + k] = (double)g3[sl][r];
+          else if (k == NH) out[L.b3 + d] = (double)g3[sl][r];
         }
       }
     }

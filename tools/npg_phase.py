@@ -125,7 +125,7 @@ def trace(N, S, A, mode_name="fvp"):
     for bi, blk in enumerate((0, 64, 128, 255)):
         t = tr[bi]
         t0 = t[0]
-        rows = [f"setup {(t[2] - t0) / 100:5.2f}"]
+        rows = [f"setup {(t[2] - t0) / 100:5.2f} (" + " ".join(f"{(t[k] - t0) / 100:.2f}" for k in range(50, 56)) + ")"]
         per = np.zeros(8)
         for c in range(nch):
             st = [t[2 + 8 * c + k] for k in range(8)]
