@@ -61,7 +61,7 @@ __device__ unsigned long long npg_trace_buf[4][64];
 namespace {
 
 constexpr int NH = 32;                 // hidden width (both layers)
-constexpr int RC = 32;                 // rows per chunk
+constexpr int RC0 = 32;                // rows per chunk: 32, or 64 when the LDS image fits (f32 inputs)
 constexpr int NT = 512;                // threads per block: 8 waves, 2 per SIMD
 constexpr int NW = NT / 64;
 constexpr int MAXS = 256;              // max state dim
@@ -69,11 +69,10 @@ constexpr int MAXA = 64;               // max action dim
 constexpr int HS = 52;                 // H1/H2 row stride: 32 units | 1 (ones column) | 0 to 48 | pad
 constexpr int DS = 36;                 // D1/D2 (JVP, then delta) row stride
 constexpr int WS = 36;                 // W2 / W3 LDS row stride
-constexpr int MAXJJ = MAXS / 16;       // float4 W1 fragments per lane
+constexpr int MAXJJ = MAXS / 16;       // float4 W1 fragments per lane (at most)
+constexpr int W1U = (NH * MAXS / 4 + NT - 1) / NT;  // W1 float4s per thread in the setup
 constexpr int G1SLOTS = (2 * ((MAXS + 16) / 16) + NW - 1) / NW;  // gW1 tiles per wave
 constexpr int G3SLOTS = (3 * (MAXA / 16) + NW - 1) / NW;         // gW3 tiles per wave
-constexpr int XU = MAXS / 16;          // observation values per thread per chunk (16 threads a row)
-constexpr int AU = MAXA / 16;          // action values per thread per chunk
 
 enum { NPG_VPG = 0, NPG_FVP = 1, NPG_EVAL = 2 };
 
@@ -185,51 +184,56 @@ __device__ __forceinline__ pf4 mma(float a, float b, pf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int MODE, typename TO, typename TA>
+template <int MODE, typename TO, typename TA, int RC, int JJM>
 __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
+  // JJM: layer-1 K steps compiled (>= ceil(S / 16); steps past S multiply zero weights)
+  constexpr int mode = MODE;
+  constexpr int NRB = RC / 16;                 // 16-row blocks per chunk
+  constexpr int TPR = NT / RC;                 // staging threads per row
+  constexpr int XU = MAXS / TPR, AU = MAXA / TPR;
+  constexpr bool two = mode != NPG_VPG;
+  constexpr int NMAT = two ? 2 : 1;            // parameter sets in the forward
+  constexpr int NI = NRB * 2 * NMAT;           // layer-1 / layer-2 tiles per chunk
+  constexpr int MI = (NI + NW - 1) / NW;       // ... per wave
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const Geo g(a.S, a.A);
   const Lay L(a.S, a.A);
   const int S = g.S, A = g.A;
-  constexpr int mode = MODE;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, i = lane & 15, kq = lane >> 4;
-  const bool two = mode != NPG_VPG;
   float* p = sm;
   const Small th = carve_small(p, g);
   Small tv = th;
   if (two) tv = carve_small(p, g);
-  float* X = carve(p, RC * g.XS);     // [32][XS]: S observations | 1 | zeros
+  float* X = carve(p, RC * g.XS);     // [RC][XS]: S observations | 1 | zeros
   float* H1 = carve(p, RC * HS);      // tanh activations | 1 | zeros
   float* H2 = carve(p, RC * HS);
   float* D1 = carve(p, RC * DS);      // FVP: tangent pre-activation (V1 x + vb1); EVAL: new h1; then delta
   float* D2 = carve(p, RC * DS);
-  float* M = carve(p, RC * g.GS);     // mean (EVAL), z (VPG)
   float* G = carve(p, RC * g.GS);     // output-layer gradient (VPG / FVP), new mean (EVAL)
-  float* ACT = carve(p, RC * A);
-  double* ADV = reinterpret_cast<double*>(carve(p, 2 * RC));
+  float* M = mode == NPG_FVP ? G : carve(p, RC * g.GS);  // mean (EVAL), z (VPG)
+  float* ACT = mode == NPG_FVP ? G : carve(p, RC * A);
+  double* ADV = reinterpret_cast<double*>(mode == NPG_FVP ? G : carve(p, 2 * RC));
   float* TAB = carve(p, 2 * g.A16);   // per action: FVP 2 / (2 sigma^2 + 1e-8); VPG sigma; EVAL sigma_old | sigma_new
 
   NPG_STAMP(0);
   // Setup issues every global load before the first store (one memory round trip, not one per
-  // array): this wave's W1 fragments, the small parameter images, the log_std table and the
-  // first chunk's inputs, in that order (the fragments' and images' waits leave the chunk
-  // loads in flight).
-  const int n1 = two ? 8 : 4;
-  const bool f1 = wave < n1;
-  const int rb1 = wave & 1, cb1 = (wave >> 1) & 1, mat1 = wave >> 2;
-  pf4 wf[MAXJJ];
-  {
-    const float* wrow = ((f1 && mat1) ? a.vec : a.theta) + L.w1 + (cb1 * 16 + i) * S;
+  // array): W1 (and the tangent's / new W1) as coalesced float4s, the small parameter images,
+  // the log_std table and the first chunk's inputs.  W1 then goes through LDS (the X tile's
+  // space, before the first chunk) into each wave's fragment registers: read from global
+  // memory directly, the fragments' row-strided lanes cost ~3 us of L1 line traffic.
+  // Layer-1/2 tiles of this wave: item = wave + 8 m (m < MI): units 16 cb1, parameter set mat1
+  // (the same for every m), rows 16 rb(m).
+  const bool f1 = wave < NI;
+  const int cb1 = wave & 1, mat1 = (wave >> 1) % NMAT;
+  const int nw4 = NH * S / 4;  // float4s of W1 (32 S floats)
+  pf4 w1a[W1U], w1b[W1U];
 #pragma unroll
-    for (int jj = 0; jj < MAXJJ; ++jj) {
-      pf4 v = {0.f, 0.f, 0.f, 0.f};
-      if (f1 && jj < g.JJ) {
-        const int k0 = 4 * (kq + 4 * jj);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (k0 + e < S) v[e] = wrow[k0 + e];
-      }
-      wf[jj] = v;
+  for (int u = 0; u < W1U; ++u) {
+    const int e = t + u * NT;
+    w1a[u] = w1b[u] = pf4{0.f, 0.f, 0.f, 0.f};
+    if (e < nw4) {
+      w1a[u] = reinterpret_cast<const pf4*>(a.theta)[e];
+      if (two) w1b[u] = reinterpret_cast<const pf4*>(a.vec)[e];
     }
   }
   NPG_STAMP(50);
@@ -249,27 +253,27 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   }
   NPG_STAMP(51);
   float lso = 0.f, lsn = 0.f;
-  if (t < g.A16 && t < A) {
+  if (t < A) {
     lso = a.theta[L.ls + t];
     if (mode == NPG_EVAL) lsn = a.vec[L.ls + t];
   }
 
   // next chunk's inputs, held in registers while the current chunk computes: thread t stages
-  // row t / 16, columns t % 16 + 16 u (affine in u: one address register per array)
+  // row t / TPR, columns t % TPR + TPR u (affine in u: one address register per array)
   TO xv[XU];
   TA av[AU];
   double dv = 0.0;
-  const int pr = t >> 4, pc = t & 15;
-  const bool need_act = mode != NPG_FVP;
+  const int pr = t / TPR, pc = t % TPR;
+  constexpr bool need_act = mode != NPG_FVP;
   auto prefetch = [&](int c0, int nr) {
     const bool rv = pr < nr;
     const TO* xs = static_cast<const TO*>(a.obs) + (long long)(c0 + (rv ? pr : 0)) * a.ldo + pc;
 #pragma unroll
-    for (int u = 0; u < XU; ++u) xv[u] = (rv && pc + 16 * u < S) ? xs[16 * u] : TO(0);
+    for (int u = 0; u < XU; ++u) xv[u] = (rv && pc + TPR * u < S) ? xs[TPR * u] : TO(0);
     if (need_act) {
       const TA* as = static_cast<const TA*>(a.act) + (long long)(c0 + (rv ? pr : 0)) * a.lda + pc;
 #pragma unroll
-      for (int u = 0; u < AU; ++u) av[u] = (rv && pc + 16 * u < A) ? as[16 * u] : TA(0);
+      for (int u = 0; u < AU; ++u) av[u] = (rv && pc + TPR * u < A) ? as[TPR * u] : TA(0);
       if (t < RC) dv = t < nr ? a.adv[c0 + t] : 0.0;
     }
   };
@@ -277,12 +281,12 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     float* xd = X + pr * g.XS + pc;
 #pragma unroll
     for (int u = 0; u < XU; ++u)
-      if (pc + 16 * u < S) xd[16 * u] = (float)xv[u];  // np.float32(observation)
+      if (pc + TPR * u < S) xd[TPR * u] = (float)xv[u];  // np.float32(observation)
     if (need_act) {
       float* ad = ACT + pr * A + pc;
 #pragma unroll
       for (int u = 0; u < AU; ++u)
-        if (pc + 16 * u < A) ad[16 * u] = (float)av[u];
+        if (pc + TPR * u < A) ad[TPR * u] = (float)av[u];
       if (t < RC) ADV[t] = dv;
     }
   };
@@ -291,6 +295,34 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   NPG_STAMP(52);
   if (r0 < r1) prefetch(r0, min(RC, r1 - r0));
   NPG_STAMP(53);
+
+  // W1 fragments via LDS: set 0, then (FVP / EVAL) set 1, through the X tile's space
+  pf4 wf[JJM];
+  auto fragments = [&](const pf4 (&w)[W1U], int set) {
+#pragma unroll
+    for (int u = 0; u < W1U; ++u) {
+      const int e = t + u * NT;
+      if (e < nw4) reinterpret_cast<pf4*>(X)[e] = w[u];
+    }
+    lds_barrier();
+    if (f1 && mat1 == set) {
+      const float* wrow = X + (cb1 * 16 + i) * S;
+#pragma unroll
+      for (int jj = 0; jj < JJM; ++jj) {
+        pf4 v = {0.f, 0.f, 0.f, 0.f};
+        const int k0 = 4 * (kq + 4 * jj);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (k0 + e < S) v[e] = wrow[k0 + e];
+        wf[jj] = v;
+      }
+    }
+    lds_barrier();
+  };
+#pragma unroll
+  for (int jj = 0; jj < JJM; ++jj) wf[jj] = pf4{0.f, 0.f, 0.f, 0.f};
+  fragments(w1a, 0);
+  if (two) fragments(w1b, 1);
 
   // stores: parameter images, constant pads, the per-action table
 #pragma unroll
@@ -320,10 +352,6 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     }
   }
   NPG_STAMP(54);
-  // the fragments' loads complete here, outside the chunk loop (otherwise the loop's first
-  // use waits on vmcnt(0), i.e. on the next chunk's prefetch as well)
-#pragma unroll
-  for (int jj = 0; jj < MAXJJ; ++jj) asm volatile("" ::"v"(wf[jj]));
 
   NPG_STAMP(55);
   // the owned weight-gradient tiles: MFMA accumulators carried across the block's chunks
@@ -344,78 +372,95 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     asm volatile("" : "+s"(xs_), "+s"(gs_), "+s"(jj_));
     const int i = i_, kq = kq_, XS = xs_, GS = gs_, JJ = jj_;
     const int nr = min(RC, r1 - c0);
-    lds_barrier();
-    NPG_STAMP(2 + 8 * ci + 0);  // the previous chunk is consumed (first chunk: parameters and pads are stored)
-    if (NPG_PHASES & 64) stash();
-    if ((NPG_PHASES & 64) && c0 + RC < r1) prefetch(c0 + RC, min(RC, r1 - c0 - RC));
+    lds_barrier();  // the previous chunk is consumed (first chunk: parameters and pads are stored)
+    NPG_STAMP(2 + 8 * ci + 0);
+    if (NPG_PHASES & 64) {
+      stash();
+      if (c0 + RC < r1) prefetch(c0 + RC, min(RC, r1 - c0 - RC));
+    }
     lds_barrier();
     NPG_STAMP(2 + 8 * ci + 1);
 
     // ---- layer 1: H1 = tanh(X W1^T + b1); FVP: D1 = X V1^T + vb1; EVAL: D1 = tanh(X V1n^T + b1n)
     if ((NPG_PHASES & 1) && f1) {
-      const float* xr = X + (rb1 * 16 + i) * XS + 4 * kq;
-      pf4 ca = {0.f, 0.f, 0.f, 0.f}, cb = {0.f, 0.f, 0.f, 0.f};
-      // software-pipelined: step jj + 2's operand is read while step jj multiplies (clamped to
-      // the last step: a read past JJ is never used)
-      pf4 xq[2];
-      xq[0] = *reinterpret_cast<const pf4*>(xr);
-      xq[1] = *reinterpret_cast<const pf4*>(xr + 16 * min(1, JJ - 1));
+      const float* xr[MI];
+      pf4 ca[MI], cb[MI], xq[MI][2];
 #pragma unroll
-      for (int jj = 0; jj < MAXJJ; ++jj) {
-        const pf4 x = xq[jj & 1];
-        if (jj + 2 < MAXJJ) xq[jj & 1] = *reinterpret_cast<const pf4*>(xr + 16 * min(jj + 2, JJ - 1));
-        if (jj < JJ) {  // uniform
-          ca = mma(x.x, wf[jj].x, ca);
-          cb = mma(x.y, wf[jj].y, cb);
-          ca = mma(x.z, wf[jj].z, ca);
-          cb = mma(x.w, wf[jj].w, cb);
+      for (int m = 0; m < MI; ++m) {
+        xr[m] = X + (((wave + NW * m) / (2 * NMAT)) * 16 + i) * XS + 4 * kq;
+        ca[m] = cb[m] = pf4{0.f, 0.f, 0.f, 0.f};
+        // software-pipelined: step jj + 2's operand is read while step jj multiplies (clamped to
+        // the last step: a read past JJ is never used)
+        xq[m][0] = *reinterpret_cast<const pf4*>(xr[m]);
+        xq[m][1] = *reinterpret_cast<const pf4*>(xr[m] + 16 * min(1, JJ - 1));
+      }
+#pragma unroll
+      for (int jj = 0; jj < JJM; ++jj) {  // no branch: a guarded MFMA costs accumulator copies
+        pf4 x[MI];
+#pragma unroll
+        for (int m = 0; m < MI; ++m) {
+          x[m] = xq[m][jj & 1];
+          if (jj + 2 < JJM) xq[m][jj & 1] = *reinterpret_cast<const pf4*>(xr[m] + 16 * min(jj + 2, JJ - 1));
+        }
+#pragma unroll
+        for (int m = 0; m < MI; ++m) {
+          ca[m] = mma(x[m].x, wf[jj].x, ca[m]);
+          cb[m] = mma(x[m].y, wf[jj].y, cb[m]);
+          ca[m] = mma(x[m].z, wf[jj].z, ca[m]);
+          cb[m] = mma(x[m].w, wf[jj].w, cb[m]);
         }
       }
       const int col = cb1 * 16 + i;
       const float bias = (mat1 ? tv.b1 : th.b1)[col];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rb1 * 16 + 4 * kq + r;
-        const float z = (ca[r] + cb[r]) + bias;
-        if (!mat1) H1[row * HS + col] = tanhf(z);
-        else D1[row * DS + col] = mode == NPG_EVAL ? tanhf(z) : z;  // FVP: tanh' applied on use
+      for (int m = 0; m < MI; ++m) {
+        const int rb = (wave + NW * m) / (2 * NMAT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * kq + r;
+          const float z = (ca[m][r] + cb[m][r]) + bias;
+          if (!mat1) H1[row * HS + col] = tanhf(z);
+          else D1[row * DS + col] = mode == NPG_EVAL ? tanhf(z) : z;  // FVP: tanh' applied on use
+        }
       }
     }
     lds_barrier();
     NPG_STAMP(2 + 8 * ci + 2);
 
-    // ---- layer 2 (same tile per wave): H2 = tanh(H1 W2^T + b2);
+    // ---- layer 2 (the layer-1 tiles): H2 = tanh(H1 W2^T + b2);
     //      FVP: D2 = H1 V2^T + (D1 (1 - H1^2)) W2^T + vb2; EVAL: D2 = tanh(D1 V2n^T + b2n)
     if ((NPG_PHASES & 2) && f1) {
-      const int rowA = rb1 * 16 + i, u = cb1 * 16 + i;
-      pf4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
-      if (!mat1) {
+      const int u = cb1 * 16 + i;
+      pf4 acc[MI], acc2[MI];
 #pragma unroll
-        for (int s = 0; s < NH / 4; ++s) {
-          const int k = 4 * s + kq;
-          acc = mma(H1[rowA * HS + k], th.w2[u * WS + k], acc);
-        }
-      } else if (mode == NPG_FVP) {
+      for (int m = 0; m < MI; ++m) acc[m] = acc2[m] = pf4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < NH / 4; ++s) {
-          const int k = 4 * s + kq;
-          const float h = H1[rowA * HS + k];
-          acc = mma(h, tv.w2[u * WS + k], acc);
-          acc2 = mma(D1[rowA * DS + k] * (1.f - h * h), th.w2[u * WS + k], acc2);
-        }
-      } else {
+      for (int s = 0; s < NH / 4; ++s) {
+        const int k = 4 * s + kq;
 #pragma unroll
-        for (int s = 0; s < NH / 4; ++s) {
-          const int k = 4 * s + kq;
-          acc = mma(D1[rowA * DS + k], tv.w2[u * WS + k], acc);
+        for (int m = 0; m < MI; ++m) {
+          const int rowA = ((wave + NW * m) / (2 * NMAT)) * 16 + i;
+          if (!mat1) {
+            acc[m] = mma(H1[rowA * HS + k], th.w2[u * WS + k], acc[m]);
+          } else if (mode == NPG_FVP) {
+            const float h = H1[rowA * HS + k];
+            acc[m] = mma(h, tv.w2[u * WS + k], acc[m]);
+            acc2[m] = mma(D1[rowA * DS + k] * (1.f - h * h), th.w2[u * WS + k], acc2[m]);
+          } else {
+            acc[m] = mma(D1[rowA * DS + k], tv.w2[u * WS + k], acc[m]);
+          }
         }
       }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rb1 * 16 + 4 * kq + r;
-        if (!mat1) H2[row * HS + u] = tanhf(acc[r] + th.b2[u]);
-        else if (mode == NPG_FVP) D2[row * DS + u] = (acc[r] + acc2[r]) + tv.b2[u];
-        else D2[row * DS + u] = tanhf(acc[r] + tv.b2[u]);
+      for (int m = 0; m < MI; ++m) {
+        const int rb = (wave + NW * m) / (2 * NMAT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * kq + r;
+          if (!mat1) H2[row * HS + u] = tanhf(acc[m][r] + th.b2[u]);
+          else if (mode == NPG_FVP) D2[row * DS + u] = (acc[m][r] + acc2[m][r]) + tv.b2[u];
+          else D2[row * DS + u] = tanhf(acc[m][r] + tv.b2[u]);
+        }
       }
     }
     lds_barrier();
@@ -423,9 +468,9 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
 
     // ---- output layer: VPG mean -> G (and z -> M); FVP JVP of the mean -> G; EVAL M, new mean G
     if (NPG_PHASES & 4) {
-      const int n3 = mode == NPG_EVAL ? 4 * g.nA : 2 * g.nA;
+      const int n3 = NRB * g.nA * (mode == NPG_EVAL ? 2 : 1);
       for (int it = wave; it < n3; it += NW) {
-        const int rb = it & 1, cbk = (it >> 1) % g.nA, mat = it / (2 * g.nA);
+        const int rb = it % NRB, cbk = (it / NRB) % g.nA, mat = it / (NRB * g.nA);
         const int rowA = rb * 16 + i, u = cbk * 16 + i;
         pf4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
         if (mode == NPG_FVP) {
@@ -477,10 +522,10 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     NPG_STAMP(2 + 8 * ci + 4);
 
     if (mode == NPG_EVAL) {
-      // per row: LL_new - LL_old and sample_kl (gaussian_mlp.py:110-155); 16 threads per row
-      // (actions pc + 16 u), combined over the 16 by butterfly shuffles
+      // per row: LL_new - LL_old and sample_kl (gaussian_mlp.py:110-155); TPR threads per row
+      // (actions pc + TPR u), combined over the TPR by butterfly shuffles
       float dll = 0.f, kl = 0.f;
-      for (int d = pc; d < A; d += 16) {
+      for (int d = pc; d < A; d += TPR) {
         const float ac = ACT[pr * A + d];
         const float mo = M[pr * GS + d], mn = G[pr * GS + d];
         const float so = TAB[d], sn = TAB[g.A16 + d];
@@ -491,7 +536,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         kl += Nr / Dr + tv.ls[d] - th.ls[d];
       }
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
+      for (int o = 1; o < TPR; o <<= 1) {
         dll += __shfl_xor(dll, o);
         kl += __shfl_xor(kl, o);
       }
@@ -502,86 +547,85 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       continue;
     }
 
-    if (NPG_PHASES & 8) {
     // ---- back-propagation, output layer: gW3 | b3 (owned tiles, K = rows);
     //      D2 = (G W3)(1 - H2^2) (tiles from the last wave down); VPG: log_std sums (wave 3)
+    if (NPG_PHASES & 8) {
 #pragma unroll
-    for (int sl = 0; sl < G3SLOTS; ++sl) {
-      const int q = wave + NW * sl;
-      if (q < 3 * g.nA) {
-        const int mb = q / 3, nb = q % 3;
-        pf4 acc = g3[sl];
+      for (int sl = 0; sl < G3SLOTS; ++sl) {
+        const int q = wave + NW * sl;
+        if (q < 3 * g.nA) {
+          const int mb = q / 3, nb = q % 3;
+          pf4 acc = g3[sl];
 #pragma unroll
-        for (int s = 0; s < RC / 4; ++s) {
-          const int k = 4 * s + kq;
-          acc = mma(G[k * GS + mb * 16 + i], H2[k * HS + nb * 16 + i], acc);
+          for (int s = 0; s < RC / 4; ++s) {
+            const int k = 4 * s + kq;
+            acc = mma(G[k * GS + mb * 16 + i], H2[k * HS + nb * 16 + i], acc);
+          }
+          g3[sl] = acc;
         }
-        g3[sl] = acc;
       }
-    }
-    if (NW - 1 - wave < 4) {
-      const int it = NW - 1 - wave, rb = it & 1, cbk = it >> 1;
-      const int rowA = rb * 16 + i, col = cbk * 16 + i;
-      pf4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < g.A16 / 4; ++s) {
-        const int k = 4 * s + kq;
-        acc = mma(G[rowA * GS + k], th.w3[k * WS + col], acc);
-      }
+      for (int it = NW - 1 - wave; it < 2 * NRB; it += NW) {
+        const int rb = it % NRB, cbk = it / NRB;
+        const int rowA = rb * 16 + i, col = cbk * 16 + i;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < g.A16 / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(G[rowA * GS + k], th.w3[k * WS + col], acc);
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * kq + r;
-        const float h = H2[row * HS + col];
-        D2[row * DS + col] = acc[r] * (1.f - h * h);
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * kq + r;
+          const float h = H2[row * HS + col];
+          D2[row * DS + col] = acc[r] * (1.f - h * h);
+        }
       }
-    }
-    if (mode == NPG_VPG && t >= 192 && t < 192 + A) {
-      const int d = t - 192;
-      for (int r = 0; r < nr; ++r) {
-        const float z = M[r * GS + d];
-        gls += ADV[r] * invN * (double)(z * z - 1.f);
+      if (mode == NPG_VPG && t >= 192 && t < 192 + A) {
+        const int d = t - 192;
+        for (int r = 0; r < nr; ++r) {
+          const float z = M[r * GS + d];
+          gls += ADV[r] * invN * (double)(z * z - 1.f);
+        }
       }
-    }
     }
     lds_barrier();
     NPG_STAMP(2 + 8 * ci + 5);
 
+    // ---- layer 2: gW2 | b2 (waves 0-5); D1 = (D2 W2)(1 - H1^2) (tiles from the last wave down)
     if (NPG_PHASES & 16) {
-    // ---- layer 2: gW2 | b2 (waves 0-5); D1 = (D2 W2)(1 - H1^2) (waves 7-4)
-    if (wave < 6) {
-      const int mb = wave / 3, nb = wave % 3;
-      pf4 acc = g2;
+      if (wave < 6) {
+        const int mb = wave / 3, nb = wave % 3;
+        pf4 acc = g2;
 #pragma unroll
-      for (int s = 0; s < RC / 4; ++s) {
-        const int k = 4 * s + kq;
-        acc = mma(D2[k * DS + mb * 16 + i], H1[k * HS + nb * 16 + i], acc);
+        for (int s = 0; s < RC / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(D2[k * DS + mb * 16 + i], H1[k * HS + nb * 16 + i], acc);
+        }
+        g2 = acc;
       }
-      g2 = acc;
-    }
-    if (NW - 1 - wave < 4) {
-      const int it = NW - 1 - wave, rb = it & 1, cbk = it >> 1;
-      const int rowA = rb * 16 + i, col = cbk * 16 + i;
-      pf4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int it = NW - 1 - wave; it < 2 * NRB; it += NW) {
+        const int rb = it % NRB, cbk = it / NRB;
+        const int rowA = rb * 16 + i, col = cbk * 16 + i;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < NH / 4; ++s) {
-        const int k = 4 * s + kq;
-        acc = mma(D2[rowA * DS + k], th.w2[k * WS + col], acc);
-      }
+        for (int s = 0; s < NH / 4; ++s) {
+          const int k = 4 * s + kq;
+          acc = mma(D2[rowA * DS + k], th.w2[k * WS + col], acc);
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rb * 16 + 4 * kq + r;
-        const float h = H1[row * HS + col];
-        D1[row * DS + col] = acc[r] * (1.f - h * h);
+        for (int r = 0; r < 4; ++r) {
+          const int row = rb * 16 + 4 * kq + r;
+          const float h = H1[row * HS + col];
+          D1[row * DS + col] = acc[r] * (1.f - h * h);
+        }
       }
-    }
     }
     lds_barrier();
     NPG_STAMP(2 + 8 * ci + 6);
 
-    if (NPG_PHASES & 32) {
     // ---- layer 1: gW1 | b1 (owned tiles q = wave + 8 sl: mb = wave & 1 for every slot, so the
     //      D1 operand is shared and the slots' chains interleave; the slot count is the block's
     //      ceil(2 nS / 8), a slot past this wave's tiles computes and is discarded)
-    {
+    if (NPG_PHASES & 32) {
       auto bp1 = [&](auto nsl_c) {
         constexpr int NSL = decltype(nsl_c)::value;
         const int mb = wave & 1;
@@ -611,7 +655,6 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         case 4: bp1(std::integral_constant<int, 4>{}); break;
         default: bp1(std::integral_constant<int, G1SLOTS>{}); break;
       }
-    }
     }
     NPG_STAMP(2 + 8 * ci + 7);
   }
@@ -794,10 +837,11 @@ __global__ __launch_bounds__(CGT) void k_npg_cg_step(int P, int A, const double*
   }
 }
 
-size_t npg_lds_bytes(int S, int A, int mode) {
+size_t npg_lds_bytes(int S, int A, int mode, int rc) {
   const Geo g(S, A);
-  const size_t fl = (size_t)small_floats(g) * (mode == NPG_VPG ? 1 : 2) + r4(RC * g.XS) + 2 * r4(RC * HS) +
-                    2 * r4(RC * DS) + 2 * r4(RC * g.GS) + r4(RC * A) + r4(2 * RC) + r4(2 * g.A16);
+  size_t fl = (size_t)small_floats(g) * (mode == NPG_VPG ? 1 : 2) + r4(rc * g.XS) + 2 * r4(rc * HS) +
+              2 * r4(rc * DS) + r4(rc * g.GS) + r4(2 * g.A16);
+  if (mode != NPG_FVP) fl += r4(rc * g.GS) + r4(rc * A) + r4(2 * rc);  // M, ACT, ADV
   return fl * sizeof(float);
 }
 
@@ -815,31 +859,46 @@ extern "C" int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int 
   AMX_CHECK_ARG(mode >= NPG_VPG && mode <= NPG_EVAL, "amx_npg_pass: mode=%d", mode);
   AMX_CHECK_ARG(S > 0 && S <= MAXS && A > 0 && A <= MAXA, "amx_npg_pass: S=%d (<= %d), A=%d (<= %d)", S, MAXS, A,
                 MAXA);
-  AMX_CHECK_ARG(N > 0 && rows_per_block > 0 && rows_per_block % RC == 0,
-                "amx_npg_pass: N=%d rows_per_block=%d (multiple of %d)", N, rows_per_block, RC);
+  AMX_CHECK_ARG(N > 0 && rows_per_block > 0 && rows_per_block % RC0 == 0,
+                "amx_npg_pass: N=%d rows_per_block=%d (multiple of %d)", N, rows_per_block, RC0);
   AMX_CHECK_ARG(obs && act && theta && partials, "amx_npg_pass: null buffer");
   AMX_CHECK_ARG((mode == NPG_FVP || adv) && (mode == NPG_VPG || vec), "amx_npg_pass: adv/vec missing for mode %d",
                 mode);
   AMX_CHECK_ARG(ldo >= S && lda >= A, "amx_npg_pass: ldo=%lld lda=%lld", ldo, lda);
+  AMX_CHECK_ARG(((uintptr_t)theta & 15) == 0 && ((uintptr_t)vec & 15) == 0,
+                "amx_npg_pass: theta / vec must be 16-byte aligned (W1 is read as float4s)");
   NpgArgs a = {};
   a.mode = mode; a.N = N; a.S = S; a.A = A; a.rows_per_block = rows_per_block;
   a.obs = obs; a.ldo = ldo;
   a.act = act; a.lda = lda;
   a.adv = adv; a.theta = theta; a.vec = vec; a.partials = partials;
   a.P = (int)amx_npg_param_count(S, A);
-  const size_t lds = npg_lds_bytes(S, A, mode);
+  const bool of64 = obs_dtype == AMX_IN_F64, af64 = act_dtype == AMX_IN_F64;
+  const size_t lds = npg_lds_bytes(S, A, mode, RC0);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_npg_pass: %zu B of LDS", lds);
   const int blocks = (N + rows_per_block - 1) / rows_per_block;
-  const bool of64 = obs_dtype == AMX_IN_F64, af64 = act_dtype == AMX_IN_F64;
+  // f32 inputs (DeviceNPG casts once per update) get kernels compiled for the layer-1 depth
+  // ceil(S / 16) rounded up to 4, 8, 13 or 16 steps; fp64 inputs the 16-step kernel
+  const int jj = (S + 15) / 16;
   void (*kern)(NpgArgs) = nullptr;
-  if (mode == NPG_FVP)  // actions are not read
-    kern = of64 ? k_npg<NPG_FVP, double, float> : k_npg<NPG_FVP, float, float>;
-  else if (mode == NPG_VPG)
-    kern = of64 ? (af64 ? k_npg<NPG_VPG, double, double> : k_npg<NPG_VPG, double, float>)
-                : (af64 ? k_npg<NPG_VPG, float, double> : k_npg<NPG_VPG, float, float>);
-  else
-    kern = of64 ? (af64 ? k_npg<NPG_EVAL, double, double> : k_npg<NPG_EVAL, double, float>)
-                : (af64 ? k_npg<NPG_EVAL, float, double> : k_npg<NPG_EVAL, float, float>);
+  if (!of64 && (mode == NPG_FVP || !af64)) {
+#define NPG_PICK(J)                                                                                  \
+  kern = mode == NPG_FVP ? k_npg<NPG_FVP, float, float, RC0, J>                                      \
+       : mode == NPG_VPG ? k_npg<NPG_VPG, float, float, RC0, J> : k_npg<NPG_EVAL, float, float, RC0, J>
+    if (jj <= 4) NPG_PICK(4);
+    else if (jj <= 8) NPG_PICK(8);
+    else if (jj <= 13) NPG_PICK(13);
+    else NPG_PICK(16);
+#undef NPG_PICK
+  } else if (mode == NPG_FVP) {  // actions are not read
+    kern = k_npg<NPG_FVP, double, float, RC0, MAXJJ>;
+  } else if (mode == NPG_VPG) {
+    kern = of64 ? (af64 ? k_npg<NPG_VPG, double, double, RC0, MAXJJ> : k_npg<NPG_VPG, double, float, RC0, MAXJJ>)
+                : k_npg<NPG_VPG, float, double, RC0, MAXJJ>;
+  } else {
+    kern = of64 ? (af64 ? k_npg<NPG_EVAL, double, double, RC0, MAXJJ> : k_npg<NPG_EVAL, double, float, RC0, MAXJJ>)
+                : k_npg<NPG_EVAL, float, double, RC0, MAXJJ>;
+  }
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(NT), lds, (hipStream_t)stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;

@@ -139,11 +139,10 @@ class DeviceNPG:
         dev = self.ctx.device
         obs = torch.as_tensor(observations).to(dev)
         act = torch.as_tensor(actions).to(dev)
-        if obs.dtype not in (torch.float32, torch.float64):
-            obs = obs.double()
-        if act.dtype not in (torch.float32, torch.float64):
-            act = act.double()
-        obs, act = obs.contiguous(), act.contiguous()
+        # the policy reads float32(obs) / float32(act) (gaussian_mlp.py:112-117): one cast here
+        # serves every pass of the update and lets the pass kernel take 64-row chunks
+        obs = obs.to(torch.float32).contiguous()
+        act = act.to(torch.float32).contiguous()
         if obs.dim() != 2 or obs.shape[1] != self.S or act.shape != (obs.shape[0], self.A):
             raise ValueError(f"observations {tuple(obs.shape)} / actions {tuple(act.shape)} do not match S, A")
         adv = None

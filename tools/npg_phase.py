@@ -14,6 +14,18 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_npgvar")
+# input dtype of the timed passes: float32 (DeviceNPG casts once per update; 64-row chunks) or
+# NPG_IN=f64 (the C-ABI's fp64 path, 32-row chunks)
+_F64 = os.environ.get("NPG_IN", "f32") == "f64"
+
+
+def IN_CODE(NP):
+    return NP.N.AMX_IN_F64 if _F64 else NP.N.AMX_IN_F32
+
+
+def _in_dt():
+    import torch
+    return torch.float64 if _F64 else torch.float32
 MASKS = {
     0x7F: "all phases",
     0x40: "chunk loads only",
@@ -60,8 +72,8 @@ def time_one(lib, N, S, A):
     from amp_extensions_amd import npg as NP
     layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
     rs = np.random.RandomState(0)
-    obs = torch.from_numpy(0.5 * rs.randn(N, S)).cuda()
-    act = torch.from_numpy(rs.randn(N, A)).cuda()
+    obs = torch.from_numpy(0.5 * rs.randn(N, S)).cuda().to(_in_dt())
+    act = torch.from_numpy(rs.randn(N, A)).cuda().to(_in_dt())
     adv = torch.from_numpy(rs.randn(N)).cuda()
     ctx = amx.AmxContext(S, A, n_models=1, hidden=128, n_hidden=1, device="cuda")
     npg = amx.DeviceNPG(ctx, layers, ls)
@@ -72,8 +84,8 @@ def time_one(lib, N, S, A):
     res = {}
     for mode, name in ((NP.NPG_FVP, "fvp"), (NP.NPG_VPG, "vpg"), (NP.NPG_EVAL, "eval")):
         def call():
-            NP.N.check(ctx.lib.amx_npg_pass(ctx.h, mode, N, obs.data_ptr(), NP.N.AMX_IN_F64, obs.stride(0),
-                                            act.data_ptr(), NP.N.AMX_IN_F64, act.stride(0), adv.data_ptr(),
+            NP.N.check(ctx.lib.amx_npg_pass(ctx.h, mode, N, obs.data_ptr(), IN_CODE(NP), obs.stride(0),
+                                            act.data_ptr(), IN_CODE(NP), act.stride(0), adv.data_ptr(),
                                             npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(),
                                             ctx.stream), "amx_npg_pass")
         for _ in range(3):
@@ -101,8 +113,8 @@ def trace(N, S, A, mode_name="fvp"):
     from amp_extensions_amd import npg as NP
     layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
     rs = np.random.RandomState(0)
-    obs = torch.from_numpy(0.5 * rs.randn(N, S)).cuda()
-    act = torch.from_numpy(rs.randn(N, A)).cuda()
+    obs = torch.from_numpy(0.5 * rs.randn(N, S)).cuda().to(_in_dt())
+    act = torch.from_numpy(rs.randn(N, A)).cuda().to(_in_dt())
     adv = torch.from_numpy(rs.randn(N)).cuda()
     ctx = amx.AmxContext(S, A, n_models=1, hidden=128, n_hidden=1, device="cuda")
     npg = amx.DeviceNPG(ctx, layers, ls)
@@ -111,8 +123,8 @@ def trace(N, S, A, mode_name="fvp"):
     part = torch.empty((N + rpb - 1) // rpb, npg.P, dtype=torch.float64, device="cuda")
     mode = {"fvp": NP.NPG_FVP, "vpg": NP.NPG_VPG, "eval": NP.NPG_EVAL}[mode_name]
     for _ in range(4):
-        NP.N.check(ctx.lib.amx_npg_pass(ctx.h, mode, N, obs.data_ptr(), NP.N.AMX_IN_F64, obs.stride(0),
-                                        act.data_ptr(), NP.N.AMX_IN_F64, act.stride(0), adv.data_ptr(),
+        NP.N.check(ctx.lib.amx_npg_pass(ctx.h, mode, N, obs.data_ptr(), IN_CODE(NP), obs.stride(0),
+                                        act.data_ptr(), IN_CODE(NP), act.stride(0), adv.data_ptr(),
                                         npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(), ctx.stream))
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * 256)()
@@ -120,7 +132,8 @@ def trace(N, S, A, mode_name="fvp"):
     assert ctx.lib.amx_npg_trace_read(buf) == 0
     tr = np.array(buf, dtype=np.int64).reshape(4, 64)
     names = ["stash", "layer1", "layer2", "out", "bp3", "bp2", "bp1(w0)", "barrier"]
-    nch = (rpb + 31) // 32
+    rc = 32
+    nch = (rpb + rc - 1) // rc
     print(f"{mode_name}: N={N} S={S} A={A}, {nch} chunks per block; microseconds (100 MHz clock)")
     for bi, blk in enumerate((0, 64, 128, 255)):
         t = tr[bi]
@@ -135,13 +148,15 @@ def trace(N, S, A, mode_name="fvp"):
                 if seq[k + 1] and seq[k]:
                     per[k] += (seq[k + 1] - seq[k]) / 100
         rows += [f"{n} {v:5.2f}" for n, v in zip(names, per)]
+        rows.append("chunks " + "/".join(f"{((t[2 + 8 * (c + 1)] if c + 1 < nch else t[1]) - t[2 + 8 * c]) / 100:.2f}"
+                                         for c in range(nch)))
         rows.append(f"tail {(t[63] - t[1]) / 100:5.2f}")
         rows.append(f"total {(t[63] - t0) / 100:6.2f}")
         print(f"  block {blk:3d}: " + ", ".join(rows))
 
 
 def run(N, S, A):
-    print(f"NPG pass variants, N={N} S={S} A={A} (fp64 inputs), average of 20 back-to-back launches")
+    print(f"NPG pass variants, N={N} S={S} A={A} ({'fp64' if _F64 else 'fp32'} inputs), average of 20 back-to-back launches")
     for m, what in MASKS.items():
         lib = os.path.join(OUT, f"libamx_hip_{m:02x}.so")
         r = subprocess.run([sys.executable, __file__, "time", lib, str(N), str(S), str(A)], capture_output=True,
