@@ -175,7 +175,7 @@ class DeviceNPG:
         v32 = v.to(torch.float32).contiguous()   # the reference casts the vector to float32
         h = self._pass(NPG_FVP, obs, act, None, v32)
         h[-self.A:] += self._ls_curvature() * v32[-self.A:].double()
-        return h + regu * v32.double()
+        return h + regu * v.to(torch.float64)  # hvp_flat + regu_coef * vector (npg_cg.py:105: the fp64 vector)
 
     def cg_solve(self, obs, act, b: torch.Tensor) -> torch.Tensor:
         """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with

@@ -99,3 +99,50 @@ def test_npg_engine_path_refreshes_policy():
     # the KL of the step is about half the normalized step size (2 * kl_dist = 0.1)
     assert 0.01 < out["kl_dist"] < 0.2
     assert not torch.equal(blob0, pol.blob)
+
+
+def test_npg_device_cg_early_stop():
+    """amx_npg_cg_step's device-side `live` flag is cg_solve's break (mjrl/mjrl/utils/cg_solve.py:
+    9-21): with a residual_tol the solve reaches after 3 of 10 iterations, the device solve returns
+    the reference loop's x, the loop run in fp64 numpy with the device HVP as f_Ax."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy
+    S, A, N = 197, 36, 2048
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    p0 = pack_policy(layers, ls)
+    rs = np.random.RandomState(3)
+    obs = (0.5 * rs.randn(N, S)).astype(np.float32)
+    act = rs.randn(N, A).astype(np.float32)
+    adv = rs.randn(N)
+    npg = make(S, A, p0)
+    b = npg.flat_vpg(obs, act, adv).cpu().numpy()
+
+    def cg_ref(tol):
+        x, r = np.zeros_like(b), b.copy()
+        p, rdotr, hist = r.copy(), r @ r, []
+        for _ in range(10):
+            z = npg.HVP(obs, act, p).cpu().numpy()
+            v = rdotr / (p @ z)
+            x += v * p
+            r -= v * z
+            newrdotr = r @ r
+            mu = newrdotr / rdotr
+            p = r + mu * p
+            rdotr = newrdotr
+            hist.append(rdotr)
+            if rdotr < tol:
+                break
+        return x, hist
+
+    _, hist = cg_ref(0.0)
+    assert len(hist) == 10 and hist[2] < hist[1]
+    tol = float(np.sqrt(hist[2] * hist[1]))  # reached at iteration 3
+    x_ref, hist3 = cg_ref(tol)
+    assert len(hist3) == 3
+    o, a, _ = npg._inputs(obs, act)
+    npg.residual_tol = tol
+    x_dev = npg.cg_solve(o, a, torch.from_numpy(b).to(DEV)).cpu().numpy()
+    assert close(x_dev, x_ref, 1e-7), np.abs(x_dev - x_ref).max()
+    npg.residual_tol = 0.0
+    x10 = npg.cg_solve(o, a, torch.from_numpy(b).to(DEV)).cpu().numpy()
+    assert not close(x10, x_ref, 1e-7)  # the stop mattered
