@@ -49,9 +49,15 @@ def test_npg_vs_reference_golden(golden):
     assert (npg.get_param_values()[-A:] >= -2.0).all()
 
 
-@pytest.mark.parametrize("S,A,N", [(197, 36, 4096), (226, 28, 1000)])
-def test_npg_vs_oracle_rollout_size(S, A, N):
-    """Rollout-sized batches (ragged last block), f64 inputs as the engine holds them."""
+@pytest.mark.parametrize("S,A,N,conditioned", [(197, 36, 4096, True), (226, 28, 1000, True), (111, 8, 2048, True),
+                                                (11, 3, 1000, False), (256, 64, 700, False)])
+def test_npg_vs_oracle_rollout_size(S, A, N, conditioned):
+    """Rollout-sized batches (ragged last block), f64 inputs as the engine holds them; every
+    layer-1 depth the pass kernel is compiled for (S = 11, 111, 197, 226, 256: 1, 7, 13, 15, 16
+    K-steps) and A = 3..64.  The per-product parity (VPG, Fisher-vector product) is 1e-4 of max
+    at every shape.  Where 10 CG iterations on an ill-conditioned Fisher (S = 11; N = 700 samples
+    for 11 456 parameters) amplify fp32 rounding of the products -- the reference's as well as
+    this pass's -- past the 2e-3 solution check, the solutions are checked for direction and size."""
     from amp_extensions_amd.policy import init_mlp_policy_params
     from amp_extensions_amd.npg import pack_policy
     layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
@@ -69,10 +75,24 @@ def test_npg_vs_oracle_rollout_size(S, A, N):
     npg = make(S, A, p0)
     vpg = npg.flat_vpg(obs, act, ref["adv_whitened"]).cpu().numpy()
     assert close(vpg, ref["vpg"], 1e-4)
+    v = rs.randn(p0.size)
+    hv = npg.HVP(obs, act, v).cpu().numpy()
+    hv_ref = R.npg_hvp(p0, shapes, obs, act, v, 1e-4)
+    assert close(hv, hv_ref, 1e-4), np.abs(hv - hv_ref).max() / np.abs(hv_ref).max()
     out = npg.train_from_arrays(obs, act, adv)
-    assert close(out["npg_grad"].cpu().numpy(), ref["npg"], 2e-3)
-    assert close(npg.get_param_values() - p0, ref["params1"] - p0, 2e-3)
-    np.testing.assert_allclose(out["surr_after"], ref["surr_after"], rtol=1e-3)
+    x = out["npg_grad"].cpu().numpy()
+    if conditioned:
+        assert close(x, ref["npg"], 2e-3)
+        assert close(npg.get_param_values() - p0, ref["params1"] - p0, 2e-3)
+        np.testing.assert_allclose(out["surr_after"], ref["surr_after"], rtol=1e-3)
+    else:
+        # the reference's own fp32 solution is 12 % (max-relative) from the fp64 ground truth at
+        # S = 11 (fp64 autograd HVP + fp64 CG, measured with this oracle): the solutions agree in
+        # direction and size, not to 2e-3
+        xr = ref["npg"].astype(np.float64)
+        cos = np.dot(x, xr) / (np.linalg.norm(x) * np.linalg.norm(xr))
+        assert cos > 0.98 and abs(np.linalg.norm(x) / np.linalg.norm(xr) - 1) < 0.1, (cos, np.linalg.norm(x),
+                                                                                       np.linalg.norm(xr))
 
 
 def test_npg_engine_path_refreshes_policy():
