@@ -166,3 +166,26 @@ def test_npg_device_cg_early_stop():
     npg.residual_tol = 0.0
     x10 = npg.cg_solve(o, a, torch.from_numpy(b).to(DEV)).cpu().numpy()
     assert not close(x10, x_ref, 1e-7)  # the stop mattered
+
+
+def test_npg_pass_input_dtypes_bit_identical():
+    """amx_npg_pass on fp64 and fp32 inputs (the fp64 C-ABI path: 16 layer-1 K-steps compiled; the
+    fp32 path DeviceNPG takes: ceil(S / 16) rounded to 4 / 8 / 13 / 16) gives the same bits in all
+    three modes -- the kernels read float32(obs) either way and the extra K-steps add exact zeros."""
+    from amp_extensions_amd import npg as NP
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy
+    S, A, N = 197, 36, 2000
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=5, init_log_std=-0.4)
+    p0 = pack_policy(layers, ls)
+    npg = make(S, A, p0)
+    rs = np.random.RandomState(11)
+    obs64 = torch.from_numpy(0.5 * rs.randn(N, S)).to(DEV)
+    act64 = torch.from_numpy(rs.randn(N, A)).to(DEV)
+    adv = torch.from_numpy(rs.randn(N)).to(DEV)
+    vec = torch.from_numpy(rs.randn(npg.P).astype(np.float32)).to(DEV)
+    newp = (npg.theta + 0.01 * vec).contiguous()
+    for mode, v in ((NP.NPG_VPG, None), (NP.NPG_FVP, vec), (NP.NPG_EVAL, newp)):
+        a64 = npg._pass(mode, obs64, act64, adv, v).cpu().numpy()
+        a32 = npg._pass(mode, obs64.float().contiguous(), act64.float().contiguous(), adv, v).cpu().numpy()
+        np.testing.assert_array_equal(a64, a32)
