@@ -1863,13 +1863,37 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
 }
 
 // Output-layer tiles (128 x 224, S <= 224) of a stream-K launch for `rows` padded lanes x
-// `groups` members, 0 when the shape does not use it: fewer tiles than CUs but at least half
-// as many (so a tile's K range spans at most 3 of the evenly dealt workgroup ranges).
-static int streamk_tiles(const amx_ctx* ctx, int groups, int rows) {
+// `groups` members, 0 when the shape does not use it; *nwg workgroups, *ksplit slots per tile.
+//  * fewer tiles than CUs but at least half as many (4096-7168 lanes x 4 members): one workgroup
+//    per CU, the tiles' K-tiles dealt out evenly, so a tile's K range spans at most 3 workgroups;
+//  * fewer than half (the reference-semantics sampler's few hundred lanes: 20 tiles at 640):
+//    SPLIT = min(CUs / tiles, 6) workgroups per tile, each a contiguous K range (nwg = tiles x
+//    SPLIT, so every tile is exactly SPLIT segments); a one-wave tile grid left most CUs idle
+//    and ran the whole K = 2304 chain per tile (71 us at 640 lanes).  The last arriver reads
+//    SPLIT - 1 partial tiles, so SPLIT stays small.
+static int streamk_tiles(const amx_ctx* ctx, int groups, int rows, int* nwg = nullptr, int* ksplit = nullptr,
+                         int K = 0) {
   const int n32 = amx::round_up(ctx->S, 32);
   if (n32 <= 128 || n32 > 224 || rows % 128 != 0) return 0;
   const int tiles = rows / 128 * groups;
-  return (tiles < ctx->n_cus && 2 * tiles >= ctx->n_cus) ? tiles : 0;
+  if (tiles < ctx->n_cus && 2 * tiles >= ctx->n_cus) {
+    if (nwg) *nwg = ctx->n_cus;
+    if (ksplit) *ksplit = 3;
+    return tiles;
+  }
+  if (tiles >= 1 && 2 * tiles < ctx->n_cus) {
+    int split = ctx->n_cus / tiles;
+    split = split > 6 ? 6 : split;
+    if (K > 0) {  // at least 4 K-tiles (of 32) per segment
+      const int nk = K / 32;
+      while (split > 1 && nk / split < 4) --split;
+    }
+    if (split < 2) return 0;
+    if (nwg) *nwg = tiles * split;
+    if (ksplit) *ksplit = split;
+    return tiles;
+  }
+  return 0;
 }
 
 extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
@@ -1906,10 +1930,11 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   if (ring) {
     const int bn = ring == 3 ? 224 : 16 * nb16;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * bn || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
-    const int tiles = streamk_tiles(ctx, groups, rows);
+    int nwg = 0, ksplit = 0;
+    const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K);
     if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
-        ctx->split_floats >= (long long)tiles * 3 * 128 * bn) {
-      a.ksplit = 3; a.streamk = ctx->n_cus; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+        ctx->split_floats >= (long long)tiles * ksplit * 128 * bn) {
+      a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
     }
     if (ring == 3) return launch_ring<TileRing<4, 2, 2, 7>>(a, s);
     switch (nb16) {
@@ -1931,10 +1956,11 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     // lane counts whose 128 x 224 tiles (14 waves) are fewer than the CUs (4096-7168 lanes x 4
     // members: 128-224 tiles): stream-K over one workgroup per CU (each tile's K range in <= 3
     // segments), instead of the row-block tiles' 4-7 waves per workgroup
-    const int tiles = streamk_tiles(ctx, groups, rows);
+    int nwg = 0, ksplit = 0;
+    const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K);
     if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
-        ctx->split_floats >= (long long)tiles * 3 * 128 * 224) {
-      a.ksplit = 3; a.streamk = ctx->n_cus; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+        ctx->split_floats >= (long long)tiles * ksplit * 128 * 224) {
+      a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
       return launch_h3<EPI_UNNORM, H128x224>(a, s);
     }
     if (row_tiles) {
@@ -2016,7 +2042,8 @@ extern "C" int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long f
 
 extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters) {
   if (!ctx || groups < 1 || rows <= 0) return -1;
-  const int tiles = streamk_tiles(ctx, groups, rows);
+  int nwg = 0, ksplit = 0;
+  const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, ctx->k0_pad + ctx->L * ctx->H);
   if (n_counters) *n_counters = tiles;
-  return (long long)tiles * 3 * 128 * 224;
+  return (long long)tiles * ksplit * 128 * 224;
 }
