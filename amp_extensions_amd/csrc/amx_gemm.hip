@@ -1114,7 +1114,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       __builtin_amdgcn_sched_barrier(0);
       compute(cur * STAGE);
     }
-    if constexpr (TL::M16 && EPI == EPI_UNNORM) {
+    if constexpr (TL::M16 && (EPI == EPI_UNNORM || EPI == EPI_BIAS_ACT)) {
       if (nseg > 1) {
         __syncthreads();  // the stage buffers are free: one int of LDS for the last-arriver flag
         if (!split_combine<TL>(a, acc, tile, seg, nseg, reinterpret_cast<int*>(smem) + BM + 4)) return;
@@ -1815,6 +1815,24 @@ extern "C" int amx_row_exponents(amx_ctx* ctx, int groups, int rows, int K, cons
   return AMX_OK;
 }
 
+// Hidden-layer tiles of a stream-K launch (128 x 256, HRow<4>) when 128 x 256 tiles would fill
+// less than half the CUs (rows < 2048 at 4 members, N = 512): SPLIT = min(CUs / tiles, 6)
+// workgroups per tile over contiguous K ranges of at least 4 K-tiles, combined in K order by the
+// last arriver before the bias / ReLU / row-exponent epilogue.  0: not used.  (At the sampler's
+// 640 lanes the 128 x 128 grid put 80 workgroups on the CUs: 37 us per layer.)
+static int streamk_hidden(const amx_ctx* ctx, int groups, int rows, int N, int K, int* nwg, int* ksplit) {
+  if (N % 256 != 0 || K % 32 != 0 || rows % 128 != 0) return 0;
+  const int tiles = rows / 128 * (N / 256) * groups;
+  if (tiles < 1 || 2 * tiles >= ctx->n_cus) return 0;
+  int split = ctx->n_cus / tiles;
+  split = split > 6 ? 6 : split;
+  while (split > 1 && (K / 32) / split < 4) --split;
+  if (split < 2) return 0;
+  *nwg = tiles * split;
+  *ksplit = split;
+  return tiles;
+}
+
 extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
                                     long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
                                     long long strideWexp, const float* bias, long long strideBias, float* C, int ldc,
@@ -1856,6 +1874,15 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
         case 224: return launch_h3<EPI_BIAS_ACT, HRow<7>>(a, s);
         default: break;
       }
+    }
+  }
+  {  // few tiles (the sampler's few hundred lanes): 128 x 256 tiles split over K (stream-K)
+    int nwg = 0, ksplit = 0;
+    const int tiles = streamk_hidden(ctx, groups, rows, N, K, &nwg, &ksplit);
+    if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
+        ctx->split_floats >= (long long)tiles * ksplit * 128 * 256) {
+      a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+      return launch_h3<EPI_BIAS_ACT, HRow<4>>(a, s);
     }
   }
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
@@ -2042,8 +2069,14 @@ extern "C" int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long f
 
 extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters) {
   if (!ctx || groups < 1 || rows <= 0) return -1;
-  int nwg = 0, ksplit = 0;
+  int nwg = 0, ksplit = 0, nwg_h = 0, ksplit_h = 0;
   const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, ctx->k0_pad + ctx->L * ctx->H);
-  if (n_counters) *n_counters = tiles;
-  return (long long)tiles * ksplit * 128 * 224;
+  // the hidden layers' split at their largest K (every smaller K splits no wider)
+  const int tiles_h = ctx->H % 256 == 0 && ctx->L > 1
+                          ? streamk_hidden(ctx, groups, rows, ctx->H, ctx->k0_pad + (ctx->L - 1) * ctx->H, &nwg_h,
+                                           &ksplit_h)
+                          : 0;
+  if (n_counters) *n_counters = tiles > tiles_h ? tiles : tiles_h;
+  const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
+  return fo > fh ? fo : fh;
 }
