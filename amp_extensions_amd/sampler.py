@@ -356,7 +356,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
 
 def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_workers: int = 4, mode: str = "samples",
                   eval_mode: bool = False, verbose: bool = False, deepmimic: bool = False, rng: str = "reference",
-                  chunk: int = 8, speculate: bool = True, graph: bool = True):
+                  chunk: int = 16, speculate: bool = True, graph: bool = True):
     """milo.sampler.sample_points on the GPU.  `env` is a BatchedSimEnv (or a RolloutEngine):
     its ensemble, reset source and termination are used, and its lane count caps the
     concurrency; `policy` a DevicePolicy.  Returns the reference's list of path dicts

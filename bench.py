@@ -98,6 +98,8 @@ def parse():
                    help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward (valid "
                         "only while consecutive rollouts share the policy: fixed-policy collection / evaluation; "
                         "a trainer updates the policy between iterations, so the default is the serial order)")
+    p.add_argument("--paths-chunk", type=int, default=16,
+                   help="--mode paths: synchronous steps per sampler chunk (one host round trip each)")
     p.add_argument("--mode", choices=["engine", "paths", "train"], default="engine",
                    help="engine: persistent lanes x synchronous steps + device relabel (throughput); paths: the "
                         "reference's semantics through the drop-in surfaces -- sample_points(num_to_collect, "
@@ -401,7 +403,7 @@ def main():
         def one_rollout():
             it[0] += 1
             paths = amx.sample_points(eng, pol, num_to_collect=per_rank, base_seed=1000 * rank + it[0],
-                                      num_workers=args.workers)
+                                      num_workers=args.workers, chunk=args.paths_chunk)
             relabel_paths(paths, cost, ens, allreduce=allreduce)
             n = sum(len(p["rewards"]) for p in paths)
             paths_info.update(paths=len(paths), samples=n)
@@ -548,7 +550,7 @@ def main():
                 **({} if args.mode != "paths" else {
                     "mode": (f"reference semantics: sample_points(num_to_collect={per_rank}, num_workers="
                              f"{args.workers}) -> complete exact-seeded trajectories (per-worker quota "
-                             f"ceil(N/W)), host path dicts -> relabel_paths; chunks of 8 steps replayed as "
+                             f"ceil(N/W)), host path dicts -> relabel_paths; chunks of {args.paths_chunk} steps replayed as "
                              f"HIP graphs, speculative admission"),
                     "samples_per_rollout": paths_info.get("samples", 0) * world,
                     "samples_per_rollout_per_gpu": paths_info.get("samples", 0),
