@@ -77,6 +77,18 @@ class _Store:
         self.obs, self.nxt, self.act, self.mean = new
         self.cap = cap
 
+    def append_from(self, src, idx: torch.Tensor) -> int:
+        """Rows idx of the flat [K * L] chunk arrays src = (obs, next_obs, acts, means)."""
+        m = idx.numel()
+        if self.n + m > self.cap:
+            self._alloc(max(2 * self.cap, self.n + m))
+        s = slice(self.n, self.n + m)
+        for dst, x in zip((self.obs, self.nxt, self.act, self.mean), src):
+            torch.index_select(x, 0, idx, out=dst[s])
+        base = self.n
+        self.n += m
+        return base
+
     def append(self, eng: RolloutEngine, K: int, idx: torch.Tensor) -> int:
         m = idx.numel()
         if self.n + m > self.cap:
@@ -354,9 +366,222 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     return paths, off
 
 
+
+class _ChunkRing:
+    """Two device copies of a chunk's K x L transitions: chunk i is copied into slot i % 2 right
+    after its steps (no host information needed), so chunk i + 1 can be queued before chunk i's
+    done flags are read; chunk i's rows are compacted from its slot one iteration later."""
+
+    def __init__(self, eng: RolloutEngine, K: int):
+        c = eng.ctx
+        m = K * eng.B
+        z = lambda w, dt: torch.empty(m, w, dtype=dt, device=c.device)
+        self.slots = [(z(c.S, torch.float64), z(c.S, torch.float64), z(c.A, torch.float64), z(c.A, torch.float32))
+                      for _ in range(2)]
+        self.K, self.m = K, m
+
+    def snapshot(self, eng: RolloutEngine, si: int) -> None:
+        K, m = self.K, self.m
+        for dst, src in zip(self.slots[si], (eng.obs, eng.next_obs, eng.acts, eng.means)):
+            dst.copy_(src[:K].reshape(m, dst.shape[1]))
+
+
+def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, rng: str,
+                       eval_mode: bool, speculate: bool = True, graph: bool = True):
+    """_collect with the host one chunk behind the GPU: chunk i is queued (resets, noise, the
+    captured steps, a raw copy of its transitions and an async copy of its done flags) before
+    chunk i-1's done flags are read and its trajectories advanced.  Admission therefore sees
+    the results through chunk i-2: a lane whose trajectory ended in chunk i-1 runs chunk i
+    idle (its steps are never attributed: each chunk keeps the lane -> trajectory map it was
+    launched with) and is re-admitted one chunk later.  Trajectories are exact-seeded, so the
+    result is _collect's (the same trajectories 1..n_i per worker, the same transitions)."""
+    c = eng.ctx
+    L, S, A, K, dev = eng.B, c.S, c.A, eng.K, c.device
+    R = eng.term.horizon
+    motion = eng.motion
+    time_max = motion.get_motion_length() if motion is not None else float(eng.table.shape[0])
+    adm: list[list[_Traj]] = [[] for _ in range(W)]
+    next_j = [1] * W
+    done_w = [False] * W
+    lane_tr: list[_Traj | None] = [None] * L
+    free = list(range(L - 1, -1, -1))
+    store = _Store(dev, S, A, W * (quota + R) if mode == "samples" else W * quota * 64)
+    ring = _ChunkRing(eng, K)
+    eng.eval_mode = eval_mode
+    ref_noise = rng == "reference" and not eval_mode
+    hn = _HostNoise(c.lib, L, K, A) if ref_noise else None
+    noise_dev = torch.zeros(K, L, A, dtype=torch.float64, device=dev) if ref_noise else None
+    pin = torch.cuda.is_available()
+    # two sets of pinned staging: set i % 2 is rewritten only after chunk i - 2 has completed
+    stage = []
+    for _ in range(2):
+        mh = torch.zeros(L, dtype=torch.uint8, pin_memory=pin)
+        ch = torch.zeros(L, dtype=torch.int32, pin_memory=pin)
+        rh = torch.zeros(L, dtype=torch.float64 if motion is not None else torch.int32, pin_memory=pin)
+        dh = torch.zeros(K, L, dtype=torch.uint8, pin_memory=pin)
+        fh = torch.zeros(K * L, dtype=torch.int64, pin_memory=pin)  # compaction indices (async upload)
+        stage.append((mh, ch, rh, dh, torch.cuda.Event() if pin else None, fh))
+    mask_dev = torch.empty(L, dtype=torch.uint8, device=dev)
+    counts_dev = torch.empty(L, dtype=torch.int32, device=dev)
+    rows_dev = torch.empty(L, dtype=stage[0][2].dtype, device=dev)
+    ended_sum, ended_n = 0, 0
+    chunk_graph = None
+    chunks, budget = 0, 4 * (W * quota + W) * (R + K) // K + 64
+    pending = None  # (set index, [(lane, trajectory)]) of the queued, unread chunk
+
+    def drop(tr: _Traj) -> None:
+        if tr.lane >= 0:
+            lane_tr[tr.lane] = None
+            free.append(tr.lane)
+            tr.lane = -1
+
+    def process(p) -> None:
+        nonlocal ended_sum, ended_n
+        si, launched = p
+        ev = stage[si][4]
+        if ev is not None:
+            ev.synchronize()
+        # lanes whose trajectory is still running on them (not ended earlier, not dropped)
+        live = [(b, tr) for b, tr in launched if not tr.ended and tr.lane == b]
+        if not live:
+            return
+        lanes = np.array([b for b, _ in live], np.int64)
+        d = stage[si][3].numpy().astype(bool)[:, lanes]  # [K, n live]
+        hit = d.any(axis=0)
+        n = np.where(hit, d.argmax(axis=0) + 1, K)
+        starts = np.cumsum(n) - n
+        step_of = np.arange(int(n.sum())) - np.repeat(starts, n)
+        flat = step_of * L + np.repeat(lanes, n)
+        # pinned + non_blocking: a pageable upload would wait for the chunk queued behind this one
+        fh = stage[si][5]
+        fh.numpy()[:flat.size] = flat
+        base = store.append_from(ring.slots[si], fh[:flat.size].to(dev, non_blocking=True))
+        for i, (b, tr) in enumerate(live):
+            tr.segs.append((base + int(starts[i]), int(n[i])))
+            tr.length += int(n[i])
+            if hit[i]:
+                tr.ended = True
+                ended_sum += tr.length
+                ended_n += 1
+                drop(tr)
+
+    while True:
+        lhat = float(R) if not speculate else (ended_sum / ended_n if ended_n >= 4 else 0.5 * R)
+        for w in range(W):
+            if done_w[w]:
+                continue
+            trs = adm[w]
+            if mode == "samples":
+                lb, cut = 0, len(trs)
+                for i, tr in enumerate(trs):
+                    if lb >= quota:
+                        cut = i
+                        break
+                    lb += tr.length
+                for tr in trs[cut:]:
+                    drop(tr)
+                del trs[cut:]
+                if trs and all(tr.ended for tr in trs) and sum(tr.length for tr in trs) >= quota:
+                    done_w[w] = True
+            elif len(trs) == quota and all(tr.ended for tr in trs):
+                done_w[w] = True
+        new = []
+        progress = True
+        while free and progress:
+            progress = False
+            for w in range(W):
+                if not free or done_w[w]:
+                    continue
+                trs = adm[w]
+                if mode == "samples":
+                    lb = sum(tr.length for tr in trs)
+                    est = sum(tr.length if tr.ended else max(tr.length, lhat) for tr in trs)
+                    ok = lb < quota and est < quota
+                else:
+                    ok = len(trs) < quota
+                if ok:
+                    j = next_j[w]
+                    next_j[w] += 1
+                    tr = _Traj(w, j, 12345 + base_seed * w + j)
+                    tr.lane = free.pop()
+                    lane_tr[tr.lane] = tr
+                    trs.append(tr)
+                    new.append(tr)
+                    progress = True
+        active = np.array([b for b in range(L) if lane_tr[b] is not None], np.int64)
+        if active.size == 0:
+            if pending is None:
+                break
+            process(pending)  # the last queued chunk may end trajectories or free admissions
+            pending = None
+            continue
+        chunks += 1
+        if chunks > budget:
+            raise RuntimeError("sample_points: step budget exhausted (trajectories longer than the horizon?)")
+        si = chunks & 1
+        mask_h, counts_h, rows_h, done_h, ev, _ = stage[si]
+        mask_np, counts_np, rows_np = mask_h.numpy(), counts_h.numpy(), rows_h.numpy()
+        eng.begin_rollout()
+        mask_np.fill(1)
+        mask_np[active] = 0
+        counts_np.fill(0)
+        new_lanes = np.array([tr.lane for tr in new], np.int64)
+        for tr in new:
+            mask_np[tr.lane] = 1
+            counts_np[tr.lane] = tr.j - 1
+            if rng == "reference":
+                t = _gym_np_random(tr.seed).uniform(low=0, high=time_max)  # seed_env + reset (sim_env.py:132,276)
+                rows_np[tr.lane] = t if motion is not None else int(np.floor(t))
+        mask_dev.copy_(mask_h, non_blocking=True)
+        counts_dev.copy_(counts_h, non_blocking=True)
+        torch.where(mask_dev.bool(), counts_dev, eng.reset_count, out=eng.reset_count)
+        if rng == "reference":
+            rows_dev.copy_(rows_h, non_blocking=True)
+        eng.reset_lanes(mask_dev, rows_dev if rng == "reference" else None)
+        if hn is not None:
+            if new:
+                hn.seed(new_lanes, np.array([tr.seed for tr in new]))  # np.random.seed (sampler.py:39)
+            buf = hn.bufs[si]
+            hn.draw(active, buf)  # the next K draws of every lane in flight (finished ones idle)
+            noise_dev.copy_(buf, non_blocking=True)
+        if graph and chunk_graph is None and chunks >= 2:  # (the first chunk allocates the workspaces)
+            eng.begin_rollout()
+            chunk_graph = _ChunkGraph(eng, K, noise_dev)
+        if chunk_graph is not None:
+            chunk_graph.replay()
+        else:
+            for k in range(K):
+                eng.step(noise=None if noise_dev is None else noise_dev[k])
+        ring.snapshot(eng, si)
+        done_h.copy_(eng.done[:K], non_blocking=True)
+        if ev is not None:
+            ev.record()
+        launched = [(int(b), lane_tr[b]) for b in active.tolist()]
+        if pending is not None:
+            process(pending)
+        pending = (si, launched)
+    trajs = [tr for w in range(W) for tr in adm[w]]
+    if not trajs:
+        return [], 0
+    perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
+    pd = torch.from_numpy(perm).to(dev)
+    host = [x.index_select(0, pd).cpu().numpy() for x in (store.obs, store.nxt, store.act, store.mean)]
+    log_std = np.float64(eng.policy.log_std_val)
+    paths, off = [], 0
+    for tr in trajs:
+        T = tr.length
+        sl = slice(off, off + T)
+        m = host[3][sl]
+        paths.append(dict(observations=host[0][sl], next_observations=host[1][sl], actions=host[2][sl],
+                          rewards=np.zeros(T, dtype=np.int64),
+                          agent_infos=dict(mean=m, log_std=np.tile(log_std, (T, 1)), evaluation=m),
+                          env_infos=[{} for _ in range(T)], terminated=True))
+        off += T
+    return paths, off
+
 def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_workers: int = 4, mode: str = "samples",
                   eval_mode: bool = False, verbose: bool = False, deepmimic: bool = False, rng: str = "reference",
-                  chunk: int = 16, speculate: bool = True, graph: bool = True):
+                  chunk: int = 16, speculate: bool = True, graph: bool = True, pipeline: bool = True):
     """milo.sampler.sample_points on the GPU.  `env` is a BatchedSimEnv (or a RolloutEngine):
     its ensemble, reset source and termination are used, and its lane count caps the
     concurrency; `policy` a DevicePolicy.  Returns the reference's list of path dicts
@@ -364,7 +589,9 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
     log_std, evaluation}, env_infos, terminated).  A missing info['valid'] counts as valid
     (SimEnv returns {}; the reference's deepmimic=True branch, sampler.py:61, would raise).
     `speculate`: admit beyond the worst-case reservation from the observed trajectory lengths
-    (same result, see _collect); `graph`: replay each chunk's steps as a captured HIP graph."""
+    (same result, see _collect); `graph`: replay each chunk's steps as a captured HIP graph;
+    `pipeline`: queue chunk i before reading chunk i-1's done flags (same result,
+    _collect_pipelined)."""
     assert mode == "samples" or mode == "trajectories"
     if rng not in ("reference", "device"):
         raise ValueError("rng must be 'reference' or 'device'")
@@ -381,7 +608,8 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
     if rng == "device":
         policy.seed = (12345 + int(base_seed)) & 0xFFFFFFFFFFFFFFFF
     t0 = time.time()
-    paths, n = (_collect(eng, W, quota, mode, int(base_seed), rng, eval_mode, speculate=speculate, graph=graph)
+    collect = _collect_pipelined if pipeline else _collect
+    paths, n = (collect(eng, W, quota, mode, int(base_seed), rng, eval_mode, speculate=speculate, graph=graph)
                 if quota > 0 else ([], 0))
     if verbose:
         print(f"Collected {n} and {len(paths)} trajectories in {time.time() - t0} seconds")

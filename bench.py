@@ -98,6 +98,8 @@ def parse():
                    help="N > 1: overlap each rollout's all-reduce with the next rollout's first forward (valid "
                         "only while consecutive rollouts share the policy: fixed-policy collection / evaluation; "
                         "a trainer updates the policy between iterations, so the default is the serial order)")
+    p.add_argument("--paths-serial", action="store_true",
+                   help="--mode paths: the serial chunk loop (read each chunk's done flags before queueing the next)")
     p.add_argument("--paths-chunk", type=int, default=16,
                    help="--mode paths: synchronous steps per sampler chunk (one host round trip each)")
     p.add_argument("--mode", choices=["engine", "paths", "train"], default="engine",
@@ -403,7 +405,8 @@ def main():
         def one_rollout():
             it[0] += 1
             paths = amx.sample_points(eng, pol, num_to_collect=per_rank, base_seed=1000 * rank + it[0],
-                                      num_workers=args.workers, chunk=args.paths_chunk)
+                                      num_workers=args.workers, chunk=args.paths_chunk,
+                                      pipeline=not args.paths_serial)
             relabel_paths(paths, cost, ens, allreduce=allreduce)
             n = sum(len(p["rewards"]) for p in paths)
             paths_info.update(paths=len(paths), samples=n)

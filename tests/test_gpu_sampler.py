@@ -82,12 +82,13 @@ def test_sample_points_reproduces_reference_g8(setup, golden):
 
 @pytest.mark.parametrize("mode,N,horizon,chunk", [("samples", 400, 40, 8), ("samples", 257, 25, 5),
                                                   ("trajectories", 9, 30, 8), ("samples", 900, 30, 4)])
-@pytest.mark.parametrize("speculate,graph", [(True, True), (False, False), (True, False)])
-def test_sample_points_matches_oracle(setup, mode, N, horizon, chunk, speculate, graph):
+@pytest.mark.parametrize("speculate,graph,pipeline", [(True, True, True), (False, False, True), (True, False, True),
+                                                       (True, True, False), (False, False, False)])
+def test_sample_points_matches_oracle(setup, mode, N, horizon, chunk, speculate, graph, pipeline):
     """W=2 and W=3 workers vs the oracle's sequential get_samples with the same seeds, on a
     standing reset table (long trajectories: several chunks, mid-chunk ends, refills), with the
-    speculative admission (surplus trajectories run and are dropped) and the chunk HIP graph on
-    and off: the same paths either way."""
+    speculative admission (surplus trajectories run and are dropped), the chunk HIP graph and the
+    pipelined chunk loop (the host one chunk behind the GPU) on and off: the same paths."""
     amx, ens, ens_w, norms, pw, log_std, pol = setup
     from amp_extensions_amd.synthetic import reset_table
     table = reset_table(256, S, 1)
@@ -96,7 +97,7 @@ def test_sample_points_matches_oracle(setup, mode, N, horizon, chunk, speculate,
     for W in (2, 3):
         env = amx.BatchedSimEnv(ens, table, lanes=512, horizon=horizon, record_means=True)
         paths = amx.sample_points(env, pol, num_to_collect=N, base_seed=7, num_workers=W, mode=mode, chunk=chunk,
-                                  speculate=speculate, graph=graph)
+                                  speculate=speculate, graph=graph, pipeline=pipeline)
         per = math.ceil(N / W)
         ref = []
         for i in range(W):
@@ -147,3 +148,23 @@ def test_sample_points_eval_mode_and_member_rotation(setup):
         pred = R.ensemble_preds(ens_w, norms, torch.from_numpy(o).float(), torch.from_numpy(a).float()).numpy()
         want = o[0] + pred[j % 4, 0].astype(np.float64)
         _state_close(p["next_observations"][0], want, f"trajectory {j}")
+
+
+def test_sample_points_pipelined_bit_identical(setup):
+    """The pipelined chunk loop (chunk i queued before chunk i-1's done flags are read; lanes
+    re-admitted one chunk later) returns the serial loop's paths bit for bit: the same
+    trajectories in the same order, every array equal."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    from amp_extensions_amd.synthetic import reset_table
+    table = reset_table(256, S, 2)
+    table[::5, 2] = -2.0
+    table[1::4, 2] = -0.3
+    env = amx.BatchedSimEnv(ens, table, lanes=512, horizon=60, record_means=True)
+    for W, N, chunk in ((2, 1500, 16), (4, 999, 7)):
+        a = amx.sample_points(env, pol, num_to_collect=N, base_seed=11, num_workers=W, chunk=chunk, pipeline=False)
+        b = amx.sample_points(env, pol, num_to_collect=N, base_seed=11, num_workers=W, chunk=chunk, pipeline=True)
+        assert len(a) == len(b)
+        for pa, pb in zip(a, b):
+            for k in ("observations", "next_observations", "actions"):
+                np.testing.assert_array_equal(pa[k], pb[k])
+            np.testing.assert_array_equal(pa["agent_infos"]["mean"], pb["agent_infos"]["mean"])
