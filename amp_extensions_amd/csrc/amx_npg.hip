@@ -19,20 +19,21 @@
 //
 // Layout (round 3): a block of 8 waves walks its rows in chunks of 32.  Every product is a
 // 16x16 tile on the f32 matrix pipe (v_mfma_f32_16x16x4_f32, an exact f32 fma chain):
-//   * forward layer 1 (K = S, most of the flops): wave w owns the tile (rows 16 (w & 1),
-//     units 16 ((w >> 1) & 1), parameter set w >> 2) and keeps that tile's W1 (or tangent V1)
-//     rows in registers for the whole kernel (16 float4 per lane at S = 256); the chunk's
-//     observations are the only K-long operand in LDS, read as float4s;
+//   * forward layer 1 (K = S, most of the flops): wave w owns the tile (units 16 (w & 1),
+//     parameter set (w >> 1) % sets, rows 16 of the chunk) and keeps that tile's W1 (or tangent
+//     V1) rows in registers for the whole kernel (staged once through LDS; kernels are compiled
+//     for ceil(S / 16) rounded to 4 / 8 / 13 / 16 K-steps, so no MFMA sits under a branch); the
+//     chunk's observations are the only K-long operand in LDS, read as float4s;
 //   * layers 2 / 3 and the back-propagated deltas are 16x16 tiles over K = 32 / A, dealt
 //     over the waves; the tanh derivative of a JVP is applied as its operand is loaded;
 //   * the weight gradients (K = the chunk's rows) are tiles each wave owns across chunks,
 //     accumulated on the matrix pipe in fp32 over the block's rows (fp64 across blocks in
-//     amx_npg_reduce); the bias gradients come out of the same tiles through a column of ones next to
-//     the layer's input (x[S] = 1, h[32] = 1: grad b = sum_r delta_r * 1);
+//     amx_npg_reduce); the bias gradients come out of the same tiles through a column of ones
+//     next to the layer's input (x[S] = 1, h[32] = 1: grad b = sum_r delta_r * 1);
 //   * the next chunk's observations / actions / advantages are loaded into registers while
-//     the current chunk computes.
+//     the current chunk computes, across LDS-only barriers.
 // Round 2's kernel (scalar LDS FMA loops, 4 waves, 1 chunk-sum per thread) took 431 us per
-// pass at 40960 x 197; see DESIGN.md section 6 for this one's time.
+// FVP pass at 40960 x 197; this one 60 ('The NPG learner').
 #include "amx_common.h"
 
 #include <type_traits>
@@ -61,7 +62,7 @@ __device__ unsigned long long npg_trace_buf[4][64];
 namespace {
 
 constexpr int NH = 32;                 // hidden width (both layers)
-constexpr int RC0 = 32;                // rows per chunk: 32, or 64 when the LDS image fits (f32 inputs)
+constexpr int RC0 = 32;                // rows per chunk (64-row chunks measured slower: DESIGN.md section 6)
 constexpr int NT = 512;                // threads per block: 8 waves, 2 per SIMD
 constexpr int NW = NT / 64;
 constexpr int MAXS = 256;              // max state dim
