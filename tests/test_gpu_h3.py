@@ -46,7 +46,9 @@ def row_err(p, ref):
 def test_f16x3_ensemble_matches_oracle_and_f32(S, A, hidden, B):
     """Tile paths: 8192 lanes -> 256x256 BK32 hidden tiles; 4096 / 5120 / 6144 / 7168 lanes ->
     the row-block tiles (RB x 256 hidden, RB x 112 / RB x 128 output, RB = 128 .. 224: one
-    256-workgroup wave); other grids -> 128x128; S=197 -> the 128x224 output tile, S=100 ->
+    256-workgroup wave); 640 lanes at H = 512, S = 197 -> stream-K over K for the hidden
+    (128 x 256) and output (128 x 224) tiles (few tiles: up to 6 workgroups per tile, combined in
+    K order); other grids -> 128x128; S=197 -> the 128x224 output tile, S=100 ->
     128, S=300 -> three 128 tiles; hidden 100 -> padded columns.  Same tolerance as the f32
     path (2e-5 of max(1, |ref|)) and within 1e-6 of it."""
     amx, ctx, ens, ens_w, norms, (s, a) = make(S, A, hidden)
