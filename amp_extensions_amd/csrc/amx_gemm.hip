@@ -779,22 +779,22 @@ __device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL
   }
   __syncthreads();
   if (!*flag) return false;
-  f32x4 mine[MB][NB];
+  // per block: v = P0, v += P1, ... (own segment from the accumulators) -- the segments' sum in
+  // K order without a second copy of the accumulators (which spilled the 128-accumulator tiles)
 #pragma unroll
   for (int m = 0; m < MB; ++m)
 #pragma unroll
-    for (int n = 0; n < NB; ++n) mine[m][n] = acc[m][n];
-  for (int s = 0; s < nseg; ++s) {
-#pragma unroll
-    for (int m = 0; m < MB; ++m)
-#pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const f32x4 v = s == seg ? mine[m][n]
+    for (int n = 0; n < NB; ++n) {
+      const f32x4 mine = acc[m][n];
+      f32x4 v = mine;
+      for (int s = 0; s < nseg; ++s) {
+        const f32x4 p = s == seg ? mine
                                  : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                                                  rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
-        acc[m][n] = s == 0 ? v : acc[m][n] + v;
+        v = s == 0 ? p : v + p;
       }
-  }
+      acc[m][n] = v;
+    }
   return true;
 }
 
@@ -1114,7 +1114,9 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       __builtin_amdgcn_sched_barrier(0);
       compute(cur * STAGE);
     }
-    if constexpr (TL::M16 && (EPI == EPI_UNNORM || EPI == EPI_BIAS_ACT)) {
+    // (the 256 x 256 hidden tile is launched one tile per workgroup only: no combine code, whose
+    // registers it cannot spare)
+    if constexpr (TL::M16 && (EPI == EPI_UNNORM || (EPI == EPI_BIAS_ACT && !(BM == 256 && TL::BN == 256)))) {
       if (nseg > 1) {
         __syncthreads();  // the stage buffers are free: one int of LDS for the last-arriver flag
         if (!split_combine<TL>(a, acc, tile, seg, nseg, reinterpret_cast<int*>(smem) + BM + 4)) return;
@@ -1508,6 +1510,9 @@ using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
 using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true, true>;  // + DEEPA (-2 %)
 
 
+// output layer, 256-row stream-K tiles (amx_set_out_tile 4): 8 waves of 64 x 112 on 16x16x32
+// (28 blocks); A + W fetched per FLOP 0.68x the 128 x 224 tile's
+using H256x224 = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 4, 7, true, true, true>;
 using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
 using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 
@@ -1899,10 +1904,10 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
 //    and ran the whole K = 2304 chain per tile (71 us at 640 lanes).  The last arriver reads
 //    SPLIT - 1 partial tiles, so SPLIT stays small.
 static int streamk_tiles(const amx_ctx* ctx, int groups, int rows, int* nwg = nullptr, int* ksplit = nullptr,
-                         int K = 0) {
+                         int K = 0, int bm = 128) {
   const int n32 = amx::round_up(ctx->S, 32);
-  if (n32 <= 128 || n32 > 224 || rows % 128 != 0) return 0;
-  const int tiles = rows / 128 * groups;
+  if (n32 <= 128 || n32 > 224 || rows % bm != 0) return 0;
+  const int tiles = rows / bm * groups;
   if (tiles < ctx->n_cus && 2 * tiles >= ctx->n_cus) {
     if (nwg) *nwg = ctx->n_cus;
     if (ksplit) *ksplit = 3;
@@ -1980,6 +1985,15 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
+    if (ctx->out_tile == 4) {  // 256 x 224 tiles, stream-K over the CUs
+      int nwg = 0, ksplit = 0;
+      const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K, 256);
+      if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
+          ctx->split_floats >= (long long)tiles * ksplit * 256 * 224) {
+        a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+        return launch_h3<EPI_UNNORM, H256x224>(a, s);
+      }
+    }
     // lane counts whose 128 x 224 tiles (14 waves) are fewer than the CUs (4096-7168 lanes x 4
     // members: 128-224 tiles): stream-K over one workgroup per CU (each tile's K range in <= 3
     // segments), instead of the row-block tiles' 4-7 waves per workgroup
@@ -2051,7 +2065,7 @@ extern "C" int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf) {
 
 extern "C" int amx_set_out_tile(amx_ctx* ctx, int tile) {
   AMX_CHECK_ARG(ctx, "amx_set_out_tile: null ctx");
-  AMX_CHECK_ARG(tile >= 0 && tile <= 3, "amx_set_out_tile: tile=%d not in 0..3", tile);
+  AMX_CHECK_ARG(tile >= 0 && tile <= 4, "amx_set_out_tile: tile=%d not in 0..4", tile);
   ctx->out_tile = tile;
   return AMX_OK;
 }
@@ -2076,7 +2090,14 @@ extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, 
                           ? streamk_hidden(ctx, groups, rows, ctx->H, ctx->k0_pad + (ctx->L - 1) * ctx->H, &nwg_h,
                                            &ksplit_h)
                           : 0;
-  if (n_counters) *n_counters = tiles > tiles_h ? tiles : tiles_h;
+  // the 256-row output tiles (amx_set_out_tile 4)
+  int nwg2 = 0, ksplit2 = 0;
+  const int tiles2 = streamk_tiles(ctx, groups, rows, &nwg2, &ksplit2, ctx->k0_pad + ctx->L * ctx->H, 256);
+  int nc = tiles > tiles_h ? tiles : tiles_h;
+  nc = nc > tiles2 ? nc : tiles2;
+  if (n_counters) *n_counters = nc;
   const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
-  return fo > fh ? fo : fh;
+  const long long f2 = (long long)tiles2 * ksplit2 * 256 * 224;
+  const long long f = fo > fh ? fo : fh;
+  return f > f2 ? f : f2;
 }

@@ -64,3 +64,30 @@ def test_ring_output_layer_matches_oracle(lanes):
     ref = R.ensemble_preds(w, norms, torch.from_numpy(ob[idx]).float(), torch.from_numpy(ac[idx]).float()).numpy()
     scale = np.maximum(1.0, np.abs(ref).max(axis=2, keepdims=True))
     assert np.max(np.abs(got[:, idx] - ref) / scale) < 2e-5
+
+
+@pytest.mark.parametrize("lanes", [8192, 7168, 5120, 4096, 1000])
+def test_out_tile4_streamk_256(lanes):
+    """amx_set_out_tile 4: 256 x 224 output tiles, K-tiles dealt over the CUs (stream-K, segments
+    summed in K order by the last arriver).  Its K segments differ from the one-tile-per-workgroup
+    staged tile's single chain, so it matches it (and the oracle) to fp32 rounding, not bit for
+    bit; repeated launches are bit-identical (deterministic combine, self-resetting counters)."""
+    S, A = 197, 36
+    ctx, ens, w, norms = _ensemble(S, A)
+    rs = np.random.RandomState(lanes + 3)
+    ob = 0.5 * rs.randn(lanes, S)
+    ac = rs.randn(lanes, A)
+    obt, act = torch.from_numpy(ob).to(DEV), torch.from_numpy(ac).to(DEV)
+    ctx.set_out_tile(1)
+    staged = ens.forward_preds(obt, act, lanes)[:, :lanes].clone()
+    ctx.set_out_tile(4)
+    got = ens.forward_preds(obt, act, lanes)[:, :lanes].clone()
+    again = ens.forward_preds(obt, act, lanes)[:, :lanes]
+    assert torch.equal(again, got), "256 x 224 stream-K is not deterministic"
+    scale = torch.clamp(staged.abs().amax(dim=2, keepdim=True), min=1.0)
+    assert ((got - staged).abs() / scale).max().item() < 2e-6
+    idx = np.arange(0, lanes, 61)
+    ref = R.ensemble_preds(w, norms, torch.from_numpy(ob[idx]).float(), torch.from_numpy(ac[idx]).float()).numpy()
+    g = got.cpu().numpy()[:, idx]
+    sc = np.maximum(1.0, np.abs(ref).max(axis=2, keepdims=True))
+    assert np.max(np.abs(g - ref) / sc) < 2e-5

@@ -1,7 +1,9 @@
 """Output-layer tile A/B (amx_set_out_tile): one f16x3 ensemble forward (assembly + 4 hidden
 layers + output layer) at B lanes with the register-staged tiles (1), the LDS-DMA ring with
-16-row waves (2) and with 32 x 112 waves (3); HIP-event medians over 30 forwards, rounds
-alternating in one process.  usage: python tools/out_ab.py [B ...]"""
+16-row waves (2), with 32 x 112 waves (3) and the 256 x 224 stream-K tile (4); HIP-event medians
+over 30 forwards, rounds alternating in one process.
+usage: [OUT_TILES=1,4] python tools/out_ab.py [B ...]"""
+import os
 import sys
 
 import numpy as np
@@ -38,10 +40,18 @@ for B in lanes:
     rs = np.random.RandomState(1)
     ob = torch.from_numpy(0.5 * rs.randn(B, S)).cuda()
     ac = torch.from_numpy(rs.randn(B, A)).cuda()
+    tiles = [int(x) for x in os.environ.get("OUT_TILES", "1,2,3,4").split(",")]
+    names = {1: "staged", 2: "ring16", 3: "ring32x112", 4: "256x224-streamK"}
     for rnd in range(3):
         res = {}
-        for tile in (1, 2, 3):
+        for tile in tiles:
             ctx.set_out_tile(tile)
             res[tile] = timed(ob, ac, B)
-        print(f"lanes {B} round {rnd}: forward staged {res[1]:.1f} us, ring16 {res[2]:.1f} us, ring32x112 "
-              f"{res[3]:.1f} us", flush=True)
+        print(f"lanes {B} round {rnd}: forward " + ", ".join(f"{names[t]} {res[t]:.1f} us" for t in tiles),
+              flush=True)
+    ctx.set_out_tile(1)
+    ref = ens.forward_preds(ob, ac, B).clone()
+    for tile in tiles:
+        ctx.set_out_tile(tile)
+        d = (ens.forward_preds(ob, ac, B) - ref)[:, :B].abs().max().item()
+        print(f"lanes {B}: tile {tile} max |diff| vs staged {d:.3e}", flush=True)
