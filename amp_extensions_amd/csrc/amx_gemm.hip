@@ -59,6 +59,10 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
   return __ballot(v);
 }
 
+// RFF_EXP (diagnostic builds, tools/gemm_variant.sh): 1 = no cos, 2 = no phi store
+#ifndef RFF_EXP
+#define RFF_EXP 0
+#endif
 template <int EPI, class TL>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], int g, int tm, int tn) {
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN;
@@ -143,8 +147,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
       const int r = part * PR + i;
       const int row = tm * BM + r;
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
+#if RFF_EXP == 1
+      const float phi = z * a.rff_scale;
+#else
       const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
+#endif
+#if RFF_EXP != 2
       Cg[(long long)row * a.ldc + col] = phi;
+#endif
       csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
     }
     __syncthreads();
