@@ -59,6 +59,10 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
   return __ballot(v);
 }
 
+// H3_EXP (diagnostic builds): 1 = the split schedule's K-loop global loads left out (stale tiles)
+#ifndef H3_EXP
+#define H3_EXP 0
+#endif
 // RFF_EXP (diagnostic builds, tools/gemm_variant.sh): 1 = no cos, 2 = no phi store
 #ifndef RFF_EXP
 #define RFF_EXP 0
@@ -946,13 +950,17 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
         split2(x, l0, l1);
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+#if H3_EXP != 1
         ra[SA][j] = *reinterpret_cast<const f32x4*>((kta < nks ? Ag0 : Ag) + a_src[j] + kta * BK);
+#endif
       }
     } else if (q < VA + VW) {
       const int j = q - VA;
       if (w_ok[j]) {
         *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+#if H3_EXP != 1
         rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
+#endif
       }
     }
   };
