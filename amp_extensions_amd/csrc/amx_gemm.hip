@@ -869,7 +869,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     a_dst[j] = r * LD + (c >> 2) * 32 + (c & 3) * 4;
     a_sh[j] = HSC - sExp[r];
   }
-  const uint16_t* w_src[VW];
+  int w_off_b[VW];  // byte offsets from the tile's first weight row
   int w_dst[VW];
   bool w_ok[VW];
 #pragma unroll
@@ -877,10 +877,24 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     const int q = t + NT * j;
     w_ok[j] = (TL::NW % NT == 0 || j + 1 < VW) ? true : q < TL::NW;
     const int r = w_ok[j] ? q / CPR : 0, p = q % CPR;
-    w_src[j] = Wg + (long long)r * ldw2 + p * 8;
+    w_off_b[j] = (int)(((long long)r * ldw2 + p * 8) * 2);
     w_dst[j] = BM * LD + r * LD + p * 8;
   }
 
+  // buffer loads: SGPR descriptors for the tile's A panel (group g and group 0) and W panel, a
+  // per-thread byte offset and the K-tile's byte offset in an SGPR -- no 64-bit address VALU in
+  // the K loop (and 4 VGPRs fewer than per-thread W pointers: the 256 x 256 tile's 44 B of
+  // scratch went with them)
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Ag), 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsA0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Ag0), 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(Wg), 0, 0x7ffffff0, 0x00020000);
+  auto gA = [&](int j, int kt) -> f32x4 {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(kt < nks ? rsA0 : rsA, a_src[j] * 4,
+                                                                          kt * BK * 4, 0));
+  };
+  auto gW = [&](int j, int kt) -> u32x4 {
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, w_off_b[j], kt * 2 * BK * 2, 0));
+  };
   f32x4 ra[TL::DEEPA ? 2 : 1][VA];  // A stage registers (DEEPA: the sets of tiles t+1 and t+2)
   u32x4 rw[VW];
   constexpr int MB = TL::MB, NB = TL::NB;  // 16x16 blocks of the M16 form
@@ -903,16 +917,15 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
   const int nk = a.K / BK;
   auto load_a = [&](auto set, int kt) {
     kt = kt < nk ? kt : nk - 1;  // past the end: re-read the last tile (branch-free)
-    const float* Ab = kt < nks ? Ag0 : Ag;
 #pragma unroll
     for (int j = 0; j < VA; ++j)
-      if (a_ok[j]) ra[decltype(set)::value][j] = *reinterpret_cast<const f32x4*>(Ab + a_src[j] + kt * BK);
+      if (a_ok[j]) ra[decltype(set)::value][j] = gA(j, kt);
   };
   auto load_w = [&](int kt) {
     kt = kt < nk ? kt : nk - 1;
 #pragma unroll
     for (int j = 0; j < VW; ++j)
-      if (w_ok[j]) rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
+      if (w_ok[j]) rw[j] = gW(j, kt);
   };
   auto load = [&](int kt) {
     load_a(std::integral_constant<int, 0>{}, kt);
@@ -957,7 +970,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
 #if !(H3_EXP & 1)
-        ra[SA][j] = *reinterpret_cast<const f32x4*>((kta < nks ? Ag0 : Ag) + a_src[j] + kta * BK);
+        ra[SA][j] = gA(j, kta);
 #endif
       }
     } else if (q < VA + VW) {
@@ -965,7 +978,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       if (w_ok[j]) {
         *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
 #if !(H3_EXP & 1)
-        rw[j] = *reinterpret_cast<const u32x4*>(w_src[j] + kt * 2 * BK);
+        rw[j] = gW(j, kt);
 #endif
       }
     }

@@ -157,7 +157,15 @@ struct TileH3 {
 // 4 consecutive k of one row, pre-scaled -> two f16 limbs packed as 4 f16 each
 __device__ __forceinline__ void split2(f32x4 x, u32x2& l0, u32x2& l1) {
   const f16x4 h0 = __builtin_convertvector(x, f16x4);
-  const f32x4 r1 = x - __builtin_convertvector(h0, f32x4);  // exact
+  const u32x2 hb = __builtin_bit_cast(u32x2, h0);
+  // r1 = x - h0, exact: one mixed-precision fma per element (h0's f16 half widened inside
+  // v_fma_mix_f32) instead of a widening convert and a subtract (hipcc folds an fmaf of a
+  // widened half back into the convert + subtract, hence the asm)
+  f32x4 r1;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r1[0]) : "v"(hb[0]), "v"(x[0]));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1[1]) : "v"(hb[0]), "v"(x[1]));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r1[2]) : "v"(hb[1]), "v"(x[2]));
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r1[3]) : "v"(hb[1]), "v"(x[3]));
   const f16x4 h1 = __builtin_convertvector(r1, f16x4);
   l0 = __builtin_bit_cast(u32x2, h0);
   l1 = __builtin_bit_cast(u32x2, h1);
