@@ -44,8 +44,10 @@ __global__ __launch_bounds__(1024) void k_sum_partials(const double* __restrict_
   const int per = (n_parts + 15) / 16;
   const int p0 = w * per, p1 = min(n_parts, p0 + per);
   double s = 0.0;
-  if (f < F)
-    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];
+  if (f < F) {
+#pragma unroll 8
+    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];  // 8 loads in flight, same add order
+  }
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && f < F) {
@@ -354,8 +356,10 @@ __global__ __launch_bounds__(1024) void k_feature_message(const double* __restri
   const int per = (n_parts + 15) / 16;
   const int p0 = w * per, p1 = min(n_parts, p0 + per);
   double s = 0.0;
-  if (f < F)
-    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];
+  if (f < F) {
+#pragma unroll 8
+    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];  // 8 loads in flight, same add order
+  }
   red[w][lane] = s;
   __syncthreads();
   if (w == 0 && f < F) {

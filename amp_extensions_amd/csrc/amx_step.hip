@@ -195,6 +195,12 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int b, int lane, fl
   const amx_termination& T = a.term;
   const int S = a.S;
   const int k = a.model_idx[b];
+  // the lane's counters (and the caller's reset row) are loaded with the row, not after the
+  // row's stores the compiler cannot move them above (round 3: within noise at 8192 / 5120
+  // lanes, profiles/r03e_step_ab.txt -- the later loads were already overlapped by other waves)
+  const int ns0 = a.num_steps[b];
+  const int rc0 = a.ob_out ? a.reset_count[b] : 0;
+  const int row0 = (a.ob_out && a.rows) ? a.rows[b] : 0;
   const double* ob = a.ob + (long long)b * S;
   double* on = a.ob_next + (long long)b * S;
 
@@ -325,7 +331,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int b, int lane, fl
     if (a.disc) d = disagreement_dispatch(a.M, a.preds, a.strideP, a.ldp, b, S, lane);
   }
 
-  const int ns = a.num_steps[b] + 1;  // sim_env.py:153 (every lane: a broadcast load)
+  const int ns = ns0 + 1;  // sim_env.py:153
   const bool horizon_done = ns >= T.horizon;  // :170
   const bool dn = horizon_done || collided || vexp;  // wave-uniform
   bool reset = false;
@@ -343,10 +349,10 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int b, int lane, fl
       if (lane == 0 && a.row_out) a.row_out[b] = -1;
     } else {
       reset = true;
-      const int rc = a.reset_count[b] + 1;  // sim_env.py:282
+      const int rc = rc0 + 1;  // sim_env.py:282
       int row;
       if (a.rows) {
-        row = a.rows[b];
+        row = row0;
       } else {
         const amx::u32x4 r = amx::philox4x32_10({(uint32_t)b, (uint32_t)rc, 0u, amx::kTagReset}, a.k0, a.k1);
         row = (int)((((uint64_t)r.y << 32) | r.x) % (uint64_t)a.R);
