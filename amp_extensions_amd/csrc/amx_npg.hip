@@ -732,13 +732,15 @@ __global__ void k_npg_reduce1(const double* __restrict__ part, int nb, int P, do
   if (c >= P) return;
   const int b0 = blockIdx.y * RB, b1 = min(nb, b0 + RB);
   double s = 0.0;
-  for (int b = b0; b < b1; ++b) s += part[(long long)b * P + c];
+#pragma unroll 8
+  for (int b = b0; b < b1; ++b) s += part[(long long)b * P + c];  // 8 loads in flight, same add order
   mid[(long long)blockIdx.y * P + c] = s;
 }
 __global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, double* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= P) return;
   double s = 0.0;
+#pragma unroll 8
   for (int r = 0; r < nr; ++r) s += mid[(long long)r * P + c];
   out[c] = s;
 }
