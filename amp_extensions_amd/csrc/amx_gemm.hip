@@ -794,22 +794,21 @@ __device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL
   }
   __syncthreads();
   if (!*flag) return false;
-  // per block: v = P0, v += P1, ... (own segment from the accumulators) -- the segments' sum in
-  // K order without a second copy of the accumulators (which spilled the 128-accumulator tiles)
+  // acc = P0, acc += P1, ... in K order, this segment's own slot read back like the others (the
+  // same bits it stored), so the sum runs in place in the accumulators (a second copy spilled
+  // the 128-accumulator tiles) and one segment's loads for all MB x NB blocks are in flight
+  // together: nseg memory round trips, not one per block and segment
+  (void)seg;
+  for (int s = 0; s < nseg; ++s) {
 #pragma unroll
-  for (int m = 0; m < MB; ++m)
+    for (int m = 0; m < MB; ++m)
 #pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      const f32x4 mine = acc[m][n];
-      f32x4 v = mine;
-      for (int s = 0; s < nseg; ++s) {
-        const f32x4 p = s == seg ? mine
-                                 : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                                 rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
-        v = s == 0 ? p : v + p;
+      for (int n = 0; n < NB; ++n) {
+        const f32x4 p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
+        acc[m][n] = s == 0 ? p : acc[m][n] + p;
       }
-      acc[m][n] = v;
-    }
+  }
   return true;
 }
 

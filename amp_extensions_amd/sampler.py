@@ -104,18 +104,72 @@ class _Store:
         return base
 
 
-def _sampler_engine(env, lanes: int, K: int, policy) -> RolloutEngine:
-    """A lanes-sized engine on the env's ensemble, reset source and termination (cached)."""
+def _reset_time_max(env) -> float:
+    """The reset-time window [0, time_max) every trajectory's env.reset() draws from
+    (sim_env.py:76-77, 276): reset_args['time_max'] when custom_time is on, else the clip length
+    (a reset table: its length in rows).  A BatchedSimEnv keeps its reset_args; a RolloutEngine
+    its reset_time_max (0: the whole source)."""
+    src = env.engine if isinstance(env, BatchedSimEnv) else env
+    ra = getattr(env, "reset_args", None)
+    if ra is not None and ra.get("custom_time"):
+        return float(ra["time_max"])
+    if float(getattr(src, "reset_time_max", 0.0) or 0.0) > 0.0:
+        return float(src.reset_time_max)
+    return src.motion.get_motion_length() if src.motion is not None else float(src.table.shape[0])
+
+
+def _sampler_engine(env, lanes: int, K: int, policy, time_max: float) -> RolloutEngine:
+    """A lanes-sized engine on the env's ensemble, reset source and termination (cached per
+    lane count, chunk and reset window); its device-drawn motion resets use the env's window."""
     src = env.engine if isinstance(env, BatchedSimEnv) else env
     cache = src.__dict__.setdefault("_sampler_engines", {})
-    eng = cache.get((lanes, K))
+    key = (lanes, K, float(time_max))
+    eng = cache.get(key)
     if eng is None:
         reset_source = src.motion if src.motion is not None else src.table
         eng = RolloutEngine(src.ens, reset_source, lanes=lanes, term=src.term, policy=policy, seed=src.seed,
                             max_steps=K, auto_reset=False, record_means=True)
-        cache[(lanes, K)] = eng
+        # (0 = the whole clip; a table source is already cut to the window's rows)
+        if src.motion is not None and time_max != src.motion.get_motion_length():
+            eng.reset_time_max = float(time_max)
+        cache[key] = eng
     eng.policy = policy
     return eng
+
+
+def _mjrl_fingerprint(policy) -> tuple:
+    """Identity + in-place version of every trainable tensor of an mjrl MLP: set_param_values
+    rebinds param.data (gaussian_mlp.py:67-85), an optimizer step bumps the tensor version."""
+    ts = [p.data for p in policy.model.parameters()] + [policy.log_std.data]
+    return tuple((t.data_ptr(), t._version) for t in ts) + (np.asarray(policy.log_std_val).tobytes(),)
+
+
+def device_policy(env, policy):
+    """`policy` as the sampler's DevicePolicy.  A DevicePolicy passes through; the reference's
+    mjrl `MLP` (gaussian_mlp.py:7-104: `model.fc_layers`, `log_std`, `log_std_val`) is wrapped
+    once (DevicePolicy.from_mjrl, cached on the object) and re-synced whenever its parameters
+    changed since the last call, so batch_reinforce.py:88-90 passes its own policy unchanged."""
+    from .policy import DevicePolicy
+    if isinstance(policy, DevicePolicy):
+        return policy
+    model = getattr(policy, "model", None)
+    if model is None or not hasattr(model, "fc_layers") or not hasattr(policy, "log_std"):
+        raise TypeError(f"sample_points: policy must be a DevicePolicy or an mjrl MLP, got {type(policy).__name__}")
+    if float(getattr(policy, "eps", 0.0) or 0.0) != 0.0:
+        raise NotImplementedError("sample_points: mjrl MLP with eps > 0 (uniform random actions) is not supported")
+    src = env.engine if isinstance(env, BatchedSimEnv) else env
+    ctx = src.ctx
+    fp = _mjrl_fingerprint(policy)
+    cached = policy.__dict__.get("_amx_device_policy")
+    if cached is None or cached[0] is not ctx:
+        dp = DevicePolicy.from_mjrl(ctx, policy)
+        policy.__dict__["_amx_device_policy"] = (ctx, dp, fp)
+        return dp
+    _, dp, old = cached
+    if old != fp:
+        dp.sync_from([(l.weight.data, l.bias.data) for l in policy.model.fc_layers], policy.log_std.data)
+        policy.__dict__["_amx_device_policy"] = (ctx, dp, fp)
+    return dp
 
 
 class _HostNoise:
@@ -135,7 +189,10 @@ class _HostNoise:
 
     def seed(self, lanes: np.ndarray, seeds: np.ndarray) -> None:
         sl = np.ascontiguousarray(lanes, np.int32)
-        sd = np.ascontiguousarray(np.asarray(seeds, np.int64) & 0xFFFFFFFF, np.uint32)
+        sd = np.asarray(seeds, np.int64)
+        if sd.size and (sd.min() < 0 or sd.max() >= 2 ** 32):  # np.random.seed's own range check
+            raise ValueError(f"Seed must be between 0 and 2**32 - 1 (sample_points trajectory seeds {sd.min()}..{sd.max()})")
+        sd = np.ascontiguousarray(sd, np.uint32)
         N.check(self.lib.amx_mt_seed(self.states.ctypes.data, self.L, sl.ctypes.data, sd.ctypes.data, sl.size),
                 "amx_mt_seed")
 
@@ -187,7 +244,7 @@ class _ChunkGraph:
 
 
 def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, rng: str, eval_mode: bool,
-             speculate: bool = True, graph: bool = True):
+             time_max: float, speculate: bool = True, graph: bool = True):
     """Run the W workers' trajectory sequences on the engine's lanes (see the module notes).
 
     Admission: a worker's trajectories are admitted in seed order j.  Trajectory j is needed iff
@@ -205,7 +262,6 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     L, S, A, K, dev = eng.B, c.S, c.A, eng.K, c.device
     R = eng.term.horizon
     motion = eng.motion
-    time_max = motion.get_motion_length() if motion is not None else float(eng.table.shape[0])
     adm: list[list[_Traj]] = [[] for _ in range(W)]   # admitted trajectories, in j order
     next_j = [1] * W
     done_w = [False] * W
@@ -387,7 +443,7 @@ class _ChunkRing:
 
 
 def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, rng: str,
-                       eval_mode: bool, speculate: bool = True, graph: bool = True):
+                       eval_mode: bool, time_max: float, speculate: bool = True, graph: bool = True):
     """_collect with the host one chunk behind the GPU: chunk i is queued (resets, noise, the
     captured steps, a raw copy of its transitions and an async copy of its done flags) before
     chunk i-1's done flags are read and its trajectories advanced.  Admission therefore sees
@@ -399,7 +455,6 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
     L, S, A, K, dev = eng.B, c.S, c.A, eng.K, c.device
     R = eng.term.horizon
     motion = eng.motion
-    time_max = motion.get_motion_length() if motion is not None else float(eng.table.shape[0])
     adm: list[list[_Traj]] = [[] for _ in range(W)]
     next_j = [1] * W
     done_w = [False] * W
@@ -583,8 +638,9 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
                   eval_mode: bool = False, verbose: bool = False, deepmimic: bool = False, rng: str = "reference",
                   chunk: int = 16, speculate: bool = True, graph: bool = True, pipeline: bool = True):
     """milo.sampler.sample_points on the GPU.  `env` is a BatchedSimEnv (or a RolloutEngine):
-    its ensemble, reset source and termination are used, and its lane count caps the
-    concurrency; `policy` a DevicePolicy.  Returns the reference's list of path dicts
+    its ensemble, reset source, reset-time window (reset_args custom_time / time_max) and
+    termination are used, and its lane count caps the concurrency; `policy` a DevicePolicy or
+    the reference's mjrl MLP (wrapped and kept in sync by device_policy).  Returns the reference's list of path dicts
     (observations / next_observations / actions float64, rewards 0, agent_infos {mean,
     log_std, evaluation}, env_infos, terminated).  A missing info['valid'] counts as valid
     (SimEnv returns {}; the reference's deepmimic=True branch, sampler.py:61, would raise).
@@ -604,12 +660,15 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
         need *= 4  # room for trajectories shorter than the horizon (lengths ~R/4) to run at once
     lanes = max(1, min(need, src.B))
     K = max(1, min(int(chunk), R))
-    eng = _sampler_engine(env, lanes, K, policy)
+    time_max = _reset_time_max(env)
+    policy = device_policy(env, policy)
+    eng = _sampler_engine(env, lanes, K, policy, time_max)
     if rng == "device":
         policy.seed = (12345 + int(base_seed)) & 0xFFFFFFFFFFFFFFFF
     t0 = time.time()
     collect = _collect_pipelined if pipeline else _collect
-    paths, n = (collect(eng, W, quota, mode, int(base_seed), rng, eval_mode, speculate=speculate, graph=graph)
+    paths, n = (collect(eng, W, quota, mode, int(base_seed), rng, eval_mode, time_max, speculate=speculate,
+                        graph=graph)
                 if quota > 0 else ([], 0))
     if verbose:
         print(f"Collected {n} and {len(paths)} trajectories in {time.time() - t0} seconds")

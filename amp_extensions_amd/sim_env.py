@@ -275,6 +275,8 @@ class BatchedSimEnv:
             reset_table = motion_from_args(dev_ens.ctx, deepmimic_args, resolve=bool(self.reset_args["resolve"]))
         custom = self.reset_args["custom_time"]
         from .motion import ReferenceMotion
+        if isinstance(reset_table, ReferenceMotion) and not self.reset_args["resolve"] and reset_table.resolve:
+            raise ValueError("reset_args['resolve'] is False but the ReferenceMotion resolves ground intersections")
         if custom and not isinstance(reset_table, ReferenceMotion):
             rows = int(np.ceil(float(self.reset_args["time_max"])))
             n = int(torch.as_tensor(reset_table).shape[0])

@@ -86,8 +86,9 @@ def parse():
     p.add_argument("--cpu-samples", type=int, default=0,
                    help="env-steps per worker at each sweep point (default: sized for --cpu-point-s)")
     p.add_argument("--cpu-point-s", type=float, default=3.0, help="seconds of sampling per sweep point")
-    p.add_argument("--cpu-final-samples", type=int, default=200000,
-                   help="env-steps of the timed best-W run (five 40 000-sample rollouts: 10-30 s of CPU work)")
+    p.add_argument("--cpu-final-samples", type=int, default=120000,
+                   help="env-steps of each of the three timed best-W runs (three 40 000-sample rollouts: ~8-12 s "
+                        "of CPU work per run on a 16-core share)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the whole rollout as captured HIP graph(s); auto: when a rank's rollout is "
@@ -147,8 +148,9 @@ def cpu_baseline_leg(S, A, args):
     sweep point (W = powers of two up to the CPU share this process has, plus the share
     itself) runs about --cpu-point-s seconds of sampling; the best W is then timed end to end
     (sampler + relabel, the relabel on the whole CPU share as the reference's one-process torch
-    relabel would use it) on --cpu-final-samples env-steps, twice: the value is the faster of
-    the two and both are reported.  Runs before anything touches the GPU (the pools fork)."""
+    relabel would use it) on --cpu-final-samples env-steps, three times, the relabel on the same
+    fixed sample each time: the value is the median run and all three are reported.  Runs before
+    anything touches the GPU (the pools fork)."""
     from oracle import cpu_baseline as cb
     share = cpu_share()
     if args.cpu_workers:
@@ -163,9 +165,17 @@ def cpu_baseline_leg(S, A, args):
         r = cb.run(S, A, workers=w, samples=n, expert_rows=args.expert_rows, relabel=False)
         sweep.append((w, r))
     best_w, best = max(sweep, key=lambda x: x[1]["sampler_steps_per_s"])
-    finals = [cb.run(S, A, workers=best_w, samples=max(best["samples"], args.cpu_final_samples),
-                     expert_rows=args.expert_rows, relabel=True, relabel_threads=share) for _ in range(2)]
-    best = max(finals, key=lambda r: r["end_to_end_steps_per_s"])
+    # three end-to-end runs at the best W; every run's sampler draws the same seeded trajectories,
+    # and the relabel leg is timed three times on the SAME fixed sample (the first run's paths),
+    # so the runs differ only by the host's timing noise; the value is the median run
+    n_final = max(best["samples"], args.cpu_final_samples)
+    samp = [cb.run(S, A, workers=best_w, samples=n_final, expert_rows=args.expert_rows, relabel=False,
+                   keep_paths=(i == 0)) for i in range(3)]
+    paths = samp[0].pop("_paths")
+    rel = [cb.relabel_seconds(paths, S, A, expert_rows=args.expert_rows, threads=share) for _ in range(3)]
+    finals = [dict(r, relabel_s=t, relabel_threads=share, end_to_end_steps_per_s=r["samples"] / (r["sampler_s"] + t))
+              for r, t in zip(samp, rel)]
+    best = sorted(finals, key=lambda r: r["end_to_end_steps_per_s"])[1]
     cpu = platform.processor() or platform.machine()
     try:
         with open("/proc/cpuinfo") as f:
@@ -184,13 +194,45 @@ def cpu_baseline_leg(S, A, args):
                    f"forked sampler workers (torch threads 1) + host relabel (fit_cost + per-path bonus costs, "
                    f"{args.expert_rows}-row expert buffer, {best['relabel_threads']} torch threads); sampler alone "
                    f"{best['sampler_steps_per_s']:.0f} env-steps/s; sampler {best['sampler_s']:.2f}s + relabel "
-                   f"{best['relabel_s']:.2f}s; best of 2 end-to-end runs"),
+                   f"{best['relabel_s']:.2f}s; median of 3 end-to-end runs (the relabel timed on the same "
+                   f"fixed sample each time)"),
         "end_to_end_runs": e2e,
         "spread": round((max(e2e) - min(e2e)) / max(e2e), 4),
         "sweep_sampler_steps_per_s": pts,
         "best_workers": best_w, "relabel_threads": best["relabel_threads"],
         "cpu_share": share, "os_cpu_count": os.cpu_count(), "cpu_model": cpu,
     }
+
+
+def gemm_source_sha16() -> str:
+    """Hash of the GEMM kernel sources (csrc/amx_gemm.hip + amx_h3.h): the key that ties a PMC
+    traffic record to the build it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in ("amx_gemm.hip", "amx_h3.h"):
+        with open(os.path.join(ROOT, "amp_extensions_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def gemm_traffic(gemm: str, S: int, B: int):
+    """(HBM bytes per ensemble-GEMM launch, note) from the PMC record that ships with the package
+    (amp_extensions_amd/data/gemm_traffic_<gemm>.json, written by tools/pmc_traffic.sh: FETCH_SIZE
+    x 2 + WRITE_SIZE in separate rocprofv3 passes, MI355X_MICROARCH.md's gfx950 correction).  Only
+    a record of THIS build's GEMM sources at this shape counts; otherwise traffic is null."""
+    path = os.path.join(ROOT, "amp_extensions_amd", "data", f"gemm_traffic_{gemm}.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, f"no PMC record ({os.path.relpath(path, ROOT)})"
+    if tj.get("state_dim") != S or tj.get("lanes") != B or tj.get("gemm", "f32") != gemm:
+        return None, f"PMC record is for S={tj.get('state_dim')} lanes={tj.get('lanes')} gemm={tj.get('gemm')}"
+    if tj.get("gemm_source_sha16") != gemm_source_sha16():
+        return None, "PMC record is from another build of the GEMM sources"
+    return tj.get("hbm_bytes_per_launch"), (
+        f"rocprofv3 PMC, (2*FETCH_SIZE + WRITE_SIZE) per launch averaged over the forward's layers; "
+        f"{tj.get('ratio')}x the algorithmic {tj.get('alg_bytes_per_launch')} B; build {tj.get('gemm_source_sha16')}")
 
 
 def plan_lanes(samples: int, max_lanes: int, lanes: int = 0):
@@ -510,16 +552,7 @@ def main():
     else:
         step_flops = ens.mlp_flops_per_sample() + 2 * (cost.input_dim * 1024 + 1024 * 512 + 512)
     value = total_samples / elapsed
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"gemm_traffic_{args.gemm}.json")
-    if os.path.exists(pmc_path):
-        try:
-            with open(pmc_path) as f:
-                tj = json.load(f)
-            if tj.get("state_dim") == S and tj.get("lanes") == B and tj.get("gemm", "f32") == args.gemm:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_note = gemm_traffic(args.gemm, S, B)
 
     gi = GEMM_INFO[args.gemm]
     peak = gi["peak"]
@@ -574,7 +607,7 @@ def main():
             "roofline": {
                 "bound": "mfma", "achieved": round(achieved_tflops, 2), "peak": round(peak, 1),
                 "unit": gi["unit"],
-                "frac": round(achieved_tflops / peak, 4), "traffic": traffic,
+                "frac": round(achieved_tflops / peak, 4), "traffic": traffic, "traffic_note": traffic_note,
                 "frac_vs_f32_mfma": round(achieved_tflops / F32_MFMA_PEAK_TFLOPS, 4),
                 "peak_note": gi["peak_note"],
                 "kernel": gi["kernel"],

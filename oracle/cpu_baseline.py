@@ -35,7 +35,8 @@ def _work(i):
 
 def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers: int | None = None,
         samples: int = 20000, horizon: int = 300, expert_rows: int = 50000, feature_dim: int = 512,
-        lambda_b: float = 0.0025, seed: int = 100, relabel: bool = True, relabel_threads: int | None = None) -> dict:
+        lambda_b: float = 0.0025, seed: int = 100, relabel: bool = True, relabel_threads: int | None = None,
+        keep_paths: bool = False) -> dict:
     """Returns env-steps/s of the CPU sampler alone and (relabel=True) of sampler + relabel.
     The relabel runs in this process with `relabel_threads` torch threads (default: the
     worker count); the reference's relabel is one process with torch's default threading."""
@@ -57,11 +58,27 @@ def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers:
         t1 = time.perf_counter()
     paths = [p for r in results for p in r]
     n = sum(len(p["rewards"]) for p in paths)
+    out = dict(samples=n, paths=len(paths), workers=workers, sampler_s=t1 - t0, sampler_steps_per_s=n / (t1 - t0))
+    if keep_paths:
+        out["_paths"] = paths
     if not relabel:
-        return dict(samples=n, paths=len(paths), workers=workers, sampler_s=t1 - t0, sampler_steps_per_s=n / (t1 - t0))
-    # host relabel with the reference's batching (thread count restored for the relabel)
+        return out
     threads = relabel_threads or workers
+    rel = relabel_seconds(paths, S, A, hidden, n_models, expert_rows, feature_dim, lambda_b, seed, threads)
+    out.update(relabel_threads=threads, relabel_s=rel, end_to_end_steps_per_s=n / ((t1 - t0) + rel))
+    return out
+
+
+def relabel_seconds(paths, S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, expert_rows: int = 50000,
+                    feature_dim: int = 512, lambda_b: float = 0.0025, seed: int = 100, threads: int = 1) -> float:
+    """Seconds of the host relabel (batch_reinforce.py:103-169: fit_cost over all samples, then
+    per-path get_bonus_costs with the 4-model disagreement) over `paths`, with the reference's
+    batching on `threads` torch threads.  The cost / ensemble setup is outside the timing."""
+    from amp_extensions_amd import synthetic as syn
     torch.set_num_threads(threads)
+    s, a, s2 = syn.offline(20000, S, A, 0)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s2)])
+    ens = R.init_ensemble_weights(S, A, list(hidden), n_models, seed)
     expert = torch.from_numpy(syn.expert(expert_rows, S, 3))
     cost = R.RBFLinearCostRef(expert, feature_dim=feature_dim, bw_quantile=0.1, lambda_b=lambda_b, seed=seed)
     thr = R.compute_threshold(ens, norms, torch.from_numpy(s).float()[:4096], torch.from_numpy(a).float()[:4096])
@@ -70,6 +87,4 @@ def run(S: int, A: int, hidden=(512, 512, 512, 512), n_models: int = 4, workers:
     R.relabel_mmd(paths, cost, disc_fn, thr)
     t3 = time.perf_counter()
     torch.set_num_threads(1)
-    return dict(samples=n, paths=len(paths), workers=workers, relabel_threads=threads, sampler_s=t1 - t0,
-                relabel_s=t3 - t2,
-                sampler_steps_per_s=n / (t1 - t0), end_to_end_steps_per_s=n / ((t1 - t0) + (t3 - t2)))
+    return t3 - t2

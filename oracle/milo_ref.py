@@ -547,18 +547,18 @@ def gym_np_random(seed: int) -> np.random.Generator:
 
 
 def get_samples(env: SimEnvRef, pweights, log_std, num_to_collect: int, seed: int, reset_table: np.ndarray,
-                mode="samples", eval_mode=False):
-    """get_samples (sampler.py:8-84) with env.reset's motion time t = np_random.uniform(0, R)
-    (sim_env.py:276, time_max = R) selecting row floor(t) of the reset table in place of the
-    DeepMimicCore pose.  A missing
-    info['valid'] is treated as valid (SimEnv returns {})."""
+                mode="samples", eval_mode=False, time_max=None):
+    """get_samples (sampler.py:8-84) with env.reset's motion time t = np_random.uniform(0, time_max)
+    (sim_env.py:276; time_max = the table's R rows, or reset_args['time_max'] with custom_time,
+    sim_env.py:76-77) selecting row floor(t) of the reset table in place of the DeepMimicCore
+    pose.  A missing info['valid'] is treated as valid (SimEnv returns {})."""
     paths, samples, ctr_seed = [], 0, 0
     cond = (lambda: len(paths) < num_to_collect) if mode == "trajectories" else (lambda: samples < num_to_collect)
     while cond():
         ctr_seed += 1
         rng = gym_np_random(seed + ctr_seed)             # env.seed_env(seed + ctr), sim_env.py:132
         np.random.seed(seed + ctr_seed)                   # sampler.py:39
-        row = int(rng.uniform(low=0, high=reset_table.shape[0]))
+        row = int(rng.uniform(low=0, high=reset_table.shape[0] if time_max is None else time_max))
         o = env.reset(reset_table[row])
         obs, nobs, acts, rews, ainfos, einfos = [], [], [], [], [], []
         done = False

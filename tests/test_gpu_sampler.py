@@ -168,3 +168,100 @@ def test_sample_points_pipelined_bit_identical(setup):
             for k in ("observations", "next_observations", "actions"):
                 np.testing.assert_array_equal(pa[k], pb[k])
             np.testing.assert_array_equal(pa["agent_infos"]["mean"], pb["agent_infos"]["mean"])
+
+
+def test_sample_points_custom_time_window_table(setup):
+    """reset_args custom_time / time_max (sim_env.py:76-77, 276): every trajectory's reset draws
+    t ~ U(0, time_max), not U(0, table rows) -- with time_max 2.5 the rows are floor(t) in
+    {0, 1, 2}, row 2 half as likely.  The paths equal the oracle's get_samples over the same
+    window (the window was ignored)."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    from amp_extensions_amd.synthetic import reset_table
+    table = reset_table(64, S, 4)
+    ra = dict(custom_time=True, time_min=0, time_max=2.5)
+    env = amx.BatchedSimEnv(ens, table, lanes=128, horizon=12, record_means=True, reset_args=ra)
+    W, N = 2, 150
+    paths = amx.sample_points(env, pol, num_to_collect=N, base_seed=5, num_workers=W)
+    ref = []
+    for i in range(W):
+        envr = R.SimEnvRef(ens_w, norms, horizon=12)
+        p, _ = R.get_samples(envr, pw, log_std, math.ceil(N / W), 12345 + 5 * i, table, time_max=2.5)
+        ref.extend(p)
+    _compare_paths(paths, ref)
+    firsts = np.stack([p["observations"][0] for p in paths])
+    rows = [int(np.flatnonzero((table == f).all(1))[0]) for f in firsts]
+    assert set(rows) <= {0, 1, 2} and 2 in rows
+
+
+class _MjrlFC(torch.nn.Module):
+    """mjrl FCNetwork's attribute layout (mjrl/utils/fc_network.py: fc_layers)."""
+
+    def __init__(self, layers):
+        super().__init__()
+        self.fc_layers = torch.nn.ModuleList(layers)
+
+
+class _MjrlMLP:
+    """The attribute layout of mjrl's MLP policy (gaussian_mlp.py:7-85): model.fc_layers,
+    log_std, log_std_val, eps, trainable_params, set_param_values rebinding param.data."""
+
+    def __init__(self, pw, log_std):
+        layers = []
+        for W, b in pw:
+            lin = torch.nn.Linear(W.shape[1], W.shape[0])
+            lin.weight.data = W.clone().float()
+            lin.bias.data = b.clone().float()
+            layers.append(lin)
+        self.model = _MjrlFC(layers)
+        self.log_std = torch.autograd.Variable(log_std.clone().float(), requires_grad=True)
+        self.trainable_params = list(self.model.parameters()) + [self.log_std]
+        self.log_std_val = np.float64(self.log_std.data.numpy().ravel())
+        self.eps = 0.0
+
+    def get_param_values(self):
+        return np.concatenate([p.contiguous().view(-1).data.numpy() for p in self.trainable_params]).copy()
+
+    def set_param_values(self, new_params):
+        i = 0
+        for p in self.trainable_params:
+            n = p.data.numel()
+            p.data = torch.from_numpy(new_params[i:i + n].reshape(p.data.shape)).float()
+            i += n
+        self.log_std_val = np.float64(self.log_std.data.numpy().ravel())
+
+
+def test_sample_points_takes_mjrl_policy(setup):
+    """batch_reinforce.py:88-90 passes its mjrl MLP straight to sample_points: the drop-in wraps
+    it once (DevicePolicy.from_mjrl) and reproduces the DevicePolicy run bit for bit; after
+    set_param_values (the NPG step, npg_cg.py:186) the next call re-syncs and matches a fresh
+    DevicePolicy of the new parameters bit for bit."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    from amp_extensions_amd.synthetic import reset_table
+    table = reset_table(256, S, 1)
+    env = amx.BatchedSimEnv(ens, table, lanes=128, horizon=20, record_means=True)
+    mj = _MjrlMLP(pw, log_std)
+    for rng in ("reference", "device"):
+        # rng='device' draws Philox noise at the engine's running step counter, so its two runs
+        # start from two fresh envs (same counter); 'reference' is exact-seeded per trajectory
+        env_a = env if rng == "reference" else amx.BatchedSimEnv(ens, table, lanes=128, horizon=20, record_means=True)
+        env_b = env if rng == "reference" else amx.BatchedSimEnv(ens, table, lanes=128, horizon=20, record_means=True)
+        a = amx.sample_points(env_a, pol, num_to_collect=200, base_seed=9, num_workers=2, rng=rng)
+        b = amx.sample_points(env_b, mj, num_to_collect=200, base_seed=9, num_workers=2, rng=rng)
+        assert len(a) == len(b)
+        for pa, pb in zip(a, b):
+            for k in ("observations", "next_observations", "actions"):
+                np.testing.assert_array_equal(pa[k], pb[k])
+    dp = mj.__dict__["_amx_device_policy"][1]
+    new = mj.get_param_values() * 1.01
+    mj.set_param_values(new)
+    b = amx.sample_points(env, mj, num_to_collect=200, base_seed=9, num_workers=2)
+    assert mj.__dict__["_amx_device_policy"][1] is dp  # re-synced in place, not rebuilt
+    layers = [(l.weight.data, l.bias.data) for l in mj.model.fc_layers]
+    fresh = amx.DevicePolicy(ens.device.ctx, layers, mj.log_std.data)
+    a = amx.sample_points(env, fresh, num_to_collect=200, base_seed=9, num_workers=2)
+    assert len(a) == len(b)
+    for pa, pb in zip(a, b):
+        np.testing.assert_array_equal(pa["actions"], pb["actions"])
+        np.testing.assert_array_equal(pa["agent_infos"]["log_std"], pb["agent_infos"]["log_std"])
+    with pytest.raises(ValueError):
+        amx.sample_points(env, pol, num_to_collect=10, base_seed=2 ** 32, num_workers=1)

@@ -157,3 +157,33 @@ def test_batched_simenv_custom_time_from_args(setup):
     got = e.obs[1].cpu().numpy()
     for b in range(0, 256, 37):
         assert _rel(got[b], DR.reset_state(J, bodies, M, float(t[b]))) <= 1e-10
+
+
+def test_sample_points_custom_time_motion(setup):
+    """sample_points on a BatchedSimEnv built from the arg file with custom_time / time_max:
+    every trajectory j of worker i starts from reset_state(t), t = np_random(12345 +
+    base_seed * i + j).uniform(0, time_max) (sim_env.py:132, 276) -- the env's window, not the
+    clip length -- and with rng='device' every start time stays below time_max."""
+    amx, ens, ens_w, norms, args, J, bodies, M = setup
+    ra = dict(RUN_PY_RESET_ARGS, custom_time=True, time_max=0.35)
+    benv = amx.BatchedSimEnv(ens, None, lanes=64, deepmimic_args=args, reset_args=ra, seed=3, horizon=6,
+                             record_means=True)
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    pol = amx.DevicePolicy(ens.ctx, pw, log_std)
+    W, N, base = 2, 40, 4
+    paths = amx.sample_points(benv, pol, num_to_collect=N, base_seed=base, num_workers=W)
+    q = int(np.ceil(N / W))
+    k = 0
+    for i in range(W):
+        tot, j = 0, 0
+        while tot < q:
+            j += 1
+            t = R.gym_np_random(12345 + base * i + j).uniform(low=0, high=0.35)
+            assert _rel(paths[k]["observations"][0], DR.reset_state(J, bodies, M, t)) <= 1e-10, (i, j)
+            tot += len(paths[k]["rewards"])
+            k += 1
+    assert k == len(paths)
+    dev_paths = amx.sample_points(benv, pol, num_to_collect=N, base_seed=base, num_workers=W, rng="device")
+    eng = next(iter(benv.engine.__dict__["_sampler_engines"].values()))
+    assert eng.reset_time_max == pytest.approx(0.35)
+    assert len(dev_paths) > 0

@@ -1,4 +1,5 @@
-"""HBM traffic of the ensemble GEMM from rocprofv3 PMC passes -> profiles/gemm_traffic_<gemm>.json.
+"""HBM traffic of the ensemble GEMM from rocprofv3 PMC passes -> amp_extensions_amd/data/gemm_traffic_<gemm>.json
+(bench.py reads it there; keyed to the GEMM sources' hash).
 
 Two separate counter passes over the same bench command (MI355X_MICROARCH.md, HBM section:
 one counter per pass, FETCH_SIZE counts half of the wide coalesced loads on gfx950 -> x2):
@@ -66,8 +67,10 @@ def main():
         layers.append({"layer": i, "K": K, "fetch_kb": f[i], "write_kb": w[i], "hbm_bytes": hbm, "alg_bytes": alg})
         tot_hbm += hbm
         tot_alg += alg
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import gemm_source_sha16
     print(json.dumps({
-        "kernel": f"{kernel} (ensemble layers)", "gemm": gemm, "state_dim": S, "action_dim": A, "lanes": B,
+        "kernel": f"{kernel} (ensemble layers)", "gemm": gemm, "gemm_source_sha16": gemm_source_sha16(), "state_dim": S, "action_dim": A, "lanes": B,
         "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), bench.py --steps 3, last step",
         "method": "hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch (gfx950: FETCH_SIZE counts 1/2 of "
                   "wide coalesced loads, MI355X_MICROARCH.md HBM section); L2<->fabric traffic (Infinity-Cache "

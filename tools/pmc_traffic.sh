@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC HBM-traffic passes for the ensemble GEMM (one counter per pass, no trace domains),
-# then gpurun_out/gemm_traffic_<gemm>.json (copy to profiles/).
+# then gpurun_out/gemm_traffic_<gemm>.json (copy to amp_extensions_amd/data/, where bench.py reads it).
 # usage (on the GPU box): bash tools/pmc_traffic.sh [tag] [f16x3|bf16x6|f32]
 set -o pipefail
 TAG=${1:-r01}
