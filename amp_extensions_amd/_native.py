@@ -29,6 +29,12 @@ SIGNATURES = {
                                     c_int, c_int, c_dbl, c_int, c_dbl]),
     "amx_assemble_input": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp]),
     "amx_assemble_input_rexp": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp, c_ll, c_ll, c_int, vp]),
+    "amx_set_lb_stage": (c_int, [vp, c_int]),
+    "amx_assemble_input_limbs": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp, c_ll, vp]),
+    "amx_gemm_bias_act_lb": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll, vp, c_ll,
+                                     vp, c_int, c_ll, c_int, c_int, vp, c_ll, c_ll, vp, c_int, c_int, vp]),
+    "amx_gemm_out_unnorm_lb": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll, vp, c_ll,
+                                       vp, c_int, c_ll, vp, c_ll, c_ll, c_int, c_int, vp]),
     "amx_gemm_bias_act": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
                                   vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp]),
     "amx_gemm_out_unnorm": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,

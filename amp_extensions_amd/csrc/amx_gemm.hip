@@ -739,79 +739,6 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
   }
 }
 
-// amx_set_gemm_timer: the last workgroup of a forward's output layer adds (now - start) to the
-// tick sum (stamps only in a buffer nothing else reads)
-__device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t nwg = gridDim.x;
-    if (atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 1), 1ull) == nwg - 1) {
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 2), (unsigned long long)(now - a.timer[0]));
-      atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 3), 1ull);
-      atomicExch(reinterpret_cast<unsigned long long*>(a.timer + 1), 0ull);
-    }
-  }
-}
-
-typedef __attribute__((address_space(1))) uint32_t gu32s;
-
-// Stream-K combine (the output layer at lane counts whose 128 x 224 tiles are fewer than the
-// CUs: the tiles' K-tiles are dealt out evenly over one workgroup per CU, so a tile's K range is
-// covered by nseg <= 3 consecutive workgroups): every segment stores its raw (scaled)
-// accumulators write-through (sc1, 16-B per lane) in its slot, drains, and adds to the tile's
-// arrival counter (agent scope); the last arriver acquires, sums the segments in K order --
-// P0 + P1 + ... whatever the arrival order, so the result is deterministic -- resets the
-// counter and returns true to run the epilogue (cdna_hip_programming.md §5, in-launch split-K:
-// one release and one acquire per tile).
-template <class TL>
-__device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL::MB][TL::NB], int tile, int seg,
-                                              int nseg, int* flag) {
-  constexpr int MB = TL::MB, NB = TL::NB, NT = TL::NT;
-  const int t = threadIdx.x;
-  const long long per_slice = (long long)MB * NB * NT;  // f32x4 per slot
-  f32x4* base = reinterpret_cast<f32x4*>(a.split_scratch) + (long long)tile * a.ksplit * per_slice;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < NB; ++n)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m][n]), rs,
-                                             (int)(((seg * MB + m) * NB + n) * NT + t) * 16, 0, 16 /* sc1 */);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t == 0) {
-    const uint32_t old = __hip_atomic_fetch_add((gu32s*)(a.split_cnt + tile), 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (uint32_t)(nseg - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store((gu32s*)(a.split_cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *flag = last;
-  }
-  __syncthreads();
-  if (!*flag) return false;
-  // acc = P0, acc += P1, ... in K order, this segment's own slot read back like the others (the
-  // same bits it stored), so the sum runs in place in the accumulators (a second copy spilled
-  // the 128-accumulator tiles) and one segment's loads for all MB x NB blocks are in flight
-  // together: nseg memory round trips, not one per block and segment
-  (void)seg;
-  for (int s = 0; s < nseg; ++s) {
-#pragma unroll
-    for (int m = 0; m < MB; ++m)
-#pragma unroll
-      for (int n = 0; n < NB; ++n) {
-        const f32x4 p = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                      rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
-        acc[m][n] = s == 0 ? p : acc[m][n] + p;
-      }
-  }
-  return true;
-}
-
 // One output tile (logical id `tile`, see map_tile; or, stream-K, the K-tiles [kb, ke) of it:
 // segment seg of nseg) of the f16x3 GEMM; the caller runs the timer hooks.
 template <int EPI, class TL>
@@ -2129,11 +2056,16 @@ extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, 
   // the 256-row output tiles (amx_set_out_tile 4)
   int nwg2 = 0, ksplit2 = 0;
   const int tiles2 = streamk_tiles(ctx, groups, rows, &nwg2, &ksplit2, ctx->k0_pad + ctx->L * ctx->H, 256);
+  // the limb-format forward's stream-K shapes (amx_gemm_lb.hip)
+  int nc_lb = 0;
+  const long long f_lb = amx::lb_split_floats(ctx, groups, rows, &nc_lb);
   int nc = tiles > tiles_h ? tiles : tiles_h;
   nc = nc > tiles2 ? nc : tiles2;
+  nc = nc > nc_lb ? nc : nc_lb;
   if (n_counters) *n_counters = nc;
   const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
   const long long f2 = (long long)tiles2 * ksplit2 * 256 * 224;
-  const long long f = fo > fh ? fo : fh;
-  return f > f2 ? f : f2;
+  long long f = fo > fh ? fo : fh;
+  f = f > f2 ? f : f2;
+  return f > f_lb ? f : f_lb;
 }

@@ -46,6 +46,10 @@ struct GemmArgs {
   uint32_t* split_cnt;     //   arrivals per tile (zero between launches: the last arriver resets it)
   uint64_t* timer;         // amx_set_gemm_timer buffer (null: off)
   int timer_role;          //   1: first layer of a forward (block 0 stamps the start), 2: output layer
+  // limb-format activations (amx_gemm_lb.hip): A is stored as scaled fp16 limb pairs, one
+  // exponent per row and chunk (x0, then 128-column chunks of the hidden slices)
+  int lb_k0;               // columns of chunk 0 (the x0 slice)
+  long long rexp_ld;       // elements between two exponent slots of one group (the padded rows)
 };
 
 // Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over
@@ -184,6 +188,82 @@ __device__ __forceinline__ void rs_step(uint32_t* v, int li) {
     const uint32_t recv = (uint32_t)__builtin_amdgcn_ds_swizzle((int)send, 0x1f | (MASK << 10));
     v[i] = keep > recv ? keep : recv;
   }
+}
+
+// amx_set_gemm_timer: the last workgroup of a forward's output layer adds (now - start) to the
+// tick sum (stamps only in a buffer nothing else reads)
+__device__ __forceinline__ void gemm_timer_end(const GemmArgs& a) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t nwg = gridDim.x;
+    if (atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 1), 1ull) == nwg - 1) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 2), (unsigned long long)(now - a.timer[0]));
+      atomicAdd(reinterpret_cast<unsigned long long*>(a.timer + 3), 1ull);
+      atomicExch(reinterpret_cast<unsigned long long*>(a.timer + 1), 0ull);
+    }
+  }
+}
+
+typedef __attribute__((address_space(1))) uint32_t gu32s;
+
+// Stream-K combine (the output layer at lane counts whose 128 x 224 tiles are fewer than the
+// CUs: the tiles' K-tiles are dealt out evenly over one workgroup per CU, so a tile's K range is
+// covered by nseg <= 3 consecutive workgroups): every segment stores its raw (scaled)
+// accumulators write-through (sc1, 16-B per lane) in its slot, drains, and adds to the tile's
+// arrival counter (agent scope); the last arriver acquires, sums the segments in K order --
+// P0 + P1 + ... whatever the arrival order, so the result is deterministic -- resets the
+// counter and returns true to run the epilogue (cdna_hip_programming.md §5, in-launch split-K:
+// one release and one acquire per tile).
+template <class TL>
+__device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL::MB][TL::NB], int tile, int seg,
+                                              int nseg, int* flag) {
+  constexpr int MB = TL::MB, NB = TL::NB, NT = TL::NT;
+  const int t = threadIdx.x;
+  const long long per_slice = (long long)MB * NB * NT;  // f32x4 per slot
+  f32x4* base = reinterpret_cast<f32x4*>(a.split_scratch) + (long long)tile * a.ksplit * per_slice;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[m][n]), rs,
+                                             (int)(((seg * MB + m) * NB + n) * NT + t) * 16, 0, 16 /* sc1 */);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add((gu32s*)(a.split_cnt + tile), 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(nseg - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store((gu32s*)(a.split_cnt + tile), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  // per block: v = P0, v += P1, ... (own segment from the accumulators) -- the segments' sum in
+  // K order without a second copy of the accumulators (which spilled the 128-accumulator tiles).
+  // (Round 4: reading this segment's slot back with the others so every segment's loads are in
+  // flight together measured no faster at the N = 8 share, profiles/r04a_share_ab.txt.)
+#pragma unroll
+  for (int m = 0; m < MB; ++m)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) {
+      const f32x4 mine = acc[m][n];
+      f32x4 v = mine;
+      for (int s = 0; s < nseg; ++s) {
+        const f32x4 p = s == seg ? mine
+                                 : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                 rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
+        v = s == 0 ? p : v + p;
+      }
+      acc[m][n] = v;
+    }
+  return true;
 }
 
 }  // namespace

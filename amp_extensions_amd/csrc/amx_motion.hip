@@ -181,12 +181,126 @@ __device__ inline MView stage_tables(const double* blob, double* hdr, double* jt
   return m;
 }
 
+// ---- reset noise: cKinCharacter::AddNoise (anim/KinCharacter.cpp:340-470) -------------------
+// SceneImitate::ResetKinCharTime (scenes/SceneImitate.cpp:469-489) perturbs the kinematic pose /
+// velocity at the reset time before the sim character takes them (SyncCharacters) and before the
+// placement and the ground resolve (SceneSimChar.cpp:699-716).  The reference draws from
+// DeepMimicCore's process-global std::default_random_engine (util/Rand.cpp), which cannot be
+// reproduced; here draw k of a reset comes from Philox(seed; lane, reset#, k/2, tag) (tags split
+// RandomRotatePoseVel's RandDouble stream from AddNoisePoseVel's RandDoubleEigen stream, as the
+// reference's mRandGen / mGen), or from an injected [B][ld] table (tests: rotation draws at
+// [0, AMX_NOISE_ROT_SLOTS), pose / velocity draws after them).  u -> lo + u (hi - lo) as
+// cRand::RandDouble.  Same operation order as oracle/deepmimic_ref.add_noise.
+constexpr uint32_t kTagNoiseRot = 0x4E524F54u;  // 'NROT'
+constexpr uint32_t kTagNoisePV = 0x4E505620u;   // 'NPV '
+
+struct NoiseArgs {
+  int on;  // any noise (radian != 0 or (min, max) != (0, 0))
+  int bef_rot, rot_vel_w_pose, vel_noise, knee_rot;
+  double lo, hi, radian, interp;
+  const double* draws;  // nullable injected uniforms [B][ld]
+  long long ld;
+  uint32_t k0, k1;      // Philox key
+};
+
+struct NoiseDraws {
+  const NoiseArgs& n;
+  int lane, rc;
+  __device__ double u(int k, bool pv) const {
+    if (n.draws) return n.draws[(long long)lane * n.ld + (pv ? AMX_NOISE_ROT_SLOTS : 0) + k];
+    const amx::u32x4 r = amx::philox4x32_10({(uint32_t)lane, (uint32_t)rc, (uint32_t)(k >> 1), pv ? kTagNoisePV : kTagNoiseRot},
+                                            n.k0, n.k1);
+    return (k & 1) ? amx::u53(r.z, r.w) : amx::u53(r.x, r.y);
+  }
+};
+
+// cMathUtil::EulerToQuaternion (util/MathUtil.cpp:347-381, 423-466)
+__device__ inline Q euler_q(double x, double y, double z) {
+  const double xs = sin(x), xc = cos(x), ys = sin(y), yc = cos(y), zs = sin(z), zc = cos(z);
+  double c = (yc * zc + xs * ys * zs + xc * zc + xc * yc - 1) * 0.5;
+  c = fmin(fmax(c, -1.0), 1.0);
+  const double th = acos(c);
+  V3 ax = {0.0, 0.0, 1.0};
+  if (!(fabs(th) < 0.00001)) {
+    const double m21 = xs * yc - xc * ys * zs + xs * zc;
+    const double m02 = xc * ys * zc + xs * zs + ys;
+    const double m10 = yc * zs - xs * ys * zc + xc * zs;
+    const double den = sqrt(m21 * m21 + m02 * m02 + m10 * m10);
+    ax = {m21 / den, m02 / den, m10 / den};
+  }
+  const double ch = cos(th / 2), sh = sin(th / 2);
+  return {ch, sh * ax.x, sh * ax.y, sh * ax.z};
+}
+__device__ inline void stq(double* p, Q q) { p[0] = q.w; p[1] = q.x; p[2] = q.y; p[3] = q.z; }
+
+// one thread, the lane's pose / vel in LDS (humanoid3d's knee / hip / ankle joint indices, as
+// hard-coded in the reference, including its velocity-noise test !(j == 4 || j != 10))
+__device__ void add_noise(const MView& m, double* pose, double* vel, const NoiseArgs& n, const NoiseDraws& d) {
+  int kr = 0, kp = 0;
+  const double r = n.radian, lo = n.lo, hi = n.hi;
+  auto rnd = [&]() { return -r + d.u(kr++, false) * (r - (-r)); };
+  auto pose_vel = [&]() {  // AddNoisePoseVel
+    if (lo == 0 && hi == 0) return;
+    for (int i = 0; i < m.D; ++i) pose[i] = pose[i] + (lo + d.u(kp++, true) * (hi - lo));
+    for (int i = 0; i < m.D; ++i) vel[i] = vel[i] + (lo + d.u(kp++, true) * (hi - lo));
+  };
+  auto rotate = [&]() {  // RandomRotatePoseVel
+    if (r == 0) return;
+    const double a = rnd();
+    Q q = qmul({cos(a / 2), 0.0, sin(a / 2), 0.0}, ldq(pose + 3));  // cCharacter::RotateRoot
+    stq(pose + 3, qnorm(q));
+    for (int i = 0; i < 7; ++i) vel[i] = n.interp * vel[i];  // root vel (3) + root ang vel (gRotDim 4)
+    for (int j = 1; j < m.J; ++j) {
+      const int o = (int)m.joints[8 * j + 2], sz = (int)m.joints[8 * j + 3];
+      for (int i = 0; i < sz; ++i) vel[o + i] = n.interp * vel[o + i];
+    }
+    for (int j = 1; j < m.J; ++j) {
+      const int t = (int)m.joints[8 * j], o = (int)m.joints[8 * j + 2];
+      if (t == JT_REVOLUTE) {
+        if (!(j == 4 || j == 10) || n.knee_rot) pose[o] = pose[o] + rnd();
+      } else if (t == JT_SPHERICAL && j != 3 && j != 5 && j != 9 && j != 11) {
+        const double ps = rnd(), th = rnd(), ph = rnd();
+        const Q qr = euler_q(ps, th, ph);
+        stq(pose + o, qmul(qr, ldq(pose + o)));
+        if (n.rot_vel_w_pose) stq(vel + o, qmul(qr, ldq(vel + o)));
+      }
+    }
+    if (n.vel_noise) {
+      const double ps = rnd(), th = rnd(), ph = rnd();
+      stq(vel + 3, qmul(euler_q(ps, th, ph), ldq(vel + 3)));
+      for (int j = 1; j < m.J; ++j) {
+        const int t = (int)m.joints[8 * j], o = (int)m.joints[8 * j + 2];
+        if (t == JT_REVOLUTE) {
+          if (!(j == 4 || j != 10) || n.knee_rot) vel[o] = vel[o] + rnd();
+        } else if (t == JT_SPHERICAL && j != 3 && j != 5 && j != 9 && j != 11) {
+          const double ps2 = rnd(), th2 = rnd(), ph2 = rnd();
+          stq(vel + o, qmul(euler_q(ps2, th2, ph2), ldq(vel + o)));
+        }
+      }
+    }
+    stq(pose + 3, qnorm(ldq(pose + 3)));  // KinTree::PostProcessPose
+    for (int j = 1; j < m.J; ++j)
+      if ((int)m.joints[8 * j] == JT_SPHERICAL) {
+        const int o = (int)m.joints[8 * j + 2];
+        stq(pose + o, qnorm(ldq(pose + o)));
+      }
+  };
+  if (n.bef_rot) {
+    pose_vel();
+    rotate();
+  } else {
+    rotate();
+    pose_vel();
+  }
+}
+
 // The recorded state at motion time `time` (see the file comment).  out: [S] = 1 + 15 J.
 // Called by all 64 threads of a one-wave workgroup; thread j < J owns joint j.  The joint
 // transforms are composed level by level down the tree (the parent is always done first),
 // with the same per-joint arithmetic as a sequential walk, so the result does not depend on
 // the thread mapping.
-__device__ void motion_state(const MView& m, double time, int flags, double* __restrict__ out, MotionLds& L) {
+__device__ void motion_state(const MView& m, double time, int flags, double* __restrict__ out, MotionLds& L,
+                             const NoiseArgs* noise = nullptr, int lane = 0, int rc = 0) {
   const int tid = threadIdx.x;
   const double dur = m.h[4];
   const bool loop = m.h[3] != 0.0;
@@ -233,12 +347,16 @@ __device__ void motion_state(const MView& m, double time, int flags, double* __r
       L.pose[1] += cycles * m.h[9];
       L.pose[2] += cycles * m.h[10];
     }
-    L.pose[0] = 0.0;  // random placement on the plane: root x, z = 0
-    L.pose[2] = 0.0;
   } else if (tid < m.J && (int)m.joints[8 * tid] == JT_SPHERICAL) {
     const int o = (int)m.joints[8 * tid + 2];
     const Q q = slerp(ldq(f0 + o), ldq(f1 + o), lerp);
     L.pose[o] = q.w; L.pose[o + 1] = q.x; L.pose[o + 2] = q.y; L.pose[o + 3] = q.z;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (noise && noise->on) add_noise(m, L.pose, L.vel, *noise, NoiseDraws{*noise, lane, rc});
+    L.pose[0] = 0.0;  // random placement on the plane: root x, z = 0 (after the noise)
+    L.pose[2] = 0.0;
   }
   __syncthreads();
   // ---- kinematics, one tree level per pass ----------------------------------------------------
@@ -660,12 +778,13 @@ __global__ __launch_bounds__(64) void k_motion_amp_obs(const double* __restrict_
 
 // one 64-thread workgroup per lane (motion_state)
 __global__ __launch_bounds__(64) void k_motion_states(const double* __restrict__ blob, const double* __restrict__ times,
-                                                      int B, int flags, double* __restrict__ ob, long long ldo) {
+                                                      int B, int flags, double* __restrict__ ob, long long ldo,
+                                                      NoiseArgs noise) {
   __shared__ MotionLds L;
   const int b = blockIdx.x;
   if (b >= B) return;
   const MView m = stage_tables(blob, L.hdr, L.jt, L.bt);
-  motion_state(m, times[b], flags, ob + (long long)b * ldo, L);
+  motion_state(m, times[b], flags, ob + (long long)b * ldo, L, &noise, b, 0);
 }
 
 // SimEnv.reset on masked lanes with motion states: reset_count/model_idx/num_steps as in
@@ -676,7 +795,7 @@ __global__ __launch_bounds__(64) void k_reset_motion(const double* __restrict__ 
                                                      const double* __restrict__ times, uint32_t k0, uint32_t k1,
                                                      double tmax, int flags, const double* ob_src, double* ob_out,
                                                      int32_t* num_steps, int32_t* model_idx, int32_t* reset_count,
-                                                     double* t_out, int S, int M, int B) {
+                                                     double* t_out, int S, int M, int B, NoiseArgs noise) {
   __shared__ MotionLds L;
   const int b = blockIdx.x, tid = threadIdx.x;
   if (b >= B) return;
@@ -696,7 +815,7 @@ __global__ __launch_bounds__(64) void k_reset_motion(const double* __restrict__ 
     const amx::u32x4 r = amx::philox4x32_10({(uint32_t)b, (uint32_t)rc, 0u, amx::kTagMotion}, k0, k1);
     t = 0.0 + (tmax - 0.0) * amx::u53(r.x, r.y);
   }
-  motion_state(m, t, flags, ob_out + (long long)b * S, L);
+  motion_state(m, t, flags, ob_out + (long long)b * S, L, &noise, b, rc);
   if (tid == 0) {
     reset_count[b] = rc;
     model_idx[b] = rc % M;
@@ -758,13 +877,72 @@ extern "C" int amx_set_motion(amx_ctx* c, const double* blob, long long n) {
 
 extern "C" double amx_motion_duration(const amx_ctx* c) { return (c && c->d_motion) ? c->motion_duration : -1.0; }
 
-extern "C" int amx_motion_states(amx_ctx* c, const double* times, int B, int flags, double* ob, long long ldo,
-                                 void* stream) {
+namespace {
+// NoiseArgs of a launch (no noise when `noise` is null or all its amounts are zero)
+int noise_args(const char* fn, const amx_ctx* c, const amx_reset_noise* noise, const double* draws, long long ld,
+               uint64_t seed, NoiseArgs& n) {
+  n = NoiseArgs{};
+  if (!noise) return AMX_OK;
+  AMX_CHECK_ARG(noise->radian == noise->radian && noise->noise_min == noise->noise_min &&
+                    noise->noise_max == noise->noise_max && noise->interp == noise->interp,
+                "%s: NaN in the reset noise", fn);
+  n.on = noise->radian != 0.0 || noise->noise_min != 0.0 || noise->noise_max != 0.0;
+  n.bef_rot = noise->noise_bef_rot != 0;
+  n.rot_vel_w_pose = noise->rot_vel_w_pose != 0;
+  n.vel_noise = noise->vel_noise != 0;
+  n.knee_rot = noise->knee_rot != 0;
+  n.lo = noise->noise_min;
+  n.hi = noise->noise_max;
+  n.radian = noise->radian;
+  n.interp = noise->interp;
+  n.k0 = (uint32_t)seed;
+  n.k1 = (uint32_t)(seed >> 32);
+  AMX_CHECK_ARG(!draws || ld >= AMX_NOISE_ROT_SLOTS + 2LL * c->motion_D,
+                "%s: injected draws need ld >= %d + 2 D = %lld", fn, AMX_NOISE_ROT_SLOTS,
+                AMX_NOISE_ROT_SLOTS + 2LL * c->motion_D);
+  n.draws = draws;
+  n.ld = ld;
+  return AMX_OK;
+}
+}  // namespace
+
+extern "C" int amx_motion_states_noise(amx_ctx* c, const double* times, int B, int flags, const amx_reset_noise* noise,
+                                       const double* draws, long long ld_draws, uint64_t seed, double* ob,
+                                       long long ldo, void* stream) {
   AMX_CHECK_ARG(c && c->d_motion, "amx_motion_states: no motion set (amx_set_motion)");
   AMX_CHECK_ARG(times && ob && B >= 0 && ldo >= c->S, "amx_motion_states: bad arguments");
+  NoiseArgs n;
+  int rc = noise_args("amx_motion_states_noise", c, noise, draws, ld_draws, seed, n);
+  if (rc) return rc;
   if (B == 0) return AMX_OK;
   hipLaunchKernelGGL(k_motion_states, dim3(B), dim3(64), 0, (hipStream_t)stream, c->d_motion, times, B,
-                     flags, ob, ldo);
+                     flags, ob, ldo, n);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_motion_states(amx_ctx* c, const double* times, int B, int flags, double* ob, long long ldo,
+                                 void* stream) {
+  return amx_motion_states_noise(c, times, B, flags, nullptr, nullptr, 0, 0, ob, ldo, stream);
+}
+
+extern "C" int amx_reset_lanes_motion_noise(amx_ctx* c, const uint8_t* mask, const double* times, uint64_t seed,
+                                            double time_max, int flags, const amx_reset_noise* noise,
+                                            const double* draws, long long ld_draws, const double* ob_src,
+                                            double* ob_out, int32_t* num_steps, int32_t* model_idx,
+                                            int32_t* reset_count, double* t_out, int B, void* stream) {
+  AMX_CHECK_ARG(c && c->d_motion, "amx_reset_lanes_motion: no motion set (amx_set_motion)");
+  AMX_CHECK_ARG(ob_out && num_steps && model_idx && reset_count && B >= 0, "amx_reset_lanes_motion: null pointer");
+  AMX_CHECK_ARG(mask == nullptr || ob_src != nullptr, "amx_reset_lanes_motion: masked reset needs ob_src");
+  AMX_CHECK_ARG(time_max == time_max, "amx_reset_lanes_motion: time_max is NaN");
+  NoiseArgs n;
+  // the noise stream's key: the lane seed with the high word flipped (the reset-time draw uses the seed itself)
+  int rc = noise_args("amx_reset_lanes_motion_noise", c, noise, draws, ld_draws, seed ^ 0x9E3779B97F4A7C15ull, n);
+  if (rc) return rc;
+  if (B == 0) return AMX_OK;
+  hipLaunchKernelGGL(k_reset_motion, dim3(B), dim3(64), 0, (hipStream_t)stream, c->d_motion, mask, times,
+                     (uint32_t)seed, (uint32_t)(seed >> 32), time_max > 0.0 ? time_max : c->motion_duration, flags, ob_src, ob_out, num_steps, model_idx,
+                     reset_count, t_out, c->S, c->M, B, n);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -772,16 +950,8 @@ extern "C" int amx_motion_states(amx_ctx* c, const double* times, int B, int fla
 extern "C" int amx_reset_lanes_motion(amx_ctx* c, const uint8_t* mask, const double* times, uint64_t seed,
                                       double time_max, int flags, const double* ob_src, double* ob_out, int32_t* num_steps,
                                       int32_t* model_idx, int32_t* reset_count, double* t_out, int B, void* stream) {
-  AMX_CHECK_ARG(c && c->d_motion, "amx_reset_lanes_motion: no motion set (amx_set_motion)");
-  AMX_CHECK_ARG(ob_out && num_steps && model_idx && reset_count && B >= 0, "amx_reset_lanes_motion: null pointer");
-  AMX_CHECK_ARG(mask == nullptr || ob_src != nullptr, "amx_reset_lanes_motion: masked reset needs ob_src");
-  AMX_CHECK_ARG(time_max == time_max, "amx_reset_lanes_motion: time_max is NaN");
-  if (B == 0) return AMX_OK;
-  hipLaunchKernelGGL(k_reset_motion, dim3(B), dim3(64), 0, (hipStream_t)stream, c->d_motion, mask, times,
-                     (uint32_t)seed, (uint32_t)(seed >> 32), time_max > 0.0 ? time_max : c->motion_duration, flags, ob_src, ob_out, num_steps, model_idx,
-                     reset_count, t_out, c->S, c->M, B);
-  AMX_CHECK_LAUNCH();
-  return AMX_OK;
+  return amx_reset_lanes_motion_noise(c, mask, times, seed, time_max, flags, nullptr, nullptr, 0, ob_src, ob_out,
+                                      num_steps, model_idx, reset_count, t_out, B, stream);
 }
 
 // ---- AMP observation features ----------------------------------------------------------------

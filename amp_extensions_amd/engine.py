@@ -146,13 +146,32 @@ class DeviceEnsemble:
 
     GEMM_PRECISIONS = ("f16x3", "bf16x6", "f32")
 
-    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "f16x3"):
+    ACT_FORMATS = ("f32", "limbs")
+
+    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "f16x3",
+                 act_format: str = "f32"):
         """gemm: "bf16x6" (fp32 operands split into 3 bf16 limbs, 6 limb products on the bf16
         MFMA pipe: fp32-level error, amx_gemm_*_x6), "f16x3" (power-of-two scaled operands
-        split into 2 fp16 limbs, 3 products: amx_gemm_*_h3) or "f32" (v_mfma_f32_32x32x2_f32)."""
+        split into 2 fp16 limbs, 3 products) or "f32" (v_mfma_f32_32x32x2_f32).
+        act_format (f16x3): "f32" (default) -- fp32 activation rows, split into limbs by every
+        consumer (amx_gemm_*_h3); "limbs" -- rows stored as scaled fp16 limb pairs with one
+        exponent per row and 128-column chunk, each value split once by its producer
+        (amx_assemble_input_limbs, amx_gemm_*_lb; hidden width a multiple of 256).  The limb form
+        is exact to the same tolerance and measured slower (the K loop's time per K-tile is the
+        same without the split, the limb epilogue costs more)."""
         if gemm not in self.GEMM_PRECISIONS:
             raise ValueError(f"gemm must be one of {self.GEMM_PRECISIONS}, got {gemm!r}")
+        if act_format not in self.ACT_FORMATS:
+            raise ValueError(f"act_format must be one of {self.ACT_FORMATS}, got {act_format!r}")
         self.gemm = gemm
+        lb_ok = (gemm == "f16x3" and ctx.Hp % 256 == 0 and ctx.k0_pad <= 1024
+                 and 1 + ctx.L * ctx.Hp // 128 <= 24)
+        if act_format == "limbs" and not lb_ok:
+            raise ValueError("act_format='limbs' needs gemm='f16x3', a hidden width that is a multiple of 256, "
+                             "S + A <= 1024 and at most 23 hidden chunks of 128 columns")
+        self.limbs = act_format == "limbs"
+        # exponent slots per row: f32 format x0, h0 .. h_{L-1}; limbs x0 + one per 128 hidden columns
+        self.n_slots = 1 + ctx.L * ctx.Hp // 128 if self.limbs else ctx.L + 1
         self.shared_x0 = True  # f16x3: x0 assembled once, read by every member (k_shared)
         self.ctx = ctx
         S, A, M, Hp, L = ctx.S, ctx.A, ctx.M, ctx.Hp, ctx.L
@@ -211,8 +230,9 @@ class DeviceEnsemble:
             c = self.ctx
             ws = dict(Bp=Bp, act=torch.zeros(c.M, Bp, c.ldk, dtype=torch.float32, device=c.device),
                       preds=torch.zeros(c.M, Bp, c.S, dtype=torch.float32, device=c.device),
-                      # f16x3: row exponents of the activation slices [M][L+1][Bp] (x0, h0..h_{L-1})
-                      rexp=torch.zeros(c.M, c.L + 1, Bp, dtype=torch.int32, device=c.device))
+                      # f16x3: row exponents [M][slots][Bp] (f32 format: x0, h0..h_{L-1}; limbs: x0, then
+                      # one slot per 128 hidden columns)
+                      rexp=torch.zeros(c.M, self.n_slots, Bp, dtype=torch.int32, device=c.device))
             if self.W2 is not None:
                 self._ensure_split_workspace(Bp)
             self._ws[Bp] = ws
@@ -258,6 +278,15 @@ class DeviceEnsemble:
         s = c.stream
         rexp = ws["rexp"]
         k_shared = 0
+        if self.limbs:
+            if x0_ready or assembled:
+                raise ValueError("x0_ready / assembled need act_format='f32' (the fused assemblies write fp32 x0)")
+            k_shared = c.k0_pad if self.shared_x0 else 0
+            N.check(c.lib.amx_assemble_input_limbs(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(),
+                                                   0 if k_shared else Bp * c.ldk, c.ldk, B, rexp.data_ptr(),
+                                                   self.n_slots * Bp, s), "amx_assemble_input_limbs")
+            self._mlp(buf, preds, Bp, s, rexp, row_exponents=False, k_shared=k_shared)
+            return preds
         if x0_ready:
             if self.W2 is None:
                 raise ValueError("x0_ready needs the f16x3 GEMM (shared x0 slice + row exponents)")
@@ -290,6 +319,24 @@ class DeviceEnsemble:
                                              Bp * c.S, rexp.data_ptr(), sR, L + 1, k_shared, s),
                 "amx_gemm_out_unnorm_h3")
 
+    def _mlp_lb(self, buf, preds, Bp, s, rexp, k_shared=0):
+        """The limb-format forward: L hidden layers (each writes its slice's limbs and chunk
+        exponents) and the output layer, amx_gemm_*_lb."""
+        c = self.ctx
+        sA, sR, L, per = Bp * c.ldk, self.n_slots * Bp, c.L, c.Hp // 128
+        for i in range(L):
+            K = c.k0_pad + i * c.Hp
+            N.check(c.lib.amx_gemm_bias_act_lb(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),
+                                               c.Hp * 2 * K, self.wexp[i].data_ptr(), c.Hp, self.b[i].data_ptr(), c.Hp,
+                                               buf.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, rexp.data_ptr(), sR, Bp,
+                                               rexp[0, 1 + i * per].data_ptr(), c.k0_pad, k_shared, s),
+                    "amx_gemm_bias_act_lb")
+        N.check(c.lib.amx_gemm_out_unnorm_lb(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
+                                             self.W2[L].data_ptr(), c.n_out_pad * 2 * c.ldk, self.wexp[L].data_ptr(),
+                                             c.n_out_pad, self.b[L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
+                                             Bp * c.S, rexp.data_ptr(), sR, Bp, c.k0_pad, k_shared, s),
+                "amx_gemm_out_unnorm_lb")
+
     def _mlp(self, buf, preds, Bp, s, rexp, row_exponents=True, k_shared=0):
         c = self.ctx
         sA = Bp * c.ldk
@@ -301,7 +348,7 @@ class DeviceEnsemble:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         if self.W2 is not None:
-            self._mlp_h3(buf, preds, Bp, s, rexp, k_shared)
+            (self._mlp_lb if self.limbs else self._mlp_h3)(buf, preds, Bp, s, rexp, k_shared)
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1, Bp))

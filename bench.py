@@ -80,6 +80,11 @@ def parse():
     p.add_argument("--gemm", choices=["f16x3", "bf16x6", "f32"], default="f16x3",
                    help="ensemble GEMM: scaled 2-limb fp16 split (3 products) or 3-limb bf16 split (6 products) on "
                         "the 16-bit MFMA pipe (both fp32-level error), or f32 MFMA")
+    p.add_argument("--act-format", choices=["f32", "limbs"], default="f32",
+                   help="f16x3 activation rows: f32 (split by every consumer, amx_gemm_*_h3; default) or limbs "
+                        "(split once by the producer, amx_gemm_*_lb; measured slower, DESIGN §6 round 4)")
+    p.add_argument("--lb-stage", type=int, choices=[0, 1], default=0,
+                   help="limb forward's K-loop staging: 0 registers, 1 LDS-DMA (A/B)")
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
@@ -364,7 +369,9 @@ def main():
     from amp_extensions_amd.ensemble import init_ensemble_weights
     ens_w = init_ensemble_weights(S, A, hidden, M, base_seed=100)
     ctx = amx.AmxContext(S, A, n_models=M, hidden=512, n_hidden=4, feat_dim=512, device=dev)
-    ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm)
+    ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm, act_format=args.act_format)
+    if args.lb_stage:
+        ctx.lib.amx_set_lb_stage(ctx.h, args.lb_stage)
     thr = ens.compute_threshold(st.to(dev), at.to(dev))
     reset_source = syn.reset_table(65536, S, 1)
     if args.cost == "amp":

@@ -318,12 +318,143 @@ def body_aabb_min_y(body, R, c):
     return c[1] - np.abs(R[1]) @ half
 
 
+# ---- reset noise: cKinCharacter::AddNoise (anim/KinCharacter.cpp:340-470) ------------------
+NOISE_ROT_SLOTS = 48   # uniforms reserved per reset for RandomRotatePoseVel's draws
+HIPS_ANKLES = (3, 5, 9, 11)   # humanoid3d joints RandomRotatePoseVel never perturbs
+KNEES = (4, 10)
+
+
+def euler_to_quat(x, y, z):
+    """cMathUtil::EulerToQuaternion = AxisAngleToQuaternion(EulerToAxisAngle(euler))
+    (util/MathUtil.cpp:347-381, 423-466)."""
+    xs, xc, ys, yc, zs, zc = math.sin(x), math.cos(x), math.sin(y), math.cos(y), math.sin(z), math.cos(z)
+    c = (yc * zc + xs * ys * zs + xc * zc + xc * yc - 1) * 0.5
+    c = min(max(c, -1.0), 1.0)
+    th = math.acos(c)
+    if abs(th) < 0.00001:
+        axis = np.array([0.0, 0.0, 1.0])
+    else:
+        m21 = xs * yc - xc * ys * zs + xs * zc
+        m02 = xc * ys * zc + xs * zs + ys
+        m10 = yc * zs - xs * ys * zc + xc * zs
+        den = math.sqrt(m21 * m21 + m02 * m02 + m10 * m10)
+        axis = np.array([m21 / den, m02 / den, m10 / den])
+    ch, sh = math.cos(th / 2), math.sin(th / 2)
+    return np.array([ch, sh * axis[0], sh * axis[1], sh * axis[2]])
+
+
+def add_noise(joints, pose, vel, ra, u_rot, u_pv):
+    """cKinCharacter::AddNoise(noise_bef_rot, min, max, radian, rot_vel_w_pose, vel_noise, interp,
+    knee_rot) on the kinematic pose / velocity at the reset time (SceneImitate::ResetKinCharTime,
+    scenes/SceneImitate.cpp:469-489), with its uniforms injected: u_rot feeds RandomRotatePoseVel's
+    cMathUtil::RandDouble(-radian, radian) draws (gRand's mRandGen) in call order, u_pv
+    AddNoisePoseVel's RandDoubleEigen(size, min, max) draws (gRand's mGen): pose elements, then
+    velocity elements.  A draw u in [0, 1) gives lo + u (hi - lo) (cRand::RandDouble,
+    util/Rand.cpp:35-46; std::uniform_real_distribution).  Quaternions are (w, x, y, z) pose
+    segments (cMathUtil::VecToQuat / QuatToVec); velocity segments are rotated as the reference
+    does, the 4-vector (w_x, w_y, w_z, pad) read as a quaternion (w = w_x).  The joint indices of
+    the knee / hip / ankle exclusions are humanoid3d's, as hard-coded in the reference, and so is
+    the velocity-noise revolute test `!(j == 4 || j != 10) || knee_rot` (only joint 10 unless
+    knee_rot).  Returns new (pose, vel)."""
+    pose, vel = np.array(pose, float), np.array(vel, float)
+    lo, hi, r = float(ra["noise_min"]), float(ra["noise_max"]), float(ra["radian"])
+    it_r, it_p = iter(u_rot), iter(u_pv)
+
+    def rnd():
+        return -r + next(it_r) * (r - (-r))
+
+    def pose_vel():   # AddNoisePoseVel (KinCharacter.cpp:354-366)
+        if lo == 0 and hi == 0:
+            return
+        n = len(pose)
+        pose[:] = pose + np.array([lo + next(it_p) * (hi - lo) for _ in range(n)])
+        vel[:] = vel + np.array([lo + next(it_p) * (hi - lo) for _ in range(n)])
+
+    def rotate():   # RandomRotatePoseVel (KinCharacter.cpp:367-470)
+        if r == 0:
+            return
+        a = rnd()
+        qy = np.array([math.cos(a / 2), 0.0, math.sin(a / 2), 0.0])   # AxisAngleToQuaternion((0,1,0), a)
+        q = qmul(qy, pose[3:7])   # cCharacter::RotateRoot: rot * root_rot, normalized
+        pose[3:7] = q / np.linalg.norm(q)
+        interp = float(ra["interp"])
+        vel[0:3] = interp * vel[0:3]   # GetRootVel / SetRootVel (gPosDim)
+        vel[3:7] = interp * vel[3:7]   # GetRootAngVel / SetRootAngVel (gRotDim = 4)
+        for jt in joints[1:]:
+            o, sz = jt["offset"], jt["size"]
+            vel[o:o + sz] = interp * vel[o:o + sz]
+        for j in range(1, len(joints)):
+            o, t = joints[j]["offset"], joints[j]["type"]
+            if t == 0:
+                if j not in KNEES or ra["knee_rot"]:
+                    pose[o] = pose[o] + rnd()
+            elif t == 4 and j not in HIPS_ANKLES:
+                ps, th, ph = rnd(), rnd(), rnd()
+                qr = euler_to_quat(ps, th, ph)
+                pose[o:o + 4] = qmul(qr, pose[o:o + 4])
+                if ra["rot_vel_w_pose"]:
+                    vel[o:o + 4] = qmul(qr, vel[o:o + 4])
+        if ra["vel_noise"]:
+            ps, th, ph = rnd(), rnd(), rnd()
+            vel[3:7] = qmul(euler_to_quat(ps, th, ph), vel[3:7])
+            for j in range(1, len(joints)):
+                o, t = joints[j]["offset"], joints[j]["type"]
+                if t == 0:
+                    if not (j == 4 or j != 10) or ra["knee_rot"]:
+                        vel[o] = vel[o] + rnd()
+                elif t == 4 and j not in HIPS_ANKLES:
+                    ps, th, ph = rnd(), rnd(), rnd()
+                    vel[o:o + 4] = qmul(euler_to_quat(ps, th, ph), vel[o:o + 4])
+        pose[3:7] = pose[3:7] / np.linalg.norm(pose[3:7])   # KinTree::PostProcessPose
+        for jt in joints[1:]:
+            if jt["type"] == 4:
+                o = jt["offset"]
+                pose[o:o + 4] = pose[o:o + 4] / np.linalg.norm(pose[o:o + 4])
+
+    if ra["noise_bef_rot"]:
+        pose_vel()
+        rotate()
+    else:
+        rotate()
+        pose_vel()
+    return pose, vel
+
+
+def noise_draws(joints, ra):
+    """(uniforms RandomRotatePoseVel consumes, uniforms AddNoisePoseVel consumes) for reset_args ra."""
+    nr = 0
+    if float(ra["radian"]) != 0:
+        nr = 1
+        for j in range(1, len(joints)):
+            t = joints[j]["type"]
+            if t == 0:
+                nr += int(j not in KNEES or bool(ra["knee_rot"]))
+            elif t == 4 and j not in HIPS_ANKLES:
+                nr += 3
+        if ra["vel_noise"]:
+            nr += 3
+            for j in range(1, len(joints)):
+                t = joints[j]["type"]
+                if t == 0:
+                    nr += int((not (j == 4 or j != 10)) or bool(ra["knee_rot"]))
+                elif t == 4 and j not in HIPS_ANKLES:
+                    nr += 3
+    D = sum(j["size"] for j in joints)
+    npv = 0 if float(ra["noise_min"]) == 0 and float(ra["noise_max"]) == 0 else 2 * D
+    return nr, npv
+
+
 def reset_state(joints, bodies, motion, time, record_world_root_pos=False, record_world_root_rot=True,
-                record_all_world=False, ground_pad=0.001, resolve=True):
+                record_all_world=False, ground_pad=0.001, resolve=True, noise=None, u_rot=(), u_pv=()):
     """The 226-d state SimEnv.reset records after reset_time(time); `resolve` = reset_args'
-    'resolve' (SceneSimChar::ResetSceneTime, scenes/SceneSimChar.cpp:714-716)."""
+    'resolve' (SceneSimChar::ResetSceneTime, scenes/SceneSimChar.cpp:714-716); `noise` = the
+    reset_args of AddNoise with its injected uniforms u_rot / u_pv (add_noise), applied to the
+    kinematic pose / velocity before the placement and the ground resolve
+    (SceneSimChar.cpp:699-716: ResetCharactersTime, then InitCharacterPos, then resolve)."""
     pose = motion.pose(time)
     vel = motion.vel(time)
+    if noise is not None:
+        pose, vel = add_noise(joints, pose, vel, noise, u_rot, u_pv)
     pose[0] = 0.0   # SetCharRandPlacement on the plane: root x, z -> 0 (y kept)
     pose[2] = 0.0
     R, o, w, v = forward_kinematics(joints, pose, vel)

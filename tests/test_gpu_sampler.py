@@ -264,4 +264,4 @@ def test_sample_points_takes_mjrl_policy(setup):
         np.testing.assert_array_equal(pa["actions"], pb["actions"])
         np.testing.assert_array_equal(pa["agent_infos"]["log_std"], pb["agent_infos"]["log_std"])
     with pytest.raises(ValueError):
-        amx.sample_points(env, pol, num_to_collect=10, base_seed=2 ** 32, num_workers=1)
+        amx.sample_points(env, pol, num_to_collect=10, base_seed=2 ** 32, num_workers=2)  # worker 1: seeds >= 2**32

@@ -25,7 +25,7 @@ for x in rows:
     k = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
     agg[k][0] += 1
     agg[k][1] += d
-    if re.search(r"k_gemm_(nt|x6|h3)<[01],", name):
+    if re.search(r"k_gemm_(nt|x6|h3|lb)<[01],", name):
         gemm.append(d)
 span = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1000
 tot = sum(v[1] for v in agg.values())
