@@ -17,6 +17,25 @@ _HEADER = os.path.join(_build.INCLUDE, "amx_hip.h")
 c_int, c_ll, c_dbl, c_flt, c_u64, c_u32, vp = C.c_int, C.c_longlong, C.c_double, C.c_float, C.c_uint64, C.c_uint32, C.c_void_p
 ip = C.POINTER(C.c_int)
 
+
+class ResetNoise(C.Structure):
+    """amx_reset_noise: SimEnv reset_args' AddNoise options (run.py:113-117)."""
+    _fields_ = [("noise_bef_rot", C.c_int), ("noise_min", C.c_double), ("noise_max", C.c_double),
+                ("radian", C.c_double), ("rot_vel_w_pose", C.c_int), ("vel_noise", C.c_int),
+                ("interp", C.c_double), ("knee_rot", C.c_int)]
+
+    @classmethod
+    def from_reset_args(cls, ra: dict) -> "ResetNoise | None":
+        """None when reset_args add no noise (radian 0 and noise_min = noise_max = 0)."""
+        if float(ra["radian"]) == 0 and float(ra["noise_min"]) == 0 and float(ra["noise_max"]) == 0:
+            return None
+        return cls(int(bool(ra["noise_bef_rot"])), float(ra["noise_min"]), float(ra["noise_max"]),
+                   float(ra["radian"]), int(bool(ra["rot_vel_w_pose"])), int(bool(ra["vel_noise"])),
+                   float(ra["interp"]), int(bool(ra["knee_rot"])))
+
+
+AMX_NOISE_ROT_SLOTS = 48
+
 # name -> (restype, argtypes); must match include/amx_hip.h exactly.
 SIGNATURES = {
     "amx_create": (vp, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
@@ -55,6 +74,9 @@ SIGNATURES = {
     "amx_set_motion": (c_int, [vp, vp, c_ll]),
     "amx_motion_duration": (c_dbl, [vp]),
     "amx_motion_states": (c_int, [vp, vp, c_int, c_int, vp, c_ll, vp]),
+    "amx_motion_states_noise": (c_int, [vp, vp, c_int, c_int, vp, vp, c_ll, c_u64, vp, c_ll, vp]),
+    "amx_reset_lanes_motion_noise": (c_int, [vp, vp, vp, c_u64, c_dbl, c_int, vp, vp, c_ll, vp, vp, vp, vp, vp, vp,
+                                             c_int, vp]),
     "amx_reset_lanes_motion": (c_int, [vp, vp, vp, c_u64, c_dbl, c_int, vp, vp, vp, vp, vp, vp, c_int, vp]),
     "amx_amp_obs_size": (c_int, [vp]),
     "amx_state_amp_obs": (c_int, [vp, vp, vp, c_ll, c_int, c_int, vp, c_ll, vp]),

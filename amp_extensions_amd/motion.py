@@ -15,6 +15,7 @@ positions + tangent-normal rotations + linear/angular velocities, humanoid3d: 22
 """
 from __future__ import annotations
 
+import ctypes as C
 import json
 import math
 import os
@@ -215,12 +216,23 @@ class ReferenceMotion:
         """DeepMimicEnv.get_motion_length (SimEnv's time_max, sim_env.py:77)."""
         return self.duration
 
-    def states(self, times) -> torch.Tensor:
-        """[B, S] float64 device states at the given motion times."""
+    def states(self, times, reset_args: dict | None = None, draws: torch.Tensor | None = None,
+               seed: int = 0) -> torch.Tensor:
+        """[B, S] float64 device states at the given motion times.  `reset_args` with noise
+        (noise_min / noise_max / radian, ...): cKinCharacter::AddNoise applied before the
+        placement and the ground resolve, its uniforms from Philox(seed; lane) or `draws`
+        ([B, >= 48 + 2 D] float64 in [0, 1): RandomRotatePoseVel's draws first, AddNoisePoseVel's
+        from column 48)."""
         c = self.ctx
         t = torch.as_tensor(times, dtype=torch.float64).reshape(-1).to(c.device).contiguous()
         out = torch.empty(t.numel(), self.S, dtype=torch.float64, device=c.device)
-        N.check(c.lib.amx_motion_states(c.h, t.data_ptr(), t.numel(), self.kernel_flags, out.data_ptr(), self.S,
-                                        c.stream),
-                "amx_motion_states")
+        noise = N.ResetNoise.from_reset_args(reset_args) if reset_args is not None else None
+        if draws is not None:
+            draws = torch.as_tensor(draws, dtype=torch.float64).to(c.device).contiguous()
+        N.check(c.lib.amx_motion_states_noise(c.h, t.data_ptr(), t.numel(), self.kernel_flags,
+                                              None if noise is None else C.byref(noise),
+                                              None if draws is None else draws.data_ptr(),
+                                              0 if draws is None else draws.stride(0), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                              out.data_ptr(), self.S, c.stream),
+                "amx_motion_states_noise")
         return out

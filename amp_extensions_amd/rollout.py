@@ -24,6 +24,7 @@ member 1 (sim_env.py:118, 282-283).
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
 
 import numpy as np
@@ -153,15 +154,28 @@ class RolloutEngine:
         """SimEnv.reset on every lane (sim_env.py:270-285)."""
         self.reset_lanes(None, rows)
 
+    def set_reset_noise(self, reset_args: dict | None) -> None:
+        """SimEnv reset_args' AddNoise options for this engine's motion resets (run.py:113-117):
+        None or no noise -> the plain reset.  Needs a ReferenceMotion reset source (the noise
+        perturbs the kinematic pose and velocity; a reset-state table has neither)."""
+        noise = N.ResetNoise.from_reset_args(reset_args) if reset_args is not None else None
+        if noise is not None and self.motion is None:
+            raise NotImplementedError("reset noise needs a ReferenceMotion reset source (AddNoise perturbs the "
+                                      "kinematic pose / velocity, which a reset-state table does not hold)")
+        self._reset_noise = noise
+
     def _reset_motion(self, mask, times, src, dst, t_out) -> None:
         c = self.ctx
-        N.check(c.lib.amx_reset_lanes_motion(c.h, None if mask is None else mask.data_ptr(),
-                                             None if times is None else times.data_ptr(), self.seed,
-                                             float(self.reset_time_max), self.motion.kernel_flags,
-                                             src.data_ptr(), dst.data_ptr(),
-                                             self.num_steps.data_ptr(), self.model_idx.data_ptr(),
-                                             self.reset_count.data_ptr(), None if t_out is None else t_out.data_ptr(),
-                                             self.B, c.stream), "amx_reset_lanes_motion")
+        noise = getattr(self, "_reset_noise", None)
+        N.check(c.lib.amx_reset_lanes_motion_noise(c.h, None if mask is None else mask.data_ptr(),
+                                                   None if times is None else times.data_ptr(), self.seed,
+                                                   float(self.reset_time_max), self.motion.kernel_flags,
+                                                   None if noise is None else C.byref(noise), None, 0,
+                                                   src.data_ptr(), dst.data_ptr(),
+                                                   self.num_steps.data_ptr(), self.model_idx.data_ptr(),
+                                                   self.reset_count.data_ptr(),
+                                                   None if t_out is None else t_out.data_ptr(),
+                                                   self.B, c.stream), "amx_reset_lanes_motion_noise")
 
     def reset_lanes(self, mask: torch.Tensor | None, rows: torch.Tensor | None = None) -> None:
         """SimEnv.reset on the lanes with mask != 0 (all lanes when mask is None); the lane

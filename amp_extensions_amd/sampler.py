@@ -129,6 +129,7 @@ def _sampler_engine(env, lanes: int, K: int, policy, time_max: float) -> Rollout
         reset_source = src.motion if src.motion is not None else src.table
         eng = RolloutEngine(src.ens, reset_source, lanes=lanes, term=src.term, policy=policy, seed=src.seed,
                             max_steps=K, auto_reset=False, record_means=True)
+        eng._reset_noise = getattr(src, "_reset_noise", None)  # the env's reset_args noise (AddNoise)
         # (0 = the whole clip; a table source is already cut to the window's rows)
         if src.motion is not None and time_max != src.motion.get_motion_length():
             eng.reset_time_max = float(time_max)

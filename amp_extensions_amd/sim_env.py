@@ -126,18 +126,20 @@ def motion_from_args(ctx: AmxContext, deepmimic_args: str, resolve: bool = True)
 
 def check_reset_args(reset_args: dict | None) -> dict:
     """reset_args with the reference's defaults filled in.  The noise options (noise_min /
-    noise_max, radian) draw from DeepMimicCore's C++ RNG in cKinCharacter::AddNoise
-    (anim/KinCharacter.cpp:340-400): that stream cannot be reproduced, so they are refused
-    rather than approximated.  `interp` and the flags that only shape the rotation noise
-    (rot_vel_w_pose, vel_noise, knee_rot, noise_bef_rot) act only inside RandomRotatePoseVel,
-    which returns before touching the state when radian == 0 (KinCharacter.cpp:360-364): with
-    the noise off they are exact no-ops, as in the reference."""
+    noise_max, radian, rot_vel_w_pose, vel_noise, interp, knee_rot, noise_bef_rot) are
+    cKinCharacter::AddNoise (anim/KinCharacter.cpp:340-470), applied on the device to the
+    kinematic pose / velocity of every motion reset (csrc/amx_motion.hip add_noise).  The
+    reference draws them from DeepMimicCore's process-global std::default_random_engine, which
+    cannot be reproduced: the device draws come from Philox(seed; lane, reset #) -- same
+    distribution and transform, another stream.  `interp` and the rotation-noise
+    flags act only inside RandomRotatePoseVel, which returns before touching the state when
+    radian == 0 (KinCharacter.cpp:367-371)."""
     ra = dict(DEFAULT_RESET_ARGS)
     ra.update(reset_args or {})
-    if float(ra["noise_min"]) != 0.0 or float(ra["noise_max"]) != 0.0 or float(ra["radian"]) != 0.0:
-        raise NotImplementedError(
-            "reset_args noise (noise_min/noise_max/radian) is drawn from DeepMimicCore's C++ RNG "
-            "(cKinCharacter::AddNoise, anim/KinCharacter.cpp:340-400), which cannot be reproduced on the device")
+    for k in ("noise_min", "noise_max", "radian", "interp"):
+        v = float(ra[k])
+        if v != v:
+            raise ValueError(f"reset_args[{k!r}] is NaN")
     return ra
 
 
@@ -175,6 +177,7 @@ class SimEnv(_EnvBase):
             reset_table = motion_from_args(dev_ens.ctx, deepmimic_args, resolve=bool(self.reset_args["resolve"]))
         self._eng = RolloutEngine(dev_ens, reset_table, lanes=1, term=self.term, seed=0, max_steps=1,
                                   auto_reset=False)
+        self._eng.set_reset_noise(self.reset_args)  # AddNoise (raises for a table source with noise)
         c = self._eng.ctx
         self.state_size, self.action_size = c.S, c.A
         self.observation_space = Box([-np.inf] * c.S, [np.inf] * c.S)
@@ -195,8 +198,11 @@ class SimEnv(_EnvBase):
         self.seed_env(seed)
 
     def seed_env(self, seed=None):
-        """sim_env.py:122-132 (gym 0.26 seeding: Generator(PCG64(SeedSequence(seed))))."""
+        """sim_env.py:122-132 (gym 0.26 seeding: Generator(PCG64(SeedSequence(seed)))); the seed
+        also keys the device reset noise's Philox stream (AddNoise, check_reset_args)."""
         self.np_random = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+        if hasattr(self, "_eng"):
+            self._eng.seed = int(seed or 0) & 0xFFFFFFFFFFFFFFFF
 
     def get_observation(self):
         return self.ob
@@ -265,7 +271,7 @@ class BatchedSimEnv:
                  reset_args=None):
         """`reset_table` None: the arg file's character + motion (as SimEnv); reset_args as
         SimEnv's (custom_time / time_max bound the lanes' Philox reset times, or the table rows
-        drawn; noise raises NotImplementedError)."""
+        drawn; the noise options perturb every motion reset, check_reset_args)."""
         self.reset_args = check_reset_args(reset_args)
         dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
         self.term = termination_from_args(deepmimic_args, horizon, enable_velocity_check)
@@ -285,6 +291,7 @@ class BatchedSimEnv:
             reset_table = torch.as_tensor(reset_table)[:rows]
         self.engine = RolloutEngine(dev_ens, reset_table, lanes=lanes, term=self.term, policy=policy, cost=cost,
                                     seed=seed, max_steps=max_steps, record_means=record_means)
+        self.engine.set_reset_noise(self.reset_args)
         if custom and self.engine.motion is not None:
             self.engine.reset_time_max = float(self.reset_args["time_max"])
         self.num_envs = lanes

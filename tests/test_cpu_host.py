@@ -212,8 +212,8 @@ def test_deepmimic_arg_file_parsing_and_reset_args(tmp_path):
     """SimEnv's host side of the run.py construction (sim_env.py:76-99): DeepMimic's ArgParser
     rules (comment lines and tokens skipped, the first occurrence of a key wins, data paths
     resolved from the package root), the ctrl flags and BodyDefs read into the termination
-    config, and reset_args: defaults filled in, noise refused (C++ RNG stream), interp and the
-    rotation-noise flags accepted as the no-ops they are with radian == 0."""
+    config, and reset_args: defaults filled in, the AddNoise options accepted (applied on the
+    device, tests/test_gpu_motion.py), NaN amounts refused."""
     from amp_extensions_amd import sim_env as SE
     from test_gpu_simenv_dropin import RUN_PY_RESET_ARGS, write_deepmimic_tree
     args = write_deepmimic_tree(str(tmp_path))
@@ -229,9 +229,10 @@ def test_deepmimic_arg_file_parsing_and_reset_args(tmp_path):
     assert ra["resolve"] is True and ra["time_max"] == 0.5 and ra["radian"] == 0
     assert SE.check_reset_args(RUN_PY_RESET_ARGS)["interp"] == 1.0
     assert SE.check_reset_args(dict(RUN_PY_RESET_ARGS, vel_noise=True, knee_rot=True, interp=0.3))
-    for bad in ({"noise_max": 0.1}, {"noise_min": -0.1}, {"radian": 0.2}):
-        with pytest.raises(NotImplementedError):
-            SE.check_reset_args(dict(RUN_PY_RESET_ARGS, **bad))
+    ra = SE.check_reset_args(dict(RUN_PY_RESET_ARGS, noise_max=0.1, radian=0.2))  # AddNoise (device)
+    assert ra["noise_max"] == 0.1 and ra["radian"] == 0.2
+    with pytest.raises(ValueError):
+        SE.check_reset_args(dict(RUN_PY_RESET_ARGS, radian=float("nan")))
     with pytest.raises(FileNotFoundError):
         SE.motion_from_args(None, str(tmp_path / "missing_args.txt"))
 

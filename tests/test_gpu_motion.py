@@ -152,3 +152,88 @@ def test_state_amp_obs_recovers_the_pose_features(setup):
         ref = np.stack(ref)
         err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
         assert err.max() <= 1e-9, (local, err.max(), np.unravel_index(err.argmax(), err.shape))
+
+
+NOISE_BASE = dict(custom_time=False, time_min=0, time_max=0, resolve=True, noise_bef_rot=False, noise_min=0,
+                  noise_max=0, radian=0, rot_vel_w_pose=False, vel_noise=False, interp=1.0, knee_rot=False)
+
+
+@pytest.mark.parametrize("opts", [dict(radian=0.2), dict(noise_min=-0.05, noise_max=0.08),
+                                  dict(radian=0.25, noise_min=-0.03, noise_max=0.03, rot_vel_w_pose=True,
+                                       vel_noise=True, interp=0.3),
+                                  dict(radian=0.15, noise_min=-0.02, noise_max=0.04, noise_bef_rot=True,
+                                       knee_rot=True, vel_noise=True, interp=0.0),
+                                  dict(radian=3.0, vel_noise=True, rot_vel_w_pose=True, knee_rot=True)])
+def test_reset_noise_with_injected_draws_matches_oracle(setup, opts):
+    """SimEnv reset_args noise = cKinCharacter::AddNoise (anim/KinCharacter.cpp:340-470) before the
+    placement and the ground resolve: with the same uniforms injected on both sides
+    (RandomRotatePoseVel's draws at [0, 48), AddNoisePoseVel's after them) the device states equal
+    the oracle's add_noise + reset_state at 1e-10 for every option combination."""
+    amx, ctx, rm, J, B, M = setup
+    ra = dict(NOISE_BASE, **opts)
+    nr, npv = D.noise_draws(J, ra)
+    assert nr <= 48
+    Dof = sum(j["size"] for j in J)
+    rs = np.random.RandomState(7)
+    L = 64
+    times = rs.uniform(0, M.duration, L)
+    draws = rs.rand(L, 48 + 2 * Dof)
+    got = rm.states(times, reset_args=ra, draws=torch.from_numpy(draws)).cpu().numpy()
+    ref = np.stack([D.reset_state(J, B, M, float(times[i]), noise=ra, u_rot=draws[i, :nr], u_pv=draws[i, 48:48 + npv])
+                    for i in range(L)])
+    err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref))
+    assert err.max() <= 1e-10, (err.max(), np.unravel_index(err.argmax(), err.shape))
+    plain = np.stack([D.reset_state(J, B, M, float(t)) for t in times])
+    assert np.abs(ref - plain).max() > 1e-3  # the noise does move the state
+
+
+def test_reset_noise_philox_stream(setup):
+    """Without injected draws the uniforms come from Philox(seed; lane, reset#): repeatable,
+    seed-dependent, finite, and zero amounts give the plain states bit for bit."""
+    amx, ctx, rm, J, B, M = setup
+    ra = dict(NOISE_BASE, radian=0.2, noise_min=-0.05, noise_max=0.05, vel_noise=True)
+    times = np.linspace(0.05, M.duration - 0.05, 40)
+    a = rm.states(times, reset_args=ra, seed=11)
+    b = rm.states(times, reset_args=ra, seed=11)
+    c = rm.states(times, reset_args=ra, seed=12)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and not torch.equal(a, c) and torch.isfinite(a).all()
+    assert torch.equal(rm.states(times, reset_args=NOISE_BASE), rm.states(times))
+
+
+def test_simenv_with_reset_noise_runs(setup):
+    """SimEnv(..., reset_args={'noise_max': 0.1, 'radian': 0.2, ...}) constructs and runs: its
+    resets carry the noise (states differ from the noise-free reset at the same drawn time),
+    BatchedSimEnv and sample_points too; a reset-state table with noise is refused (AddNoise
+    perturbs a pose / velocity the table does not hold)."""
+    amx, ctx, rm, J, B, M = setup
+    from oracle import milo_ref as R
+    S, A = 226, 28
+    rs = np.random.RandomState(3)
+    s = 0.5 * rs.randn(2048, S)
+    s[:, 0] = rs.uniform(0.8, 0.95, 2048)
+    a = rs.randn(2048, A)
+    norms = R.get_transformations(*[torch.from_numpy(x).float() for x in (s, a, s + 0.01 * rs.randn(2048, S))])
+    ens = amx.DeviceEnsemble(ctx, R.init_ensemble_weights(S, A, [128] * 2, 4, 100), norms)
+    ra = dict(NOISE_BASE, noise_min=-0.1, noise_max=0.1, radian=0.2, vel_noise=True, interp=1.0)
+    env = amx.SimEnv(ens, reset_table=rm, reset_args=ra, seed=5)
+    env0 = amx.SimEnv(ens, reset_table=rm, reset_args=NOISE_BASE, seed=5)
+    for _ in range(5):
+        o, o0 = env.reset(), env0.reset()
+        assert env.last_reset_time == env0.last_reset_time and np.abs(o - o0).max() > 1e-3
+        for _ in range(10):
+            o, r, d, info = env.step(np.zeros(A))
+            assert np.isfinite(o).all()
+            if d:
+                break
+    benv = amx.BatchedSimEnv(ens, rm, lanes=64, reset_args=ra, seed=2, max_steps=4)
+    benv.reset()
+    for _ in range(4):
+        benv.step(torch.zeros(64, A, dtype=torch.float64, device=DEV))
+    assert torch.isfinite(benv.engine.obs[:4]).all()
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100)
+    pol = amx.DevicePolicy(ctx, pw, log_std)
+    paths = amx.sample_points(benv, pol, num_to_collect=60, base_seed=1, num_workers=2)
+    assert sum(len(p["rewards"]) for p in paths) >= 60
+    with pytest.raises(NotImplementedError):
+        amx.BatchedSimEnv(ens, s[:64], lanes=8, reset_args=ra)

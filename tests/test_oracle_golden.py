@@ -230,3 +230,55 @@ def test_g11_npg_update(golden):
     np.testing.assert_array_equal(out["npg"], g["npg"])
     np.testing.assert_array_equal(out["params1"], g["params1"])
     assert out["surr_after"] == float(g["surr_after"])
+
+
+def test_oracle_reset_noise_structure():
+    """oracle.deepmimic_ref.add_noise (cKinCharacter::AddNoise, KinCharacter.cpp:340-470) on the
+    humanoid3d character: the draw counts per option, the no-noise identity, noise_bef_rot's
+    order, the hip / ankle / knee exclusions (their pose parameters untouched by the rotation
+    noise), interp scaling of every velocity, normalised quaternions, and EulerToQuaternion's
+    known values (zero angles -> identity; a pure x rotation -> its axis-angle quaternion).
+    Parity with the C++ core itself is unpinned (no Bullet/Eigen/GL here)."""
+    import json
+    import math
+    from oracle import deepmimic_ref as DR
+    from amp_extensions_amd.motion import ReferenceMotion
+    z = np.load(ReferenceMotion.DEFAULT_BUNDLE, allow_pickle=False)
+    J, bodies, D = DR.load_character(json.loads(str(z["character_json"])))
+    M = DR.Motion({"Loop": str(z["loop"]), "Frames": z["frames"].tolist()}, J)
+    base = dict(noise_bef_rot=False, noise_min=0, noise_max=0, radian=0, rot_vel_w_pose=False, vel_noise=False,
+                interp=1.0, knee_rot=False)
+    pose, vel = M.pose(0.41), M.vel(0.41)
+    assert DR.noise_draws(J, base) == (0, 0)
+    p0, v0 = DR.add_noise(J, pose, vel, base, [], [])
+    np.testing.assert_array_equal(p0, pose)
+    np.testing.assert_array_equal(v0, vel)
+    ra = dict(base, radian=0.3)
+    nr, npv = DR.noise_draws(J, ra)
+    # root yaw + revolute elbows (7, 13) + spherical chest, neck, shoulders (1, 2, 6, 12) x 3
+    assert (nr, npv) == (1 + 2 + 4 * 3, 0)
+    assert DR.noise_draws(J, dict(ra, knee_rot=True))[0] == nr + 2
+    assert DR.noise_draws(J, dict(ra, vel_noise=True))[0] == nr + 3 + 1 + 4 * 3  # only joint 10's vel
+    assert DR.noise_draws(J, dict(base, noise_min=-0.1, noise_max=0.1)) == (0, 2 * D)
+    rs = np.random.RandomState(1)
+    u = rs.rand(nr)
+    p1, v1 = DR.add_noise(J, pose, vel, dict(ra, interp=0.5), u, [])
+    for j in (3, 4, 5, 9, 10, 11):   # hips, knees, ankles untouched by the pose rotation noise
+        o, s = J[j]["offset"], J[j]["size"]
+        np.testing.assert_allclose(p1[o:o + s], pose[o:o + s] / (np.linalg.norm(pose[o:o + s]) if s == 4 else 1.0),
+                                   rtol=0, atol=1e-15)
+    np.testing.assert_allclose(v1, 0.5 * vel, rtol=0, atol=0)
+    for j in range(len(J)):
+        if J[j]["type"] == 4:
+            o = J[j]["offset"]
+            assert abs(np.linalg.norm(p1[o:o + 4]) - 1.0) < 1e-14
+    assert abs(np.linalg.norm(p1[3:7]) - 1.0) < 1e-14
+    np.testing.assert_allclose(DR.euler_to_quat(0.0, 0.0, 0.0), [1, 0, 0, 0], atol=0)
+    np.testing.assert_allclose(DR.euler_to_quat(0.4, 0.0, 0.0), [math.cos(0.2), math.sin(0.2), 0, 0], atol=1e-15)
+    # noise_bef_rot changes the order of the two perturbations (different results, same draws)
+    ra2 = dict(base, radian=0.3, noise_min=-0.05, noise_max=0.05)
+    nr2, npv2 = DR.noise_draws(J, ra2)
+    ur, up = rs.rand(nr2), rs.rand(npv2)
+    a, _ = DR.add_noise(J, pose, vel, ra2, ur, up)
+    b, _ = DR.add_noise(J, pose, vel, dict(ra2, noise_bef_rot=True), ur, up)
+    assert np.abs(a - b).max() > 1e-6
