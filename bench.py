@@ -202,6 +202,8 @@ def cpu_baseline_leg(S, A, args):
                    f"{best['relabel_s']:.2f}s; median of 3 end-to-end runs (the relabel timed on the same "
                    f"fixed sample each time)"),
         "end_to_end_runs": e2e,
+        "sampler_s_runs": [round(r["sampler_s"], 3) for r in finals],
+        "relabel_s_runs": [round(r["relabel_s"], 3) for r in finals],
         "spread": round((max(e2e) - min(e2e)) / max(e2e), 4),
         "sweep_sampler_steps_per_s": pts,
         "best_workers": best_w, "relabel_threads": best["relabel_threads"],
