@@ -60,7 +60,7 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 }
 
 // H3_EXP (diagnostic builds, bits): 1 = the split schedule's K-loop global loads left out (stale
-// tiles), 2 = its A limb split left out (raw bits published)
+// tiles), 2 = the A limb split left out (raw bits published)
 #ifndef H3_EXP
 #define H3_EXP 0
 #endif
@@ -862,10 +862,15 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     for (int j = 0; j < VA; ++j)
       if (a_ok[j]) {
         f32x4 x = ra[0][j];
+#if H3_EXP & 2
+        const u32x4 xb = __builtin_bit_cast(u32x4, x);
+        const u32x2 l0 = {xb[0], xb[1]}, l1 = {xb[2], xb[3]};
+#else
 #pragma unroll
         for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ldexpf(x[i], a_sh[j]);
         u32x2 l0, l1;
         split2(x, l0, l1);
+#endif
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
         *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
       }

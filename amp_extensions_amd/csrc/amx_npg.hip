@@ -89,6 +89,7 @@ struct NpgArgs {
   const float* vec;          // FVP: tangent; EVAL: new parameters
   double* partials;          // VPG/FVP: [blocks][P]; EVAL: [blocks][2]
   int P;
+  const double* gate;        // optional CG state {rdotr, live}: live == 0 -> the pass is a no-op
 };
 
 struct Lay {  // offsets into the packed parameter vector
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   constexpr int NI = NRB * 2 * NMAT;           // layer-1 / layer-2 tiles per chunk
   constexpr int MI = (NI + NW - 1) / NW;       // ... per wave
   extern __shared__ __attribute__((aligned(16))) float sm[];
+  if (a.gate && a.gate[1] == 0.0) return;  // CG has stopped (cg_solve.py:19-20): no product needed
   const Geo g(a.S, a.A);
   const Lay L(a.S, a.A);
   const int S = g.S, A = g.A;
@@ -727,18 +729,20 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
 // out[c] = sum_b partials[b][c] in a fixed order (deterministic): stage 1 sums runs of RB
 // consecutive blocks per column (grid.y = run), stage 2 sums the runs in order.
 constexpr int RB = 16;
-__global__ void k_npg_reduce1(const double* __restrict__ part, int nb, int P, double* __restrict__ mid) {
+__global__ void k_npg_reduce1(const double* __restrict__ part, int nb, int P, double* __restrict__ mid,
+                              const double* __restrict__ gate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= P) return;
+  if (c >= P || (gate && gate[1] == 0.0)) return;
   const int b0 = blockIdx.y * RB, b1 = min(nb, b0 + RB);
   double s = 0.0;
 #pragma unroll 8
   for (int b = b0; b < b1; ++b) s += part[(long long)b * P + c];  // 8 loads in flight, same add order
   mid[(long long)blockIdx.y * P + c] = s;
 }
-__global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, double* __restrict__ out) {
+__global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, double* __restrict__ out,
+                              const double* __restrict__ gate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= P) return;
+  if (c >= P || (gate && gate[1] == 0.0)) return;
   double s = 0.0;
 #pragma unroll 8
   for (int r = 0; r < nr; ++r) s += mid[(long long)r * P + c];
@@ -857,6 +861,14 @@ extern "C" long long amx_npg_param_count(int S, int A) {
 extern "C" int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
                             const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
                             const float* vec, int rows_per_block, double* partials, void* stream) {
+  return amx_npg_pass_gated(ctx, mode, N, obs, obs_dtype, ldo, act, act_dtype, lda, adv, theta, vec, rows_per_block,
+                            partials, nullptr, stream);
+}
+
+extern "C" int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
+                                  const void* act, int act_dtype, long long lda, const double* adv,
+                                  const float* theta, const float* vec, int rows_per_block, double* partials,
+                                  const double* gate, void* stream) {
   AMX_CHECK_ARG(ctx, "amx_npg_pass: null ctx");
   const int S = ctx->S, A = ctx->A;
   AMX_CHECK_ARG(mode >= NPG_VPG && mode <= NPG_EVAL, "amx_npg_pass: mode=%d", mode);
@@ -874,7 +886,7 @@ extern "C" int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int 
   a.mode = mode; a.N = N; a.S = S; a.A = A; a.rows_per_block = rows_per_block;
   a.obs = obs; a.ldo = ldo;
   a.act = act; a.lda = lda;
-  a.adv = adv; a.theta = theta; a.vec = vec; a.partials = partials;
+  a.adv = adv; a.theta = theta; a.vec = vec; a.partials = partials; a.gate = gate;
   a.P = (int)amx_npg_param_count(S, A);
   const bool of64 = obs_dtype == AMX_IN_F64, af64 = act_dtype == AMX_IN_F64;
   const size_t lds = npg_lds_bytes(S, A, mode, RC0);
@@ -908,11 +920,16 @@ extern "C" int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int 
 }
 
 extern "C" int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, void* stream) {
+  return amx_npg_reduce_gated(ctx, partials, blocks, P, out, nullptr, stream);
+}
+
+extern "C" int amx_npg_reduce_gated(amx_ctx* ctx, const double* partials, int blocks, int P, double* out,
+                                    const double* gate, void* stream) {
   AMX_CHECK_ARG(ctx && partials && out && blocks > 0 && P > 0, "amx_npg_reduce: bad arguments");
   const int runs = (blocks + RB - 1) / RB;
   if (runs == 1) {
     hipLaunchKernelGGL(k_npg_reduce2, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, partials, blocks, P,
-                       out);
+                       out, gate);
     AMX_CHECK_LAUNCH();
     return AMX_OK;
   }
@@ -929,10 +946,10 @@ extern "C" int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, 
     ctx->npg_scratch_bytes = need;
   }
   hipLaunchKernelGGL(k_npg_reduce1, dim3((P + 255) / 256, runs), dim3(256), 0, (hipStream_t)stream, partials, blocks,
-                     P, ctx->d_npg_scratch);
+                     P, ctx->d_npg_scratch, gate);
   AMX_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_npg_reduce2, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, ctx->d_npg_scratch,
-                     runs, P, out);
+                     runs, P, out, gate);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

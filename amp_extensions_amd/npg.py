@@ -115,7 +115,7 @@ class DeviceNPG:
         # one block per CU (the pass kernel holds ~140 KB of LDS): one wave of blocks
         return max(32, int(math.ceil(n / 256 / 32)) * 32)
 
-    def _pass(self, mode, obs, act, adv, vec):
+    def _pass(self, mode, obs, act, adv, vec, gate=None):
         c = self.ctx
         n = obs.shape[0]
         rpb = self._rows_per_block(n)
@@ -127,12 +127,14 @@ class DeviceNPG:
             part = self._bufs[key] = torch.empty(nb, width, dtype=torch.float64, device=c.device)
         od = N.AMX_IN_F64 if obs.dtype == torch.float64 else N.AMX_IN_F32
         ad = N.AMX_IN_F64 if act.dtype == torch.float64 else N.AMX_IN_F32
-        N.check(c.lib.amx_npg_pass(c.h, mode, n, obs.data_ptr(), od, obs.stride(0), act.data_ptr(), ad, act.stride(0),
-                                   None if adv is None else adv.data_ptr(), self.theta.data_ptr(),
-                                   None if vec is None else vec.data_ptr(), rpb, part.data_ptr(), c.stream),
-                "amx_npg_pass")
+        g = None if gate is None else gate.data_ptr()
+        N.check(c.lib.amx_npg_pass_gated(c.h, mode, n, obs.data_ptr(), od, obs.stride(0), act.data_ptr(), ad,
+                                         act.stride(0), None if adv is None else adv.data_ptr(),
+                                         self.theta.data_ptr(), None if vec is None else vec.data_ptr(), rpb,
+                                         part.data_ptr(), g, c.stream), "amx_npg_pass")
         out = torch.empty(width, dtype=torch.float64, device=c.device)
-        N.check(c.lib.amx_npg_reduce(c.h, part.data_ptr(), nb, width, out.data_ptr(), c.stream), "amx_npg_reduce")
+        N.check(c.lib.amx_npg_reduce_gated(c.h, part.data_ptr(), nb, width, out.data_ptr(), g, c.stream),
+                "amx_npg_reduce")
         return out
 
     def _inputs(self, observations, actions, advantages=None):
@@ -181,7 +183,9 @@ class DeviceNPG:
         """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with
         NPG.HVP as the operator.  Each iteration is one Fisher-vector pass + reduce and one
         single-workgroup vector step (amx_npg_cg_step); the early stop is the step's device-side
-        `live` flag (a finished solve leaves x unchanged), so no host sync between iterations."""
+        `live` flag (a finished solve leaves x unchanged), so no host sync between iterations.
+        The FVP pass and its reduction read the same flag (amx_npg_pass_gated): after the stop
+        the remaining iterations are empty launches, not Fisher-vector products."""
         c = self.ctx
         P = self.P
         dev = c.device
@@ -193,7 +197,7 @@ class DeviceNPG:
         N.check(c.lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
                                       p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_init")
         for _ in range(self.cg_iters):
-            h = self._pass(NPG_FVP, obs, act, None, p32)
+            h = self._pass(NPG_FVP, obs, act, None, p32, gate=state)
             N.check(c.lib.amx_npg_cg_step(c.h, P, self.A, h.data_ptr(), curv.data_ptr(), self.damping,
                                           self.residual_tol, x.data_ptr(), r.data_ptr(), p.data_ptr(),
                                           p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_step")

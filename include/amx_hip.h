@@ -318,6 +318,15 @@ int amx_npg_pass(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, 
                  const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
                  const float* vec, int rows_per_block, double* partials, void* stream);
 int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, void* stream);
+/* The same with a gate: gate = the CG state of amx_npg_cg_init / _step ({rdotr, live}); with
+ * live == 0 the pass and the reduction return at once (every block reads the flag), so the FVP
+ * products of a solve that stopped early cost two empty launches, not a pass over the batch
+ * (cg_solve.py:19-20 breaks the loop there). */
+int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
+                       const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
+                       const float* vec, int rows_per_block, double* partials, const double* gate, void* stream);
+int amx_npg_reduce_gated(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, const double* gate,
+                         void* stream);
 
 /* The conjugate-gradient solve of NPG (mjrl/mjrl/utils/cg_solve.py:3-23) on the device, one
  * workgroup per call, fixed-order fp64 reductions, no host round trip between iterations.

@@ -168,6 +168,36 @@ def test_npg_device_cg_early_stop():
     assert not close(x10, x_ref, 1e-7)  # the stop mattered
 
 
+def test_npg_gated_fvp_pass_skips_after_stop():
+    """amx_npg_pass_gated / amx_npg_reduce_gated (the FVP products of cg_solve): with the CG
+    state's live flag 1 they equal the ungated pass bit for bit; with live 0 (the solve stopped,
+    cg_solve.py:19-20) neither the partials nor the output are written."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy, NPG_FVP
+    S, A, N = 197, 36, 1024
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    npg = make(S, A, pack_policy(layers, ls))
+    rs = np.random.RandomState(5)
+    o, a, _ = npg._inputs((0.5 * rs.randn(N, S)).astype(np.float32), rs.randn(N, A).astype(np.float32))
+    vec = torch.from_numpy(rs.randn(npg.P).astype(np.float32)).to(DEV)
+    h0 = npg._pass(NPG_FVP, o, a, None, vec)
+    live = torch.tensor([1.0, 1.0], dtype=torch.float64, device=DEV)
+    h1 = npg._pass(NPG_FVP, o, a, None, vec, gate=live)
+    assert torch.equal(h0, h1)
+    c, lib = npg.ctx, npg.ctx.lib
+    rpb = npg._rows_per_block(N)
+    nb = (N + rpb - 1) // rpb
+    part = torch.full((nb, npg.P), 7.0, dtype=torch.float64, device=DEV)
+    out = torch.full((npg.P,), 9.0, dtype=torch.float64, device=DEV)
+    dead = torch.tensor([1.0, 0.0], dtype=torch.float64, device=DEV)
+    assert lib.amx_npg_pass_gated(c.h, NPG_FVP, N, o.data_ptr(), 1, o.stride(0), a.data_ptr(), 1, a.stride(0), None,
+                                  npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(), dead.data_ptr(),
+                                  c.stream) == 0
+    assert lib.amx_npg_reduce_gated(c.h, part.data_ptr(), nb, npg.P, out.data_ptr(), dead.data_ptr(), c.stream) == 0
+    torch.cuda.synchronize()
+    assert bool((part == 7.0).all()) and bool((out == 9.0).all())
+
+
 def test_npg_pass_input_dtypes_bit_identical():
     """amx_npg_pass on fp64 and fp32 inputs (the fp64 C-ABI path: 16 layer-1 K-steps compiled; the
     fp32 path DeviceNPG takes: ceil(S / 16) rounded to 4 / 8 / 13 / 16) gives the same bits in all
