@@ -64,6 +64,13 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef H3_EXP
 #define H3_EXP 0
 #endif
+// RFF_TILE (A/B builds): 1 = the 128 x 256 16x16x32 split-schedule tile (H128x256) for the RFF
+// pass where it fills the CUs -- measured equal to the 128 x 128 tiles at 40 960 rows (95 us) and
+// 1 us slower at 20 480 (profiles/r04h_rff_ab.txt): both run the pass in ceil(2.5) = 3 rounds of
+// one CU's worth of tiles, so the default stays 0
+#ifndef RFF_TILE
+#define RFF_TILE 0
+#endif
 // RFF_EXP (diagnostic builds, tools/gemm_variant.sh): 1 = no cos, 2 = no phi store
 #ifndef RFF_EXP
 #define RFF_EXP 0
@@ -605,8 +612,10 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
   const int* wexp = a.w_exp + (long long)g * a.strideWexp;
   float* Cg = a.C + (long long)g * a.strideC;
   if constexpr (EPI == EPI_RFF) {  // the 32x32 path's RFF epilogue on the 16x16 accumulator layout
-    static_assert(TL::BM == 128 && TL::BN == 128 && TL::NT == 256, "RFF epilogue assumes the 128x128 tile");
-    constexpr int CLD = 128 + 4;
+    // 128 x 128 tiles of 256 threads or 128 x 256 tiles of 512: one column per thread, two halves
+    // of 64 rows (the 128-row block's partial sums: col_partials[row / 128][f])
+    constexpr int BN = TL::BN, CLD = BN + 4;
+    static_assert(TL::BM == 128 && (BN == 128 || BN == 256) && TL::NT == 2 * BN, "RFF epilogue tiles");
     // un-scale in place (exact powers of two) while sExp (in the stage area) is readable
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
@@ -630,10 +639,10 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           Cs[(lrow0 + m * 16 + 4 * lq + j) * CLD + wn * TL::WCOLS + n * 16 + lc] = acc[m][n][j];
-    const int t = threadIdx.x, c = t & 127, half = t >> 7;
+    const int t = threadIdx.x, c = t % BN, half = t / BN;
     const uint64_t vmask = row_valid_mask(a, tm * 128 + half * 64, 64);  // as the 32x32 path's epilogue
     __syncthreads();
-    const int col = tn * 128 + c;
+    const int col = tn * BN + c;
     const float bv = a.bias[col];
     double csum = 0.0;
 #pragma unroll 2
@@ -2020,6 +2029,9 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   if (K % 32 == 0) {
     // (at 40 960 rows the 128 x 128 tile is faster: 121 vs 145 us under the profiler)
     if ((rows / 128) * (F / 128) < ctx->n_cus && F % 64 == 0) return launch_h3<EPI_RFF, H128x64k32>(a, (hipStream_t)stream);
+#if RFF_TILE == 1
+    if (F % 256 == 0 && (rows / 128) * (F / 256) >= ctx->n_cus) return launch_h3<EPI_RFF, H128x256>(a, (hipStream_t)stream);
+#endif
     return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
   }
   return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);

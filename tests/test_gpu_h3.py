@@ -3,6 +3,8 @@ products on the f16 MFMA pipe, fp32 accumulation): parity with the oracle's fp32
 (dynamics.py:216-233, 422-433) at the f32 path's tolerance, per-row independence of the
 activation scaling (extreme, zero and non-finite rows), determinism, the weight split and
 the row-exponent slots, and the C ABI's argument checks."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -359,3 +361,52 @@ def test_output_stream_k_deterministic_and_close_to_unsplit(B):
     torch.cuda.synchronize()
     d = (p1 - p0).abs().max().item()
     assert d <= 1e-6 * max(1.0, p0.abs().max().item()), d
+
+
+@pytest.mark.parametrize("rows", [40960, 20480, 10240, 5120])
+def test_rff_features_every_tile_shape(rows):
+    """amx_rff_features_h3 on each of its tiles -- 40 960 / 20 480 / 10 240 rows: 128 x 128 (or,
+    RFF_TILE 1 builds, 128 x 256 16x16x32 split-schedule tiles at 40 960 / 20 480); 5 120: 128 x 64
+    -- against phi = cos(x W^T + b)
+    sqrt(2/F) in fp64 (linear_cost.py:64-71, tolerance as test_f16x3_rff_features_in_rollout), the
+    column partials against the fp64 sums of the valid phi rows of each 128-row block
+    (n_valid and row_mask both applied), and bit-identical on a second launch."""
+    import amp_extensions_amd as amx
+    K, F = 416, 512
+    ctx = amx.AmxContext(197, 36, n_models=1, hidden=128, n_hidden=1, feat_dim=F, device=DEV)
+    lib, h = ctx.lib, ctx.h
+    g = torch.Generator(device="cpu").manual_seed(rows)
+    x = (0.5 * torch.randn(rows, K, generator=g)).float()
+    x[:, 394:] = 0
+    W = (torch.rand(F, K, generator=g) / 14.0).float()
+    W[:, 394:] = 0
+    b = ((torch.rand(F, generator=g) - 0.5) * 6.28).float()
+    mask = (torch.rand(rows, generator=g) > 0.1).to(torch.uint8)
+    n_valid = rows - 77
+    xd, Wd, bd, md = x.to(DEV), W.to(DEV), b.to(DEV), mask.to(DEV)
+    W2 = torch.empty(F * 2 * K, dtype=torch.int16, device=DEV)
+    wexp = torch.empty(F, dtype=torch.int32, device=DEV)
+    rexp = torch.empty(rows, dtype=torch.int32, device=DEV)
+    st = ctx.stream
+    assert lib.amx_split_f16x2(h, 1, F, K, Wd.data_ptr(), K, 0, W2.data_ptr(), F * 2 * K, wexp.data_ptr(), F, st) == 0
+    assert lib.amx_row_exponents(h, 1, rows, K, xd.data_ptr(), K, 0, rexp.data_ptr(), rows, 1, st) == 0
+    scale = float(np.float32(np.sqrt(2.0 / F)))
+    outs = []
+    for _ in range(2):
+        phi = torch.empty(rows, F, device=DEV)
+        part = torch.empty(rows // 128, F, dtype=torch.float64, device=DEV)
+        assert lib.amx_rff_features_h3(h, rows, n_valid, F, K, xd.data_ptr(), K, W2.data_ptr(), wexp.data_ptr(),
+                                       rexp.data_ptr(), bd.data_ptr(), ctypes.c_float(scale), phi.data_ptr(), F,
+                                       part.data_ptr(), md.data_ptr(), st) == 0
+        torch.cuda.synchronize()
+        outs.append((phi.cpu(), part.cpu()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    phi, part = outs[0][0].double().numpy(), outs[0][1].numpy()
+    xn, Wn = x.double().numpy(), W.double().numpy()
+    ref = np.cos(xn @ Wn.T + b.double().numpy()) * scale
+    arg = np.abs(xn) @ np.abs(Wn).T
+    err = np.abs(phi - ref) / scale
+    assert (err <= 4e-7 * arg + 1e-6).all(), float((err - 4e-7 * arg).max())
+    valid = (mask.numpy() > 0) & (np.arange(rows) < n_valid)
+    want = (phi * valid[:, None]).reshape(rows // 128, 128, F).sum(1)
+    np.testing.assert_allclose(part, want, rtol=1e-12, atol=1e-12)
