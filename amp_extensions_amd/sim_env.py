@@ -162,7 +162,8 @@ class SimEnv(_EnvBase):
         `reset_table` (extension): a ReferenceMotion or a [R, S] reset-state table (row
         floor(t); the synthetic benchmark layout) in place of the arg file's motion.
         reset_args: custom_time / time_max set the reset-time window (sim_env.py:76-77),
-        resolve the ground lift; noise options raise NotImplementedError (check_reset_args)."""
+        resolve the ground lift; the noise options perturb every motion reset (AddNoise on the
+        device, check_reset_args; a reset-state table with noise raises NotImplementedError)."""
         self.reset_args = check_reset_args(reset_args)
         self.dynamic_ensemble = dynamic_ensemble
         dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
