@@ -87,6 +87,7 @@ SIGNATURES = {
     "amx_npg_reduce": (c_int, [vp, vp, c_int, c_int, vp, vp]),
     "amx_npg_pass_gated": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp, vp]),
     "amx_npg_reduce_gated": (c_int, [vp, vp, c_int, c_int, vp, vp, vp]),
+    "amx_npg_pass_ex": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp, vp, vp]),
     "amx_npg_cg_init": (c_int, [vp, c_int, vp, vp, vp, vp, vp, vp, vp]),
     "amx_npg_cg_step": (c_int, [vp, c_int, c_int, vp, vp, c_dbl, c_dbl, vp, vp, vp, vp, vp, vp]),
     "amx_step": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_int, vp]),

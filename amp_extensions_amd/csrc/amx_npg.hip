@@ -90,7 +90,9 @@ struct NpgArgs {
   double* partials;          // VPG/FVP: [blocks][P]; EVAL: [blocks][2]
   int P;
   const double* gate;        // optional CG state {rdotr, live}: live == 0 -> the pass is a no-op
+  float* hcache;             // optional theta forward [N][64] = H1 | H2: VPG writes it, FVP (HC) reads it
 };
+constexpr int HCW = 2 * 32;  // floats per cached row (H1 | H2)
 
 struct Lay {  // offsets into the packed parameter vector
   int w1, b1, w2, b2, w3, b3, ls;
@@ -186,10 +188,16 @@ __device__ __forceinline__ pf4 mma(float a, float b, pf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int MODE, typename TO, typename TA, int RC, int JJM>
+template <int MODE, typename TO, typename TA, int RC, int JJM, bool HC = false>
 __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   // JJM: layer-1 K steps compiled (>= ceil(S / 16); steps past S multiply zero weights)
+  // HC (FVP): the theta forward (H1, H2) is read from a.hcache, written by the VPG pass of the
+  // same update (same kernels, same bits), instead of recomputed: layer 1 computes only the
+  // tangent's tiles, its two MFMA chains (x.x/x.z and x.y/x.w) on two waves each, and layer 2's
+  // two products of the tangent (H1 V2^T and D1' W2^T) on two waves -- every sum in the order
+  // of the uncached pass, so the products are bit-identical to it
   constexpr int mode = MODE;
+  constexpr bool HCF = HC && MODE == NPG_FVP;
   constexpr int NRB = RC / 16;                 // 16-row blocks per chunk
   constexpr int TPR = NT / RC;                 // staging threads per row
   constexpr int XU = MAXS / TPR, AU = MAXA / TPR;
@@ -235,7 +243,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     const int e = t + u * NT;
     w1a[u] = w1b[u] = pf4{0.f, 0.f, 0.f, 0.f};
     if (e < nw4) {
-      w1a[u] = reinterpret_cast<const pf4*>(a.theta)[e];
+      if (!HCF) w1a[u] = reinterpret_cast<const pf4*>(a.theta)[e];
       if (two) w1b[u] = reinterpret_cast<const pf4*>(a.vec)[e];
     }
   }
@@ -266,6 +274,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   TO xv[XU];
   TA av[AU];
   double dv = 0.0;
+  pf4 hv = {0.f, 0.f, 0.f, 0.f};  // HC: cached row t / 16, floats 4 (t % 16) .. + 3
   const int pr = t / TPR, pc = t % TPR;
   constexpr bool need_act = mode != NPG_FVP;
   auto prefetch = [&](int c0, int nr) {
@@ -279,6 +288,11 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       for (int u = 0; u < AU; ++u) av[u] = (rv && pc + TPR * u < A) ? as[TPR * u] : TA(0);
       if (t < RC) dv = t < nr ? a.adv[c0 + t] : 0.0;
     }
+    if (HCF) {
+      const int hr = t >> 4;
+      hv = (t < RC * 16 && hr < nr) ? *reinterpret_cast<const pf4*>(a.hcache + (long long)(c0 + hr) * HCW + 4 * (t & 15))
+                                     : pf4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   auto stash = [&]() {
     float* xd = X + pr * g.XS + pc;
@@ -291,6 +305,10 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       for (int u = 0; u < AU; ++u)
         if (pc + TPR * u < A) ad[TPR * u] = (float)av[u];
       if (t < RC) ADV[t] = dv;
+    }
+    if (HCF && t < RC * 16) {
+      const int hr = t >> 4, hc = t & 15;
+      *reinterpret_cast<pf4*>((hc < 8 ? H1 + 4 * hc : H2 + 4 * (hc - 8)) + hr * HS) = hv;
     }
   };
   const int r0 = blockIdx.x * a.rows_per_block;
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       if (e < nw4) reinterpret_cast<pf4*>(X)[e] = w[u];
     }
     lds_barrier();
-    if (f1 && mat1 == set) {
+    if (f1 && (mat1 == set || HCF)) {  // HC: every wave holds the tangent's W1 rows
       const float* wrow = X + (cb1 * 16 + i) * S;
 #pragma unroll
       for (int jj = 0; jj < JJM; ++jj) {
@@ -324,7 +342,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   };
 #pragma unroll
   for (int jj = 0; jj < JJM; ++jj) wf[jj] = pf4{0.f, 0.f, 0.f, 0.f};
-  fragments(w1a, 0);
+  if (!HCF) fragments(w1a, 0);
   if (two) fragments(w1b, 1);
 
   // stores: parameter images, constant pads, the per-action table
@@ -385,7 +403,50 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     NPG_STAMP(2 + 8 * ci + 1);
 
     // ---- layer 1: H1 = tanh(X W1^T + b1); FVP: D1 = X V1^T + vb1; EVAL: D1 = tanh(X V1n^T + b1n)
-    if ((NPG_PHASES & 1) && f1) {
+    if constexpr (HCF) {
+      // the tangent's 4 tiles (units 16 cb, rows 16 rb), each as two chains: waves with
+      // (wave >> 1) & 1 == 0 the x.x / x.z chain (ca), the others the x.y / x.w chain (cb),
+      // which they leave in D1; then z = (ca + cb) + vb1 as the uncached pass forms it
+      if (NPG_PHASES & 1) {
+        const int cb = wave & 1, rb = wave >> 2, ch = (wave >> 1) & 1;
+        const float* xr = X + (rb * 16 + i) * XS + 4 * kq;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+        pf4 xq[2];
+        xq[0] = *reinterpret_cast<const pf4*>(xr);
+        xq[1] = *reinterpret_cast<const pf4*>(xr + 16 * min(1, JJ - 1));
+        if (ch == 0) {
+#pragma unroll
+          for (int jj = 0; jj < JJM; ++jj) {
+            const pf4 x = xq[jj & 1];
+            if (jj + 2 < JJM) xq[jj & 1] = *reinterpret_cast<const pf4*>(xr + 16 * min(jj + 2, JJ - 1));
+            acc = mma(x.x, wf[jj].x, acc);
+            acc = mma(x.z, wf[jj].z, acc);
+          }
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < JJM; ++jj) {
+            const pf4 x = xq[jj & 1];
+            if (jj + 2 < JJM) xq[jj & 1] = *reinterpret_cast<const pf4*>(xr + 16 * min(jj + 2, JJ - 1));
+            acc = mma(x.y, wf[jj].y, acc);
+            acc = mma(x.w, wf[jj].w, acc);
+          }
+        }
+        const int col = cb * 16 + i;
+        if (ch) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) D1[(rb * 16 + 4 * kq + r) * DS + col] = acc[r];
+        }
+        lds_barrier();
+        if (!ch) {
+          const float bias = tv.b1[col];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* d = D1 + (rb * 16 + 4 * kq + r) * DS + col;
+            *d = (acc[r] + *d) + bias;
+          }
+        }
+      }
+    } else if ((NPG_PHASES & 1) && f1) {
       const float* xr[MI];
       pf4 ca[MI], cb[MI], xq[MI][2];
 #pragma unroll
@@ -422,8 +483,13 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
         for (int r = 0; r < 4; ++r) {
           const int row = rb * 16 + 4 * kq + r;
           const float z = (ca[m][r] + cb[m][r]) + bias;
-          if (!mat1) H1[row * HS + col] = tanhf(z);
-          else D1[row * DS + col] = mode == NPG_EVAL ? tanhf(z) : z;  // FVP: tanh' applied on use
+          if (!mat1) {
+            const float hz = tanhf(z);
+            H1[row * HS + col] = hz;
+            if (mode == NPG_VPG && a.hcache && row < nr) a.hcache[(long long)(c0 + row) * HCW + col] = hz;
+          } else {
+            D1[row * DS + col] = mode == NPG_EVAL ? tanhf(z) : z;  // FVP: tanh' applied on use
+          }
         }
       }
     }
@@ -432,7 +498,34 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
 
     // ---- layer 2 (the layer-1 tiles): H2 = tanh(H1 W2^T + b2);
     //      FVP: D2 = H1 V2^T + (D1 (1 - H1^2)) W2^T + vb2; EVAL: D2 = tanh(D1 V2n^T + b2n)
-    if ((NPG_PHASES & 2) && f1) {
+    if constexpr (HCF) {
+      // the tangent's two products on two waves per tile: (wave >> 1) & 1 == 0 the D1' W2^T
+      // term (left in D2), the others H1 V2^T, then D2 = (H1 V2^T + D1' W2^T) + vb2
+      if (NPG_PHASES & 2) {
+        const int u = (wave & 1) * 16 + i, rb = wave >> 2, ch = (wave >> 1) & 1;
+        const int rowA = rb * 16 + i;
+        pf4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < NH / 4; ++s2) {
+          const int k = 4 * s2 + kq;
+          const float h = H1[rowA * HS + k];
+          if (ch) acc = mma(h, tv.w2[u * WS + k], acc);
+          else acc = mma(D1[rowA * DS + k] * (1.f - h * h), th.w2[u * WS + k], acc);
+        }
+        if (!ch) {  // (D2 is not read in this phase: its last readers are behind earlier barriers)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) D2[(rb * 16 + 4 * kq + r) * DS + u] = acc[r];
+        }
+        lds_barrier();
+        if (ch) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* d = D2 + (rb * 16 + 4 * kq + r) * DS + u;
+            *d = (acc[r] + *d) + tv.b2[u];
+          }
+        }
+      }
+    } else if ((NPG_PHASES & 2) && f1) {
       const int u = cb1 * 16 + i;
       pf4 acc[MI], acc2[MI];
 #pragma unroll
@@ -460,7 +553,11 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = rb * 16 + 4 * kq + r;
-          if (!mat1) H2[row * HS + u] = tanhf(acc[m][r] + th.b2[u]);
+          if (!mat1) {
+            const float hz = tanhf(acc[m][r] + th.b2[u]);
+            H2[row * HS + u] = hz;
+            if (mode == NPG_VPG && a.hcache && row < nr) a.hcache[(long long)(c0 + row) * HCW + NH + u] = hz;
+          }
           else if (mode == NPG_FVP) D2[row * DS + u] = (acc[m][r] + acc2[m][r]) + tv.b2[u];
           else D2[row * DS + u] = tanhf(acc[m][r] + tv.b2[u]);
         }
@@ -869,6 +966,14 @@ extern "C" int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs
                                   const void* act, int act_dtype, long long lda, const double* adv,
                                   const float* theta, const float* vec, int rows_per_block, double* partials,
                                   const double* gate, void* stream) {
+  return amx_npg_pass_ex(ctx, mode, N, obs, obs_dtype, ldo, act, act_dtype, lda, adv, theta, vec, rows_per_block,
+                         partials, gate, nullptr, stream);
+}
+
+extern "C" int amx_npg_pass_ex(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
+                               const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
+                               const float* vec, int rows_per_block, double* partials, const double* gate,
+                               float* hcache, void* stream) {
   AMX_CHECK_ARG(ctx, "amx_npg_pass: null ctx");
   const int S = ctx->S, A = ctx->A;
   AMX_CHECK_ARG(mode >= NPG_VPG && mode <= NPG_EVAL, "amx_npg_pass: mode=%d", mode);
@@ -886,9 +991,12 @@ extern "C" int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs
   a.mode = mode; a.N = N; a.S = S; a.A = A; a.rows_per_block = rows_per_block;
   a.obs = obs; a.ldo = ldo;
   a.act = act; a.lda = lda;
-  a.adv = adv; a.theta = theta; a.vec = vec; a.partials = partials; a.gate = gate;
+  a.adv = adv; a.theta = theta; a.vec = vec; a.partials = partials; a.gate = gate; a.hcache = hcache;
   a.P = (int)amx_npg_param_count(S, A);
   const bool of64 = obs_dtype == AMX_IN_F64, af64 = act_dtype == AMX_IN_F64;
+  AMX_CHECK_ARG(!hcache || mode == NPG_VPG || (mode == NPG_FVP && !of64),
+                "amx_npg_pass: hcache is written by VPG and read by FVP on fp32 observations (mode %d)", mode);
+  AMX_CHECK_ARG(((uintptr_t)hcache & 15) == 0, "amx_npg_pass: hcache must be 16-byte aligned");
   const size_t lds = npg_lds_bytes(S, A, mode, RC0);
   AMX_CHECK_ARG(lds <= 160 * 1024, "amx_npg_pass: %zu B of LDS", lds);
   const int blocks = (N + rows_per_block - 1) / rows_per_block;
@@ -898,7 +1006,7 @@ extern "C" int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs
   void (*kern)(NpgArgs) = nullptr;
   if (!of64 && (mode == NPG_FVP || !af64)) {
 #define NPG_PICK(J)                                                                                  \
-  kern = mode == NPG_FVP ? k_npg<NPG_FVP, float, float, RC0, J>                                      \
+  kern = mode == NPG_FVP ? (hcache ? k_npg<NPG_FVP, float, float, RC0, J, true> : k_npg<NPG_FVP, float, float, RC0, J>) \
        : mode == NPG_VPG ? k_npg<NPG_VPG, float, float, RC0, J> : k_npg<NPG_EVAL, float, float, RC0, J>
     if (jj <= 4) NPG_PICK(4);
     else if (jj <= 8) NPG_PICK(8);

@@ -115,7 +115,7 @@ class DeviceNPG:
         # one block per CU (the pass kernel holds ~140 KB of LDS): one wave of blocks
         return max(32, int(math.ceil(n / 256 / 32)) * 32)
 
-    def _pass(self, mode, obs, act, adv, vec, gate=None):
+    def _pass(self, mode, obs, act, adv, vec, gate=None, hcache=None):
         c = self.ctx
         n = obs.shape[0]
         rpb = self._rows_per_block(n)
@@ -128,10 +128,11 @@ class DeviceNPG:
         od = N.AMX_IN_F64 if obs.dtype == torch.float64 else N.AMX_IN_F32
         ad = N.AMX_IN_F64 if act.dtype == torch.float64 else N.AMX_IN_F32
         g = None if gate is None else gate.data_ptr()
-        N.check(c.lib.amx_npg_pass_gated(c.h, mode, n, obs.data_ptr(), od, obs.stride(0), act.data_ptr(), ad,
-                                         act.stride(0), None if adv is None else adv.data_ptr(),
-                                         self.theta.data_ptr(), None if vec is None else vec.data_ptr(), rpb,
-                                         part.data_ptr(), g, c.stream), "amx_npg_pass")
+        N.check(c.lib.amx_npg_pass_ex(c.h, mode, n, obs.data_ptr(), od, obs.stride(0), act.data_ptr(), ad,
+                                      act.stride(0), None if adv is None else adv.data_ptr(),
+                                      self.theta.data_ptr(), None if vec is None else vec.data_ptr(), rpb,
+                                      part.data_ptr(), g, None if hcache is None else hcache.data_ptr(), c.stream),
+                "amx_npg_pass")
         out = torch.empty(width, dtype=torch.float64, device=c.device)
         N.check(c.lib.amx_npg_reduce_gated(c.h, part.data_ptr(), nb, width, out.data_ptr(), g, c.stream),
                 "amx_npg_reduce")
@@ -179,13 +180,23 @@ class DeviceNPG:
         h[-self.A:] += self._ls_curvature() * v32[-self.A:].double()
         return h + regu * v.to(torch.float64)  # hvp_flat + regu_coef * vector (npg_cg.py:105: the fp64 vector)
 
-    def cg_solve(self, obs, act, b: torch.Tensor) -> torch.Tensor:
+    def _hcache(self, n: int) -> torch.Tensor:
+        """The per-sample theta forward (H1 | H2, [n][64] fp32) the VPG pass writes and the CG's
+        Fisher-vector passes read (amx_npg_pass_ex), grown on demand."""
+        hc = self._bufs.get("hcache")
+        if hc is None or hc.shape[0] < n:
+            hc = self._bufs["hcache"] = torch.empty(n, 64, dtype=torch.float32, device=self.ctx.device)
+        return hc
+
+    def cg_solve(self, obs, act, b: torch.Tensor, hcache=None) -> torch.Tensor:
         """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with
         NPG.HVP as the operator.  Each iteration is one Fisher-vector pass + reduce and one
         single-workgroup vector step (amx_npg_cg_step); the early stop is the step's device-side
         `live` flag (a finished solve leaves x unchanged), so no host sync between iterations.
         The FVP pass and its reduction read the same flag (amx_npg_pass_gated): after the stop
-        the remaining iterations are empty launches, not Fisher-vector products."""
+        the remaining iterations are empty launches, not Fisher-vector products.  `hcache`: the
+        theta forward written by this update's VPG pass (train_from_arrays), so every product
+        skips layers 1-2 at theta (bit-identical products)."""
         c = self.ctx
         P = self.P
         dev = c.device
@@ -197,7 +208,8 @@ class DeviceNPG:
         N.check(c.lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
                                       p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_init")
         for _ in range(self.cg_iters):
-            h = self._pass(NPG_FVP, obs, act, None, p32, gate=state)
+            h = self._pass(NPG_FVP, obs, act, None, p32, gate=state,
+                           hcache=hcache if obs.dtype == torch.float32 else None)
             N.check(c.lib.amx_npg_cg_step(c.h, P, self.A, h.data_ptr(), curv.data_ptr(), self.damping,
                                           self.residual_tol, x.data_ptr(), r.data_ptr(), p.data_ptr(),
                                           p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_step")
@@ -217,8 +229,9 @@ class DeviceNPG:
         obs, act, adv = self._inputs(observations, actions, advantages)
         if whiten:
             adv = (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-6)
-        vpg = self._pass(NPG_VPG, obs, act, adv, None)
-        npg = self.cg_solve(obs, act, vpg)
+        hc = self._hcache(obs.shape[0])
+        vpg = self._pass(NPG_VPG, obs, act, adv, None, hcache=hc)
+        npg = self.cg_solve(obs, act, vpg, hcache=hc)
         gdot = torch.dot(vpg, npg)
         if self.alpha is not None:
             alpha = torch.full((), float(self.alpha), dtype=torch.float64, device=gdot.device)

@@ -327,6 +327,14 @@ int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs, int obs_d
                        const float* vec, int rows_per_block, double* partials, const double* gate, void* stream);
 int amx_npg_reduce_gated(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, const double* gate,
                          void* stream);
+/* amx_npg_pass_gated with the policy's forward at theta cached per sample: hcache [N][64] fp32
+ * (H1 = tanh(W1 x + b1) | H2 = tanh(W2 H1 + b2)), 16-byte aligned.  Mode 0 (VPG) writes it; mode 1
+ * (FVP, fp32 observations) reads it instead of recomputing layers 1-2 at theta -- valid only for
+ * the theta and observations of the VPG pass that wrote it (npg_cg.py:123-135: the CG's ten
+ * Fisher-vector products share them).  The FVP partials are bit-identical to the uncached pass. */
+int amx_npg_pass_ex(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo, const void* act,
+                    int act_dtype, long long lda, const double* adv, const float* theta, const float* vec,
+                    int rows_per_block, double* partials, const double* gate, float* hcache, void* stream);
 
 /* The conjugate-gradient solve of NPG (mjrl/mjrl/utils/cg_solve.py:3-23) on the device, one
  * workgroup per call, fixed-order fp64 reductions, no host round trip between iterations.

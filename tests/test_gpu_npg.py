@@ -198,6 +198,32 @@ def test_npg_gated_fvp_pass_skips_after_stop():
     assert bool((part == 7.0).all()) and bool((out == 9.0).all())
 
 
+@pytest.mark.parametrize("N", [2048, 1000])
+def test_npg_fvp_theta_cache_bit_identical(N):
+    """amx_npg_pass_ex: the VPG pass writes the policy's forward at theta (H1 | H2 per sample) and
+    the Fisher-vector pass that reads it (layers 1-2 at theta skipped, the tangent's chains dealt
+    over all eight waves) gives the uncached pass's partials bit for bit -- N = 1000 leaves a
+    ragged last chunk; the VPG result is unchanged by writing the cache."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy, NPG_FVP, NPG_VPG
+    S, A = 197, 36
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    npg = make(S, A, pack_policy(layers, ls))
+    rs = np.random.RandomState(7)
+    o, a, adv = npg._inputs((0.5 * rs.randn(N, S)).astype(np.float32), rs.randn(N, A).astype(np.float32),
+                            rs.randn(N))
+    hc = torch.full((N, 64), float("nan"), dtype=torch.float32, device=DEV)
+    v0 = npg._pass(NPG_VPG, o, a, adv, None).clone()
+    v1 = npg._pass(NPG_VPG, o, a, adv, None, hcache=hc).clone()
+    assert torch.equal(v0, v1)
+    assert not torch.isnan(hc).any()
+    for seed in (1, 2):
+        vec = torch.from_numpy(np.random.RandomState(seed).randn(npg.P).astype(np.float32)).to(DEV)
+        h0 = npg._pass(NPG_FVP, o, a, None, vec).clone()
+        h1 = npg._pass(NPG_FVP, o, a, None, vec, hcache=hc).clone()
+        assert torch.equal(h0, h1), float((h0 - h1).abs().max())
+
+
 def test_npg_pass_input_dtypes_bit_identical():
     """amx_npg_pass on fp64 and fp32 inputs (the fp64 C-ABI path: 16 layer-1 K-steps compiled; the
     fp32 path DeviceNPG takes: ceil(S / 16) rounded to 4 / 8 / 13 / 16) gives the same bits in all

@@ -98,6 +98,25 @@ def time_one(lib, N, S, A):
         e1.record()
         torch.cuda.synchronize()
         res[name] = e0.elapsed_time(e1) / 20 * 1e3
+    if IN_CODE(NP) == NP.N.AMX_IN_F32 and hasattr(ctx.lib, "amx_npg_pass_ex"):
+        # the FVP pass reading the theta forward a VPG pass cached (amx_npg_pass_ex)
+        hc = torch.empty(N, 64, dtype=torch.float32, device="cuda")
+        def ex(mode, h):
+            NP.N.check(ctx.lib.amx_npg_pass_ex(ctx.h, mode, N, obs.data_ptr(), IN_CODE(NP), obs.stride(0),
+                                               act.data_ptr(), IN_CODE(NP), act.stride(0), adv.data_ptr(),
+                                               npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(), None,
+                                               h.data_ptr(), ctx.stream), "amx_npg_pass_ex")
+        ex(NP.NPG_VPG, hc)
+        for _ in range(3):
+            ex(NP.NPG_FVP, hc)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            ex(NP.NPG_FVP, hc)
+        e1.record()
+        torch.cuda.synchronize()
+        res["fvp_cached"] = e0.elapsed_time(e1) / 20 * 1e3
     print(" ".join(f"{k} {v:7.1f} us" for k, v in res.items()))
 
 
@@ -121,11 +140,18 @@ def trace(N, S, A, mode_name="fvp"):
     vec = torch.randn(npg.P, device="cuda", dtype=torch.float32)
     rpb = npg._rows_per_block(N)
     part = torch.empty((N + rpb - 1) // rpb, npg.P, dtype=torch.float64, device="cuda")
-    mode = {"fvp": NP.NPG_FVP, "vpg": NP.NPG_VPG, "eval": NP.NPG_EVAL}[mode_name]
+    mode = {"fvp": NP.NPG_FVP, "vpg": NP.NPG_VPG, "eval": NP.NPG_EVAL, "fvp_cached": NP.NPG_FVP}[mode_name]
+    hc = torch.empty(N, 64, dtype=torch.float32, device="cuda") if mode_name == "fvp_cached" else None
+    if hc is not None:  # the VPG pass writes the theta forward the cached FVP reads
+        NP.N.check(ctx.lib.amx_npg_pass_ex(ctx.h, NP.NPG_VPG, N, obs.data_ptr(), IN_CODE(NP), obs.stride(0),
+                                           act.data_ptr(), IN_CODE(NP), act.stride(0), adv.data_ptr(),
+                                           npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(), None,
+                                           hc.data_ptr(), ctx.stream))
     for _ in range(4):
-        NP.N.check(ctx.lib.amx_npg_pass(ctx.h, mode, N, obs.data_ptr(), IN_CODE(NP), obs.stride(0),
-                                        act.data_ptr(), IN_CODE(NP), act.stride(0), adv.data_ptr(),
-                                        npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(), ctx.stream))
+        NP.N.check(ctx.lib.amx_npg_pass_ex(ctx.h, mode, N, obs.data_ptr(), IN_CODE(NP), obs.stride(0),
+                                           act.data_ptr(), IN_CODE(NP), act.stride(0), adv.data_ptr(),
+                                           npg.theta.data_ptr(), vec.data_ptr(), rpb, part.data_ptr(), None,
+                                           None if hc is None else hc.data_ptr(), ctx.stream))
     torch.cuda.synchronize()
     buf = (C.c_ulonglong * 256)()
     ctx.lib.amx_npg_trace_read.argtypes = [C.c_void_p]
@@ -172,7 +198,7 @@ if __name__ == "__main__":
         build()
     elif cmd == "trace":
         args = [int(x) for x in sys.argv[2:5]] or [40960, 197, 36]
-        for m in ("fvp", "vpg", "eval"):
+        for m in ("fvp", "fvp_cached", "vpg", "eval"):
             trace(*args, mode_name=m)
     elif cmd == "time":
         time_one(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]))
