@@ -64,6 +64,10 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef H3_EXP
 #define H3_EXP 0
 #endif
+// OUT80 (A/B builds): 1 = the 80 x 224 output tile where it makes exactly one tile per CU
+#ifndef OUT80
+#define OUT80 1
+#endif
 // RFF_TILE (A/B builds): 1 = the 128 x 256 16x16x32 split-schedule tile (H128x256) for the RFF
 // pass where it fills the CUs -- measured equal to the 128 x 128 tiles at 40 960 rows (95 us) and
 // 1 us slower at 20 480 (profiles/r04h_rff_ab.txt): both run the pass in ceil(2.5) = 3 rounds of
@@ -1485,6 +1489,10 @@ using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;
 using H128x64k32 = TileH3<4, 1, 1, 2, 2, 2>;
 using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
 using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true, true>;  // + DEEPA (-2 %)
+// 80 x 224 output tiles, 7 waves of 80 x 32 (16x16x32 form, split schedule): one tile per CU when
+// groups * rows / 80 == CUs (5120 lanes x 4 members: the N = 4 / 8 per-rank shares) -- no
+// stream-K partial tiles, the A panel read once
+using H80x224 = TileH3<1, 7, 1, 1, 1, 2, true, true, true, 5, 2, true, true, true, true>;  // + DEEPA
 
 
 // output layer, 256-row stream-K tiles (amx_set_out_tile 4): 8 waves of 64 x 112 on 16x16x32
@@ -1971,6 +1979,9 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
         return launch_h3<EPI_UNNORM, H256x224>(a, s);
       }
     }
+#if OUT80
+    if (rows % 80 == 0 && (long long)groups * (rows / 80) == ctx->n_cus) return launch_h3<EPI_UNNORM, H80x224>(a, s);
+#endif
     // lane counts whose 128 x 224 tiles (14 waves) are fewer than the CUs (4096-7168 lanes x 4
     // members: 128-224 tiles): stream-K over one workgroup per CU (each tile's K range in <= 3
     // segments), instead of the row-block tiles' 4-7 waves per workgroup

@@ -4,7 +4,8 @@ and the strong-scaling shares use -- one tile per workgroup, stream-K (4096-7168
 segments combined in K order), the row-block shapes and small partial grids -- and the scene
 layout S = 226 (15 column blocks).  The ring issues the same three limb products per 16 x 16
 block and K-tile in the same order, over the same K segments, so the predictions are
-bit-identical; and against the oracle's fp64-accumulated forward at rel 2e-5 of the scale.
+bit-identical (at 5120 lanes, where the default is the 80 x 224 one-tile-per-CU tile and the
+ring keeps the stream-K segments, equal to fp32 rounding); and against the oracle's fp64-accumulated forward at rel 2e-5 of the scale.
 Reference: milo/milo/dynamics.py:216-233, 422-433 (BasicMLP output layer + un-normalisation)."""
 import numpy as np
 import pytest
@@ -42,8 +43,16 @@ def test_ring_output_layer_bit_identical(S, A, lanes):
         outs[tile] = ens.forward_preds(ob, ac, lanes).clone()
     torch.cuda.synchronize()
     assert torch.isfinite(outs[0][:, :lanes]).all()
-    assert torch.equal(outs[2][:, :lanes], outs[0][:, :lanes]), "ring 16-row waves differ from the staged tile"
-    assert torch.equal(outs[3][:, :lanes], outs[0][:, :lanes]), "ring 32x112 differs from the staged tile"
+    rows = 4 * ((lanes + 127) // 128 * 128)
+    if S == 197 and rows % 80 == 0 and rows // 80 == torch.cuda.get_device_properties(0).multi_processor_count:
+        # the default is the 80 x 224 one-tile-per-CU output tile here (one K chain per element),
+        # the ring tiles keep the stream-K segments: equal to fp32 rounding of the K split
+        for t in (2, 3):
+            d = (outs[t][:, :lanes] - outs[0][:, :lanes]).abs() / outs[0][:, :lanes].abs().clamp_min(1.0)
+            assert float(d.max()) < 2e-6, (t, float(d.max()))
+    else:
+        assert torch.equal(outs[2][:, :lanes], outs[0][:, :lanes]), "ring 16-row waves differ from the staged tile"
+        assert torch.equal(outs[3][:, :lanes], outs[0][:, :lanes]), "ring 32x112 differs from the staged tile"
     # repeated launches of the ring (its DMA ring and stream-K counters) give the same bits
     ctx.set_out_tile(2)
     again = ens.forward_preds(ob, ac, lanes)
