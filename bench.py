@@ -153,9 +153,9 @@ def cpu_baseline_leg(S, A, args):
     sweep point (W = powers of two up to the CPU share this process has, plus the share
     itself) runs about --cpu-point-s seconds of sampling; the best W is then timed end to end
     (sampler + relabel, the relabel on the whole CPU share as the reference's one-process torch
-    relabel would use it) on --cpu-final-samples env-steps, three times, the relabel on the same
-    fixed sample each time: the value is the median run and all three are reported.  Runs before
-    anything touches the GPU (the pools fork)."""
+    relabel would use it) on --cpu-final-samples env-steps, after one discarded warm-up run three
+    times, the relabel on the same fixed sample each time: the value is the median run and all
+    three are reported.  Runs before anything touches the GPU (the pools fork)."""
     from oracle import cpu_baseline as cb
     share = cpu_share()
     if args.cpu_workers:
@@ -170,14 +170,20 @@ def cpu_baseline_leg(S, A, args):
         r = cb.run(S, A, workers=w, samples=n, expert_rows=args.expert_rows, relabel=False)
         sweep.append((w, r))
     best_w, best = max(sweep, key=lambda x: x[1]["sampler_steps_per_s"])
-    # three end-to-end runs at the best W; every run's sampler draws the same seeded trajectories,
-    # and the relabel leg is timed three times on the SAME fixed sample (the first run's paths),
-    # so the runs differ only by the host's timing noise; the value is the median run
+    # one discarded warm-up end-to-end run (it also keeps the fixed relabel sample: a cold host
+    # runs its first all-core pass at a higher boost clock, 10-20 % above the runs after it on
+    # the round-4 boxes), then three end-to-end runs at the best W, sampler and relabel
+    # interleaved; every run's sampler draws the same seeded trajectories and every relabel runs
+    # on the SAME fixed sample, so the runs differ only by the host's timing noise; the value is
+    # the median run
     n_final = max(best["samples"], args.cpu_final_samples)
-    samp = [cb.run(S, A, workers=best_w, samples=n_final, expert_rows=args.expert_rows, relabel=False,
-                   keep_paths=(i == 0)) for i in range(3)]
-    paths = samp[0].pop("_paths")
-    rel = [cb.relabel_seconds(paths, S, A, expert_rows=args.expert_rows, threads=share) for _ in range(3)]
+    warm = cb.run(S, A, workers=best_w, samples=n_final, expert_rows=args.expert_rows, relabel=False, keep_paths=True)
+    paths = warm.pop("_paths")
+    warm_rel = cb.relabel_seconds(paths, S, A, expert_rows=args.expert_rows, threads=share)
+    samp, rel = [], []
+    for _ in range(3):
+        samp.append(cb.run(S, A, workers=best_w, samples=n_final, expert_rows=args.expert_rows, relabel=False))
+        rel.append(cb.relabel_seconds(paths, S, A, expert_rows=args.expert_rows, threads=share))
     finals = [dict(r, relabel_s=t, relabel_threads=share, end_to_end_steps_per_s=r["samples"] / (r["sampler_s"] + t))
               for r, t in zip(samp, rel)]
     best = sorted(finals, key=lambda r: r["end_to_end_steps_per_s"])[1]
@@ -199,8 +205,9 @@ def cpu_baseline_leg(S, A, args):
                    f"forked sampler workers (torch threads 1) + host relabel (fit_cost + per-path bonus costs, "
                    f"{args.expert_rows}-row expert buffer, {best['relabel_threads']} torch threads); sampler alone "
                    f"{best['sampler_steps_per_s']:.0f} env-steps/s; sampler {best['sampler_s']:.2f}s + relabel "
-                   f"{best['relabel_s']:.2f}s; median of 3 end-to-end runs (the relabel timed on the same "
-                   f"fixed sample each time)"),
+                   f"{best['relabel_s']:.2f}s; median of 3 end-to-end runs after a discarded warm-up run (the "
+                   f"relabel timed on the same fixed sample each time)"),
+        "warmup_run": round(warm["samples"] / (warm["sampler_s"] + warm_rel), 1),
         "end_to_end_runs": e2e,
         "sampler_s_runs": [round(r["sampler_s"], 3) for r in finals],
         "relabel_s_runs": [round(r["relabel_s"], 3) for r in finals],

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04z: the round-4 evidence pass on the final tree -- the whole -m gpu suite and smoke; the PMC
+# r04z: the round-4 evidence pass on the final tree (re-run after each GEMM-source change: the traffic record is keyed to them) -- the whole -m gpu suite and smoke; the PMC
 # HBM-traffic passes of the ensemble GEMM (their JSON goes to amp_extensions_amd/data/, where
 # bench.py reads it, keyed to the GEMM sources' hash); the timed-region rocprofv3 kernel trace of
 # the default bench; SQ counters of a hidden and the output layer; the default bench line (CPU
