@@ -79,6 +79,28 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef RFF_EXP
 #define RFF_EXP 0
 #endif
+// cos for the RFF epilogues.  RFF_HWCOS 1: z reduced to r in [-pi, pi] by a Cody-Waite step
+// (k = rint(z / 2 pi), 2 pi in three parts, fma), then the hardware v_cos_f32 on r / 2 pi; max
+// |error| 3.5e-7 against cos((double) z) over |z| <= 4096 (tools/cos_accuracy.hip,
+// profiles/r04o_cos_accuracy.txt: OCML cosf 7e-8), far below the fp32 rounding of the
+// argument itself (|z| 2^-24: 6e-6 at the MILO features' |z| ~ 1e2); |z| >= 2^16 takes cosf.
+// RFF_HWCOS 0: OCML cosf (rounds 1-3).
+#ifndef RFF_HWCOS
+#define RFF_HWCOS 1
+#endif
+__device__ __forceinline__ float rff_cos(float z) {
+#if RFF_HWCOS
+  if (__builtin_expect(__builtin_fabsf(z) >= 65536.0f, 0)) return cosf(z);
+  const float k = __builtin_rintf(z * 0.15915494309189535f);
+  float r = __builtin_fmaf(-k, 6.28318548202514648f, z);
+  r = __builtin_fmaf(-k, -1.7484555314695172e-7f, r);
+  r = __builtin_fmaf(-k, -2.3889859e-15f, r);
+  return __builtin_amdgcn_cosf(r * 0.15915494309189535f);
+#else
+  return cosf(z);
+#endif
+}
+
 template <int EPI, class TL>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM][TL::TN], int g, int tm, int tn) {
   constexpr int BM = TL::BM, BN = TL::BN, TM = TL::TM, TN = TL::TN;
@@ -166,7 +188,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
 #if RFF_EXP == 1
       const float phi = z * a.rff_scale;
 #else
-      const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
+      const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
 #endif
 #if RFF_EXP != 2
       Cg[(long long)row * a.ldc + col] = phi;
@@ -654,7 +676,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
       const int r = half * 64 + i;
       const int row = tm * 128 + r;
       const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
-      const float phi = cosf(z) * a.rff_scale;   // torch.cos(.) * np.sqrt(2/F)
+      const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
       a.C[(long long)row * a.ldc + col] = phi;
       csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
     }
