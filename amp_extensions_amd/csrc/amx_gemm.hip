@@ -68,6 +68,11 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef OUT80
 #define OUT80 1
 #endif
+// RFF_OCC3 (A/B builds): 1 = the RFF pass on 128 x 128 tiles at three workgroups per CU (H128rff3)
+// when its tiles exceed one round at two per CU
+#ifndef RFF_OCC3
+#define RFF_OCC3 1
+#endif
 // RFF_TILE (A/B builds): 1 = the 128 x 256 16x16x32 split-schedule tile (H128x256) for the RFF
 // pass where it fills the CUs -- measured equal to the 128 x 128 tiles at 40 960 rows (95 us) and
 // 1 us slower at 20 480 (profiles/r04h_rff_ab.txt): both run the pass in ceil(2.5) = 3 rounds of
@@ -153,6 +158,50 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
         }
       }
     }
+  } else if constexpr (TL::OCC >= 3) {  // EPI_RFF, 128 x 128 tiles at three workgroups per CU
+    // The staged epilogue below in two passes of the 64 rows of one wave row (wm = pass), so
+    // the staging takes 64 x 132 floats (33.8 KB) and the tile's 41.5 KB of BK-16 stage
+    // buffers set the LDS: three workgroups per CU.  Thread (c, part): column c, rows
+    // 32 part .. + 31 of each pass; its fp64 sum runs over pass 0's rows, then pass 1's, and
+    // the two parts are added in part order (deterministic).
+    static_assert(BM == 128 && BN == 128 && TL::NT == 256 && TL::WM == 2 && TM * 32 == 64, "RFF half epilogue");
+    constexpr int CLD = BN + 4;
+    float* Cs = smem;  // [64][CLD]
+    const int c = t & (BN - 1), part = t / BN;
+    const int col = tn * BN + c;
+    const float bv = a.bias[col];
+    double csum = 0.0;
+    float* Cg = a.C;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      if (wm == pass) {
+#pragma unroll
+        for (int n = 0; n < TN; ++n)
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int r = m * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+              Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
+            }
+      }
+      const uint64_t vmask = row_valid_mask(a, tm * BM + pass * 64 + part * 32, 32);
+      __syncthreads();
+#pragma unroll 8
+      for (int i = 0; i < 32; ++i) {
+        const int r = part * 32 + i;
+        const int row = tm * BM + pass * 64 + r;
+        const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
+        const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
+        Cg[(long long)row * a.ldc + col] = phi;
+        csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
+      }
+      __syncthreads();
+    }
+    double* red = reinterpret_cast<double*>(smem);  // [2][BN]
+    red[part * BN + c] = csum;
+    __syncthreads();
+    if (part == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[BN + c];
   } else {  // EPI_RFF (128 x 128 or 128 x 64 tiles of 256 threads)
     static_assert(BM == 128 && (BN == 128 || BN == 64) && TL::NT == 256, "RFF epilogue tiles");
     // Stage the raw BM x BN tile through LDS, then one column per thread over BM / PARTS rows:
@@ -1505,6 +1554,9 @@ using H256 = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 template <int MB> using HRow = TileH3<2, 4, 1, 1, 2, 2, true, true, true, MB, 4, true, true, true>;
 template <int RW, int NBO> using HOut = TileH3<RW, 1, 1, 1, 2, 2, true, true, true, 2, NBO, true, true, true>;
 using H128k32 = TileH3<2, 2, 2, 2, 2, 2>;
+// the RFF pass's 128 x 128 tile at three workgroups per CU: BK 16 (41.5 KB of stage buffers),
+// the epilogue staged in two 64-row passes (RFF_OCC3)
+using H128rff3 = TileH3<2, 2, 2, 2, 3, 1>;
 // RFF features at row counts whose 128 x 128 tiles fill less than the CUs (the 4- and 8-GPU
 // strong-scaling shares): 128 x 64, 4 waves of 32 x 64 (half the work per workgroup, twice
 // the workgroups; the same column-partial layout [rows / 128][F])
@@ -1570,7 +1622,9 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   const int tiles = a.tiles_m * a.tiles_n * a.groups;
   const int nwg = a.streamk ? a.streamk : tiles;  // stream-K: a.streamk workgroups
   if (tiles == 0) return AMX_OK;
-  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_epi_lds(TL::BM, TL::BN)) ? rff_epi_lds(TL::BM, TL::BN) : TL::LDS;
+  // (the three-per-CU RFF tile stages its epilogue in two 64-row passes)
+  constexpr size_t rff_lds = TL::OCC >= 3 ? rff_epi_lds(TL::BM / 2, TL::BN) : rff_epi_lds(TL::BM, TL::BN);
+  constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_lds) ? rff_lds : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
@@ -2062,6 +2116,9 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   if (K % 32 == 0) {
     // (at 40 960 rows the 128 x 128 tile is faster: 121 vs 145 us under the profiler)
     if ((rows / 128) * (F / 128) < ctx->n_cus && F % 64 == 0) return launch_h3<EPI_RFF, H128x64k32>(a, (hipStream_t)stream);
+#if RFF_OCC3
+    if ((long long)(rows / 128) * (F / 128) > 2LL * ctx->n_cus) return launch_h3<EPI_RFF, H128rff3>(a, (hipStream_t)stream);
+#endif
 #if RFF_TILE == 1
     if (F % 256 == 0 && (rows / 128) * (F / 256) >= ctx->n_cus) return launch_h3<EPI_RFF, H128x256>(a, (hipStream_t)stream);
 #endif
