@@ -132,12 +132,23 @@ __global__ __launch_bounds__(1024) void k_adv_whiten(Grid g, const double* __res
   __shared__ double red[1024];
   __shared__ double s_mean, s_std;
   const long long total = (long long)g.T * g.L;
+  // a flat vector (one row of L, no lengths / bases: DeviceNPG's whitening): element i is row i
+  // and every element counts -- the same thread-strided order without the 64-bit index division
+  const bool flat = g.T == 1 && g.len == nullptr && g.base == nullptr;
   double s = 0.0, cnt = 0.0;
-  for (long long i = threadIdx.x; i < total; i += 1024) {
-    const int t = (int)(i / g.L), l = (int)(i % g.L);
-    if (t < g.length(l)) {
-      s += adv[g.row(t, l)];
+  if (flat) {
+#pragma unroll 8
+    for (long long i = threadIdx.x; i < total; i += 1024) {
+      s += adv[i];
       cnt += 1.0;
+    }
+  } else {
+    for (long long i = threadIdx.x; i < total; i += 1024) {
+      const int t = (int)(i / g.L), l = (int)(i % g.L);
+      if (t < g.length(l)) {
+        s += adv[g.row(t, l)];
+        cnt += 1.0;
+      }
     }
   }
   red[threadIdx.x] = s;
@@ -159,11 +170,19 @@ __global__ __launch_bounds__(1024) void k_adv_whiten(Grid g, const double* __res
   __syncthreads();
   const double mean = s_mean;
   double q = 0.0;
-  for (long long i = threadIdx.x; i < total; i += 1024) {
-    const int t = (int)(i / g.L), l = (int)(i % g.L);
-    if (t < g.length(l)) {
-      const double d = adv[g.row(t, l)] - mean;
+  if (flat) {
+#pragma unroll 8
+    for (long long i = threadIdx.x; i < total; i += 1024) {
+      const double d = adv[i] - mean;
       q += d * d;
+    }
+  } else {
+    for (long long i = threadIdx.x; i < total; i += 1024) {
+      const int t = (int)(i / g.L), l = (int)(i % g.L);
+      if (t < g.length(l)) {
+        const double d = adv[g.row(t, l)] - mean;
+        q += d * d;
+      }
     }
   }
   __syncthreads();
@@ -182,11 +201,16 @@ __global__ __launch_bounds__(1024) void k_adv_whiten(Grid g, const double* __res
   }
   __syncthreads();
   const double den = s_std + eps;
-  for (long long i = threadIdx.x; i < total; i += 1024) {
-    const int t = (int)(i / g.L), l = (int)(i % g.L);
-    if (t < g.length(l)) {
-      const long long r = g.row(t, l);
-      out[r] = (adv[r] - mean) / den;
+  if (flat) {
+#pragma unroll 8
+    for (long long i = threadIdx.x; i < total; i += 1024) out[i] = (adv[i] - mean) / den;
+  } else {
+    for (long long i = threadIdx.x; i < total; i += 1024) {
+      const int t = (int)(i / g.L), l = (int)(i % g.L);
+      if (t < g.length(l)) {
+        const long long r = g.row(t, l);
+        out[r] = (adv[r] - mean) / den;
+      }
     }
   }
 }

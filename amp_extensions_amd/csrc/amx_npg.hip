@@ -941,6 +941,172 @@ __global__ __launch_bounds__(CGT) void k_npg_cg_step(int P, int A, const double*
   }
 }
 
+// d^2 mean_kl / d log_std^2 at new == old per action (gaussian_mlp.py:144-155 with Dr's 1e-8),
+// in DeviceNPG._ls_curvature's operation order: s = exp(log_std)^2,
+// (8 s s - 4 s eps) / (2 s + eps)^2
+__global__ __launch_bounds__(64) void k_npg_curvature(const float* __restrict__ theta, int P, int A,
+                                                      double* __restrict__ curv) {
+  const int d = blockIdx.x * 64 + threadIdx.x;
+  if (d >= A) return;
+  const double e = exp((double)theta[P - A + d]);
+  const double sq = e * e, eps = 1e-8;
+  const double den = 2.0 * sq + eps;
+  curv[d] = (8.0 * sq * sq - 4.0 * sq * eps) / (den * den);
+}
+
+// The NPG step after the CG (npg_cg.py:141-163): gdot = vpg . npg (fixed-order block sum);
+// const_learn_rate: alpha given, n_step_size = alpha^2 gdot; else n_step_size given,
+// alpha = sqrt(|n_step_size / (gdot + 1e-20)|); new = float32(float64(theta) + alpha npg), its
+// log_std block clamped below at min_log_std (gaussian_mlp.py:71-94; NaN stays NaN, as
+// torch.clamp).  scal = {alpha, n_step_size, gdot}.
+__global__ __launch_bounds__(CGT) void k_npg_apply(int P, int A, const double* __restrict__ vpg,
+                                                   const double* __restrict__ npg, const float* __restrict__ theta,
+                                                   int use_alpha, double alpha_in, double nss_in, float min_ls,
+                                                   float* __restrict__ out, double* __restrict__ scal) {
+  __shared__ double red[CGT / 64];
+  double gl = 0.0;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = threadIdx.x + u * CGT;
+    if (e < P) gl += vpg[e] * npg[e];
+  }
+  const double gdot = cg_block_sum(gl, red);
+  double alpha, nss;
+  if (use_alpha) {
+    alpha = alpha_in;
+    nss = alpha * alpha * gdot;
+  } else {
+    nss = nss_in;
+    alpha = sqrt(fabs(nss / (gdot + 1e-20)));
+  }
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = threadIdx.x + u * CGT;
+    if (e < P) {
+      float v = (float)((double)theta[e] + alpha * npg[e]);
+      if (e >= P - A && v < min_ls) v = min_ls;
+      out[e] = v;
+    }
+  }
+  if (threadIdx.x == 0) {
+    scal[0] = alpha;
+    scal[1] = nss;
+    scal[2] = gdot;
+  }
+}
+
+// One CG iteration's tail in one launch: the FVP partials' column sums (amx_npg_reduce's order:
+// runs of RB blocks, then the runs) and the CG vector step (amx_npg_cg_step).  A 1024-thread
+// block takes 64 columns, one thread per (column, run) summing the run's rows, then one thread
+// per column adds the runs in order; it forms z = h + [curv p32] + damping p for its columns
+// (zbuf) and its part of p.z; the last-arriving block (agent-scope counter, self-resetting)
+// adds the parts in block order and runs the step over all P elements.
+// work = [zbuf: P | pz parts: nblk | counter].
+constexpr int RCT = 1024, RCC = 64;  // threads, columns per block (16 run lanes per column)
+__global__ __launch_bounds__(RCT) void k_npg_reduce_cg(const double* __restrict__ part, int nb, int P, int A,
+                                                       const double* __restrict__ curv, double damping, double tol,
+                                                       double* __restrict__ x, double* __restrict__ r,
+                                                       double* __restrict__ p, float* __restrict__ p32,
+                                                       double* __restrict__ state, double* __restrict__ work) {
+  __shared__ double runs[RCT];  // [run][column]
+  __shared__ double red[RCT];
+  __shared__ int last;
+  if (state[1] == 0.0) return;  // the solve has stopped (uniform; the FVP pass was gated too)
+  const int t = threadIdx.x, cl = t & (RCC - 1), rl = t / RCC;
+  const int c = blockIdx.x * RCC + cl;
+  const int nruns = (nb + RB - 1) / RB;  // <= 16: the pass runs at most 256 blocks
+  double* zbuf = work;
+  double* pzp = work + P;
+  uint32_t* counter = reinterpret_cast<uint32_t*>(work + P + gridDim.x);
+  if (c < P && rl < nruns) {
+    const int b0 = rl * RB, b1 = min(nb, b0 + RB);
+    double sr = 0.0;
+#pragma unroll 8
+    for (int b = b0; b < b1; ++b) sr += part[(long long)b * P + c];
+    runs[rl * RCC + cl] = sr;
+  }
+  __syncthreads();
+  double pl = 0.0;
+  if (rl == 0 && c < P) {
+    double h = runs[cl];
+    if (nruns > 1) {
+      h = 0.0;
+      for (int q = 0; q < nruns; ++q) h += runs[q * RCC + cl];  // amx_npg_reduce's second stage
+    }
+    const double pv = p[c];
+    double z = h;
+    if (c >= P - A) z += curv[c - (P - A)] * (double)p32[c];
+    z += damping * pv;
+    zbuf[c] = z;
+    pl = pv * z;
+  }
+  if (rl == 0) red[cl] = pl;  // the block's part of p.z: its columns in order
+  __syncthreads();
+  if (t == 0) {
+    double sp = 0.0;
+    for (int q = 0; q < RCC; ++q) sp += red[q];
+    pzp[blockIdx.x] = sp;
+    __threadfence();  // zbuf and this part visible (agent scope) before the count
+    const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  if (!last) return;
+  // ---- the step (amx_npg_cg_step's arithmetic, z from zbuf) by the last block: CGE elements
+  // per thread with every load in flight, as amx_npg_cg_step
+  const double rdotr = state[0];
+  // p.z: the blocks' parts in block order (RCT-part slices through LDS, summed in order)
+  const int nblk = gridDim.x;
+  double pz = 0.0;
+  for (int b0 = 0; b0 < nblk; b0 += RCT) {
+    __syncthreads();
+    red[t] = b0 + t < nblk ? pzp[b0 + t] : 0.0;
+    __syncthreads();
+    const int n = min(RCT, nblk - b0);
+    for (int q = 0; q < n; ++q) pz += red[q];
+  }
+  const double v = rdotr / pz;
+  double pv[CGE], rl_[CGE], rr = 0.0;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = t + u * RCT;
+    pv[u] = rl_[u] = 0.0;
+    if (e < P) {
+      pv[u] = p[e];
+      x[e] += v * pv[u];
+      const double rv = r[e] - v * zbuf[e];
+      r[e] = rv;
+      rl_[u] = rv;
+      rr += rv * rv;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) rr += __shfl_xor(rr, o);
+  __syncthreads();
+  if ((t & 63) == 0) red[t >> 6] = rr;
+  __syncthreads();
+  double rrs = 0.0;
+  for (int w = 0; w < RCT / 64; ++w) rrs += red[w];
+  const double mu = rrs / rdotr;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    const int e = t + u * RCT;
+    if (e < P) {
+      const double pn = rl_[u] + mu * pv[u];
+      p[e] = pn;
+      p32[e] = (float)pn;
+    }
+  }
+  if (t == 0) {
+    state[0] = rrs;
+    state[1] = rrs < tol ? 0.0 : 1.0;
+  }
+}
+
 size_t npg_lds_bytes(int S, int A, int mode, int rc) {
   const Geo g(S, A);
   size_t fl = (size_t)small_floats(g) * (mode == NPG_VPG ? 1 : 2) + r4(rc * g.XS) + 2 * r4(rc * HS) +
@@ -1058,6 +1224,42 @@ extern "C" int amx_npg_reduce_gated(amx_ctx* ctx, const double* partials, int bl
   AMX_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_npg_reduce2, dim3((P + 255) / 256), dim3(256), 0, (hipStream_t)stream, ctx->d_npg_scratch,
                      runs, P, out, gate);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" long long amx_npg_reduce_cg_work(int P) {
+  const int nblk = (P + RCC - 1) / RCC;
+  return (long long)P + nblk + 1;
+}
+
+extern "C" int amx_npg_reduce_cg_step(amx_ctx* ctx, const double* partials, int blocks, int P, int A,
+                                      const double* curv, double damping, double tol, double* x, double* r,
+                                      double* p, float* p32, double* state, double* work, void* stream) {
+  AMX_CHECK_ARG(ctx && partials && curv && x && r && p && p32 && state && work,
+                "amx_npg_reduce_cg_step: null argument");
+  AMX_CHECK_ARG(blocks > 0 && blocks <= RB * RCT / RCC && P > A && A > 0 && P <= RCT * CGE,
+                "amx_npg_reduce_cg_step: blocks=%d (<= %d) P=%d A=%d", blocks, RB * RCT / RCC, P, A);
+  hipLaunchKernelGGL(k_npg_reduce_cg, dim3((P + RCC - 1) / RCC), dim3(RCT), 0, (hipStream_t)stream, partials, blocks,
+                     P, A, curv, damping, tol, x, r, p, p32, state, work);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_npg_curvature(amx_ctx* ctx, const float* theta, int P, int A, double* curv, void* stream) {
+  AMX_CHECK_ARG(ctx && theta && curv && P > A && A > 0, "amx_npg_curvature: bad arguments");
+  hipLaunchKernelGGL(k_npg_curvature, dim3((A + 63) / 64), dim3(64), 0, (hipStream_t)stream, theta, P, A, curv);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_npg_apply_step(amx_ctx* ctx, int P, int A, const double* vpg, const double* npg,
+                                  const float* theta, int use_alpha, double alpha, double n_step_size,
+                                  float min_log_std, float* new_theta, double* scal, void* stream) {
+  AMX_CHECK_ARG(ctx && vpg && npg && theta && new_theta && scal, "amx_npg_apply_step: null argument");
+  AMX_CHECK_ARG(P > A && A > 0 && P <= CGT * CGE, "amx_npg_apply_step: P=%d A=%d (P <= %d)", P, A, CGT * CGE);
+  hipLaunchKernelGGL(k_npg_apply, dim3(1), dim3(CGT), 0, (hipStream_t)stream, P, A, vpg, npg, theta, use_alpha, alpha,
+                     n_step_size, min_log_std, new_theta, scal);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

@@ -115,7 +115,9 @@ class DeviceNPG:
         # one block per CU (the pass kernel holds ~140 KB of LDS): one wave of blocks
         return max(32, int(math.ceil(n / 256 / 32)) * 32)
 
-    def _pass(self, mode, obs, act, adv, vec, gate=None, hcache=None):
+    def _pass(self, mode, obs, act, adv, vec, gate=None, hcache=None, reduce=True):
+        """One pass (amx_npg_pass_ex) and its block-order reduction; reduce=False returns the
+        [blocks][width] partials instead (the CG folds their reduction into its step)."""
         c = self.ctx
         n = obs.shape[0]
         rpb = self._rows_per_block(n)
@@ -133,6 +135,8 @@ class DeviceNPG:
                                       self.theta.data_ptr(), None if vec is None else vec.data_ptr(), rpb,
                                       part.data_ptr(), g, None if hcache is None else hcache.data_ptr(), c.stream),
                 "amx_npg_pass")
+        if not reduce:
+            return part
         out = torch.empty(width, dtype=torch.float64, device=c.device)
         N.check(c.lib.amx_npg_reduce_gated(c.h, part.data_ptr(), nb, width, out.data_ptr(), g, c.stream),
                 "amx_npg_reduce")
@@ -162,11 +166,12 @@ class DeviceNPG:
 
     def _ls_curvature(self) -> torch.Tensor:
         """d^2 mean_kl / d log_std^2 at new == old (gaussian_mlp.py:144-155 with Dr's 1e-8):
-        (8 s^2 - 4 s eps) / (2 s + eps)^2, s = exp(log_std)^2."""
-        ls = self.theta[-self.A:].double()
-        s = torch.exp(ls) ** 2
-        eps = 1e-8
-        return (8 * s * s - 4 * s * eps) / (2 * s + eps) ** 2
+        (8 s^2 - 4 s eps) / (2 s + eps)^2, s = exp(log_std)^2 -- one launch (amx_npg_curvature)."""
+        c = self.ctx
+        curv = torch.empty(self.A, dtype=torch.float64, device=c.device)
+        N.check(c.lib.amx_npg_curvature(c.h, self.theta.data_ptr(), self.P, self.A, curv.data_ptr(), c.stream),
+                "amx_npg_curvature")
+        return curv
 
     def HVP(self, observations, actions, vector, regu_coef=None) -> torch.Tensor:
         """NPG.HVP (npg_cg.py:87-106): Fisher (mean_kl Hessian) times `vector` + damping."""
@@ -191,7 +196,8 @@ class DeviceNPG:
     def cg_solve(self, obs, act, b: torch.Tensor, hcache=None) -> torch.Tensor:
         """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with
         NPG.HVP as the operator.  Each iteration is one Fisher-vector pass + reduce and one
-        single-workgroup vector step (amx_npg_cg_step); the early stop is the step's device-side
+        vector step, the pass's reduction folded into the step (amx_npg_reduce_cg_step: column sums
+        and z per block, the step by the last-arriving block); the early stop is the step's device-side
         `live` flag (a finished solve leaves x unchanged), so no host sync between iterations.
         The FVP pass and its reduction read the same flag (amx_npg_pass_gated): after the stop
         the remaining iterations are empty launches, not Fisher-vector products.  `hcache`: the
@@ -207,12 +213,18 @@ class DeviceNPG:
         curv = self._ls_curvature().contiguous()
         N.check(c.lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
                                       p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_init")
+        work = self._bufs.get("cg_work")
+        if work is None:  # zeroed once: its last slot is the fused step's self-resetting counter
+            work = self._bufs["cg_work"] = torch.zeros(int(c.lib.amx_npg_reduce_cg_work(P)), dtype=torch.float64,
+                                                       device=dev)
         for _ in range(self.cg_iters):
-            h = self._pass(NPG_FVP, obs, act, None, p32, gate=state,
-                           hcache=hcache if obs.dtype == torch.float32 else None)
-            N.check(c.lib.amx_npg_cg_step(c.h, P, self.A, h.data_ptr(), curv.data_ptr(), self.damping,
-                                          self.residual_tol, x.data_ptr(), r.data_ptr(), p.data_ptr(),
-                                          p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_step")
+            part = self._pass(NPG_FVP, obs, act, None, p32, gate=state,
+                              hcache=hcache if obs.dtype == torch.float32 else None, reduce=False)
+            # the partials' column sums and the vector step in one launch (amx_npg_reduce_cg_step)
+            N.check(c.lib.amx_npg_reduce_cg_step(c.h, part.data_ptr(), part.shape[0], P, self.A, curv.data_ptr(),
+                                                 self.damping, self.residual_tol, x.data_ptr(), r.data_ptr(),
+                                                 p.data_ptr(), p32.data_ptr(), state.data_ptr(), work.data_ptr(),
+                                                 c.stream), "amx_npg_reduce_cg_step")
         return x
 
     def surrogate_kl(self, obs, act, adv_w, new_theta) -> tuple[float, float]:
@@ -227,25 +239,31 @@ class DeviceNPG:
         (batch_reinforce.py:284-285), VPG, CG, step size, update with the log_std clamp,
         surr_after and kl_dist.  Returns the reference's infos entries."""
         obs, act, adv = self._inputs(observations, actions, advantages)
-        if whiten:
-            adv = (adv - adv.mean()) / (adv.std(unbiased=False) + 1e-6)
-        hc = self._hcache(obs.shape[0])
+        c = self.ctx
+        n = obs.shape[0]
+        if whiten:  # (adv - mean) / (std + 1e-6), population std, in one launch (amx_adv_whiten)
+            w = torch.empty_like(adv)
+            stats = torch.empty(2, dtype=torch.float64, device=c.device)
+            N.check(c.lib.amx_adv_whiten(c.h, 1, n, None, None, n, adv.data_ptr(), 1e-6, w.data_ptr(),
+                                         stats.data_ptr(), c.stream), "amx_adv_whiten")
+            adv = w
+        hc = self._hcache(n)
         vpg = self._pass(NPG_VPG, obs, act, adv, None, hcache=hc)
         npg = self.cg_solve(obs, act, vpg, hcache=hc)
-        gdot = torch.dot(vpg, npg)
-        if self.alpha is not None:
-            alpha = torch.full((), float(self.alpha), dtype=torch.float64, device=gdot.device)
-            n_step_size = alpha ** 2 * gdot
-        else:
-            n_step_size = torch.full((), float(self.n_step_size), dtype=torch.float64, device=gdot.device)
-            alpha = torch.sqrt(torch.abs(n_step_size / (gdot + 1e-20)))
-        new = (self.theta.double() + alpha * npg).to(torch.float32)
-        new[-self.A:] = torch.clamp(new[-self.A:], min=self.min_log_std)
-        n = obs.shape[0]
-        tot = self._pass(NPG_EVAL, obs, act, adv, new.contiguous())
-        self.set_param_values(new)
+        # gdot, the step size and the clamped new parameters in one launch (amx_npg_apply_step)
+        new = torch.empty(self.P, dtype=torch.float32, device=c.device)
+        scal = torch.empty(3, dtype=torch.float64, device=c.device)
+        use_alpha = self.alpha is not None
+        N.check(c.lib.amx_npg_apply_step(c.h, self.P, self.A, vpg.data_ptr(), npg.data_ptr(), self.theta.data_ptr(),
+                                         int(use_alpha), float(self.alpha) if use_alpha else 0.0,
+                                         float(self.n_step_size), self.min_log_std, new.data_ptr(),
+                                         scal.data_ptr(), c.stream), "amx_npg_apply_step")
+        tot = self._pass(NPG_EVAL, obs, act, adv, new)
+        self.theta = new  # already float32 with the log_std clamp (set_param_values' form)
+        if self.policy is not None:
+            self.policy.sync_from(*self._layers_view())
         # the update's one host sync: the reference's infos are python floats
-        alpha_h, delta_h, surr_h, kl_h = torch.stack([alpha, n_step_size, tot[0], tot[1]]).tolist()
+        alpha_h, delta_h, surr_h, kl_h = torch.cat([scal[:2], tot]).tolist()
         return {"vpg_grad": vpg, "npg_grad": npg, "alpha": alpha_h, "delta": delta_h, "surr_before": 0.0,
                 "surr_after": surr_h / n, "kl_dist": kl_h / n, "advantages": adv}
 

@@ -344,6 +344,27 @@ int amx_npg_pass_ex(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtyp
  *   v = rdotr / p.z; x += v p; r -= v z; rr = r.r; p = r + (rr / rdotr) p; rdotr = rr;
  *   live = rdotr >= residual_tol (cg_solve's break: a finished solve leaves x/r/p unchanged);
  *   p32 = float32(p) for the next product.  curv [A]: d^2 mean_kl / d log_std^2.  P <= 16384. */
+/* d^2 mean_kl / d log_std^2 per action at new == old (NPG.HVP's log_std block,
+ * gaussian_mlp.py:144-155): curv[d] = (8 s^2 - 4 s 1e-8) / (2 s + 1e-8)^2, s = exp(log_std[d])^2,
+ * log_std = theta[P - A ..]. */
+int amx_npg_curvature(amx_ctx* ctx, const float* theta, int P, int A, double* curv, void* stream);
+/* The NPG step after the CG (npg_cg.py:141-163) in one workgroup: gdot = vpg . npg; use_alpha
+ * (const_learn_rate): n_step_size = alpha^2 gdot, else alpha = sqrt(|n_step_size / (gdot + 1e-20)|);
+ * new_theta = float32(theta + alpha npg) with the log_std block clamped at min_log_std
+ * (gaussian_mlp.py:71-94); scal = {alpha, n_step_size, gdot}.  P <= 16384. */
+int amx_npg_apply_step(amx_ctx* ctx, int P, int A, const double* vpg, const double* npg, const float* theta,
+                       int use_alpha, double alpha, double n_step_size, float min_log_std, float* new_theta,
+                       double* scal, void* stream);
+/* amx_npg_reduce (the FVP pass's partials, the same summation order) and amx_npg_cg_step in one
+ * launch: every block sums its columns and forms their z and p.z part, the last-arriving block
+ * adds the parts in block order and runs the vector step (so p.z sums in another order than
+ * amx_npg_cg_step's).  work: caller-owned fp64 [amx_npg_reduce_cg_work(P)], ZEROED once before
+ * first use (its last slot is a self-resetting arrival counter); returns at once after the early
+ * stop (state[1] == 0). */
+long long amx_npg_reduce_cg_work(int P);
+int amx_npg_reduce_cg_step(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
+                           double damping, double tol, double* x, double* r, double* p, float* p32, double* state,
+                           double* work, void* stream);
 int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, double* r, double* p, float* p32,
                     double* state, void* stream);
 int amx_npg_cg_step(amx_ctx* ctx, int P, int A, const double* h, const double* curv, double damping,

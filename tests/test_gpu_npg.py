@@ -224,6 +224,51 @@ def test_npg_fvp_theta_cache_bit_identical(N):
         assert torch.equal(h0, h1), float((h0 - h1).abs().max())
 
 
+def test_npg_fused_reduce_cg_step_matches_separate():
+    """amx_npg_reduce_cg_step (the FVP partials' column sums + the CG vector step in one launch,
+    the step by the last-arriving block) against amx_npg_reduce + amx_npg_cg_step from the same
+    state, three iterations: the same h (the reduction's order is kept), p.z summed in block order
+    instead of the 1024-thread tree -- x, r, p within 1e-12 of the scale; the counter self-resets
+    (a second solve from the same start reproduces the first bit for bit)."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy, NPG_FVP
+    S, A, N = 197, 36, 3000
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    npg = make(S, A, pack_policy(layers, ls))
+    rs = np.random.RandomState(11)
+    o, a, _ = npg._inputs((0.5 * rs.randn(N, S)).astype(np.float32), rs.randn(N, A).astype(np.float32))
+    c, lib, P = npg.ctx, npg.ctx.lib, npg.P
+    b = torch.from_numpy(rs.randn(P)).to(DEV)
+    curv = npg._ls_curvature()
+    work = torch.zeros(int(lib.amx_npg_reduce_cg_work(P)), dtype=torch.float64, device=DEV)
+
+    def solve(fused):
+        x, r, p = (torch.empty(P, dtype=torch.float64, device=DEV) for _ in range(3))
+        p32 = torch.empty(P, dtype=torch.float32, device=DEV)
+        st = torch.empty(2, dtype=torch.float64, device=DEV)
+        assert lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(), p32.data_ptr(),
+                                   st.data_ptr(), c.stream) == 0
+        for _ in range(3):
+            if fused:
+                part = npg._pass(NPG_FVP, o, a, None, p32, gate=st, reduce=False)
+                assert lib.amx_npg_reduce_cg_step(c.h, part.data_ptr(), part.shape[0], P, A, curv.data_ptr(),
+                                                  npg.damping, 0.0, x.data_ptr(), r.data_ptr(), p.data_ptr(),
+                                                  p32.data_ptr(), st.data_ptr(), work.data_ptr(), c.stream) == 0
+            else:
+                h = npg._pass(NPG_FVP, o, a, None, p32, gate=st)
+                assert lib.amx_npg_cg_step(c.h, P, A, h.data_ptr(), curv.data_ptr(), npg.damping, 0.0, x.data_ptr(),
+                                           r.data_ptr(), p.data_ptr(), p32.data_ptr(), st.data_ptr(), c.stream) == 0
+        torch.cuda.synchronize()
+        return [t.cpu().double().numpy() for t in (x, r, p, st)]
+
+    sep, fus, fus2 = solve(False), solve(True), solve(True)
+    for u, v in zip(sep[:3], fus[:3]):
+        assert close(v, u, 1e-12), np.abs(u - v).max()
+    assert sep[3][1] == fus[3][1] and close(fus[3][:1], sep[3][:1], 1e-12)
+    for u, v in zip(fus, fus2):
+        assert np.array_equal(u, v)
+
+
 def test_npg_pass_input_dtypes_bit_identical():
     """amx_npg_pass on fp64 and fp32 inputs (the fp64 C-ABI path: 16 layer-1 K-steps compiled; the
     fp32 path DeviceNPG takes: ceil(S / 16) rounded to 4 / 8 / 13 / 16) gives the same bits in all
