@@ -47,6 +47,20 @@ def test_abi_version_and_errors(lib):
     assert rc == -1 and b"amx_step" in lib.amx_last_error()
 
 
+def test_round4_entry_points_validate_without_gpu(lib):
+    """The round-4 NPG / noise entry points refuse bad arguments before any launch, and the
+    fused CG step's workspace size is pure host arithmetic (P + ceil(P / 64) + 1 doubles)."""
+    assert lib.amx_npg_reduce_cg_work(8616) == 8616 + 135 + 1
+    assert lib.amx_npg_reduce_cg_work(64) == 64 + 1 + 1
+    assert lib.amx_npg_curvature(None, None, 10, 4, None, None) == -1
+    assert lib.amx_npg_apply_step(None, 10, 4, None, None, None, 0, 0.0, 0.1, -2.0, None, None, None) == -1
+    assert b"amx_npg_apply_step" in lib.amx_last_error()
+    assert lib.amx_npg_reduce_cg_step(None, None, 1, 10, 4, None, 0.0, 0.0, None, None, None, None, None, None,
+                                      None) == -1
+    assert lib.amx_npg_pass_ex(None, 1, 64, None, 1, 197, None, 1, 36, None, None, None, 32, None, None, None,
+                               None) == -1
+
+
 def test_dense_layer_shapes_match_basicmlp():
     # dynamics.py:412-420: input of layer i = concat of all previous widths
     assert basic_mlp_layer_shapes(226, 28, [512] * 4) == [(512, 254), (512, 766), (512, 1278), (512, 1790),
