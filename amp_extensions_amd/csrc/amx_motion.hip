@@ -247,8 +247,18 @@ __device__ void add_noise(const MView& m, double* pose, double* vel, const Noise
   auto rotate = [&]() {  // RandomRotatePoseVel
     if (r == 0) return;
     const double a = rnd();
-    Q q = qmul({cos(a / 2), 0.0, sin(a / 2), 0.0}, ldq(pose + 3));  // cCharacter::RotateRoot
-    stq(pose + 3, qnorm(q));
+    // cCharacter::RotateRoot (Character.cpp:210-216) -> cKinCharacter::SetRootRotation ->
+    // RotateOrigin(dq) (KinCharacter.cpp:259-264, 300-337): the root rotation becomes
+    // normalize(dq * old) with dq = normalize(rot * old) * old^-1, and the root's linear and
+    // angular velocities are rotated by dq (QuatRotVec writes the gRotDim pad slot as 0)
+    const Q old = ldq(pose + 3);
+    const Q nq = qnorm(qmul({cos(a / 2), 0.0, sin(a / 2), 0.0}, old));
+    const Q dq = qmul(nq, {old.w, -old.x, -old.y, -old.z});
+    stq(pose + 3, qnorm(qmul(dq, old)));
+    const V3 rv = qrot(dq, {vel[0], vel[1], vel[2]});
+    const V3 rw = qrot(dq, {vel[3], vel[4], vel[5]});
+    vel[0] = rv.x; vel[1] = rv.y; vel[2] = rv.z;
+    vel[3] = rw.x; vel[4] = rw.y; vel[5] = rw.z; vel[6] = 0.0;
     for (int i = 0; i < 7; ++i) vel[i] = n.interp * vel[i];  // root vel (3) + root ang vel (gRotDim 4)
     for (int j = 1; j < m.J; ++j) {
       const int o = (int)m.joints[8 * j + 2], sz = (int)m.joints[8 * j + 3];

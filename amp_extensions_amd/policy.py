@@ -38,9 +38,11 @@ class DevicePolicy:
 
     @classmethod
     def from_mjrl(cls, ctx: AmxContext, policy, seed: int = 0):
-        """Build from an mjrl `MLP` object (model.fc_layers + log_std)."""
+        """Build from an mjrl `MLP` object: model.fc_layers for the mean, and log_std_val -- the
+        float64 copy mjrl's get_action draws its noise with and reports as agent_infos['log_std']
+        (gaussian_mlp.py:53, 95-104), refreshed only by set_param_values -- for the noise."""
         layers = [(l.weight.data, l.bias.data) for l in policy.model.fc_layers]
-        return cls(ctx, layers, policy.log_std.data, seed)
+        return cls(ctx, layers, np.asarray(policy.log_std_val, np.float64), seed)
 
     def sync_from(self, layers, log_std) -> None:
         dev = self.ctx.device

@@ -129,20 +129,34 @@ def _sampler_engine(env, lanes: int, K: int, policy, time_max: float) -> Rollout
         reset_source = src.motion if src.motion is not None else src.table
         eng = RolloutEngine(src.ens, reset_source, lanes=lanes, term=src.term, policy=policy, seed=src.seed,
                             max_steps=K, auto_reset=False, record_means=True)
-        eng._reset_noise = getattr(src, "_reset_noise", None)  # the env's reset_args noise (AddNoise)
         # (0 = the whole clip; a table source is already cut to the window's rows)
         if src.motion is not None and time_max != src.motion.get_motion_length():
             eng.reset_time_max = float(time_max)
         cache[key] = eng
+    # the env's reset_args noise (AddNoise) as it is NOW: a later set_reset_noise on the env
+    # reaches the cached engine.  The noise draws come from Philox(engine seed; lane, reset#),
+    # not from the trajectory seed, so with noise on, sample_points' paths depend on the lane
+    # count and the admission order (the reference's own gRand stream is seeded from the wall
+    # clock, util/Rand.cpp:8-9, so it is not reproducible either).
+    eng._reset_noise = getattr(src, "_reset_noise", None)
     eng.policy = policy
     return eng
 
 
 def _mjrl_fingerprint(policy) -> tuple:
-    """Identity + in-place version of every trainable tensor of an mjrl MLP: set_param_values
-    rebinds param.data (gaussian_mlp.py:67-85), an optimizer step bumps the tensor version."""
-    ts = [p.data for p in policy.model.parameters()] + [policy.log_std.data]
-    return tuple((t.data_ptr(), t._version) for t in ts) + (np.asarray(policy.log_std_val).tobytes(),)
+    """The VALUES of every trainable tensor of an mjrl MLP (≈8.6 k floats at S = 197, a 34 KB
+    copy per sample_points call).  Identities and version counters are not enough:
+    set_param_values rebinds param.data (gaussian_mlp.py:67-85), but an optimizer step updates
+    in place (behavior_cloning.py:125-132) and `p.data.add_()` / `p.data.copy_()` go through a
+    `.data` alias whose version counter is not the parameter's, so only the values see every
+    kind of update."""
+    ts = [p.detach() for p in policy.model.parameters()] + [policy.log_std.detach()]
+    vals = torch.cat([t.reshape(-1).to("cpu", torch.float64) for t in ts])
+    return vals, np.asarray(policy.log_std_val).tobytes()
+
+
+def _same_fingerprint(a: tuple, b: tuple) -> bool:
+    return a[1] == b[1] and a[0].shape == b[0].shape and torch.equal(a[0], b[0])
 
 
 def device_policy(env, policy):
@@ -167,8 +181,9 @@ def device_policy(env, policy):
         policy.__dict__["_amx_device_policy"] = (ctx, dp, fp)
         return dp
     _, dp, old = cached
-    if old != fp:
-        dp.sync_from([(l.weight.data, l.bias.data) for l in policy.model.fc_layers], policy.log_std.data)
+    if not _same_fingerprint(old, fp):
+        dp.sync_from([(l.weight.data, l.bias.data) for l in policy.model.fc_layers],
+                     np.asarray(policy.log_std_val, np.float64))
         policy.__dict__["_amx_device_policy"] = (ctx, dp, fp)
     return dp
 

@@ -123,7 +123,29 @@ def parse():
                    help="print this rank's launch layout (rank, world, rendezvous) and exit before any GPU or "
                         "CPU-baseline work (checks the --gpus N process launch)")
     p.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    p.add_argument("--dry-run-hang-rank", type=int, default=-1,
+                   help="--dry-run at N > 1: the ranks join one CPU (gloo) all-reduce, except this one, which "
+                        "sleeps (checks that a hung collective ends the run at --dist-timeout)")
+    p.add_argument("--dist-timeout", type=float, default=300.0,
+                   help="seconds a rendezvous or collective may block before the rank exits non-zero (the process "
+                        "group's timeout; RCCL's watchdog tears the process down, TORCH_NCCL_ASYNC_ERROR_HANDLING=1)")
+    p.add_argument("--diag-rollouts", type=int, default=5,
+                   help="N > 1: untimed rollouts after the timed region with the all-reduce bracketed by HIP events "
+                        "(the line's dist_diag.allreduce_wait_us)")
     return p.parse_args()
+
+
+def init_dist(backend: str, timeout_s: float, dev=None) -> None:
+    """One process group per run, fail-fast: a rendezvous or collective that blocks longer than
+    timeout_s raises (gloo) or is aborted by the RCCL watchdog, which tears the process down
+    (async error handling 1), so a hung rank exits non-zero and launch_ranks stops the others."""
+    import datetime
+    import torch.distributed as dist
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = dict(timeout=datetime.timedelta(seconds=timeout_s))
+    if backend == "nccl":
+        kw["device_id"] = dev
+    dist.init_process_group(backend, **kw)
 
 
 def cpu_share() -> int:
@@ -336,6 +358,14 @@ def main():
             raise SystemExit(3)
         if args.dry_run_fail_rank >= 0:
             time.sleep(60)  # the launcher must stop the surviving ranks
+        if args.dry_run_hang_rank >= 0 and world > 1:
+            import torch
+            import torch.distributed as dist
+            init_dist("gloo", args.dist_timeout)
+            if rank == args.dry_run_hang_rank:
+                time.sleep(120)  # never joins: the others' all-reduce must time out
+            dist.all_reduce(torch.ones(4))
+            dist.destroy_process_group()
         return
     if args.cost == "amp":
         args.faithful = True   # the AMP features are defined on the humanoid3d CtController state
@@ -359,11 +389,21 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.dist_backend)
-    allreduce = (lambda t: dist.all_reduce(t)) if world > 1 else None
+        init_dist(args.dist_backend, args.dist_timeout, dev)
+    # the fused [sum phi, count] all-reduce; after the timed region (dist_diag) its calls are
+    # bracketed by HIP events on the current stream: the wait for the collective, including the
+    # slowest rank's arrival
+    ar_diag = {"on": False, "ev": []}
+
+    def _allreduce(t):
+        if not ar_diag["on"]:
+            return dist.all_reduce(t)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dist.all_reduce(t)
+        e1.record()
+        ar_diag["ev"].append((e0, e1))
+    allreduce = _allreduce if world > 1 else None
     # the overlapped form: the all-reduce is queued asynchronously (GPU-side wait) and runs under
     # the next rollout's first ensemble forward (RolloutEngine.rollout_overlapped)
     allreduce_async = (lambda t: dist.all_reduce(t, async_op=True)) if world > 1 else None
@@ -535,6 +575,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     term_rate = float(eng.done[:T].float().mean().item()) if args.mode != "paths" else None
+    own_elapsed = elapsed
     if world > 1:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -561,6 +602,37 @@ def main():
         flops_per_fwd = ens.mlp_flops_per_sample() * samples / max(n_fwd, 1)
     achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
     ens.gemm_events = None
+
+    # N > 1 diagnostics (untimed, after the timed region): the all-reduce wait per rollout, the
+    # ranks' elapsed-time spread and every rank's GEMM fraction, gathered to rank 0
+    dist_diag = None
+    if world > 1:
+        wait_us = float("nan")
+        if args.diag_rollouts > 0 and args.mode == "engine" and not overlap:
+            ar_diag["on"] = True
+            for _ in range(args.diag_rollouts):
+                one_rollout() if graph is None else graph()
+            torch.cuda.synchronize()
+            ar_diag["on"] = False
+            if ar_diag["ev"]:
+                wait_us = 1e3 * sum(a.elapsed_time(b) for a, b in ar_diag["ev"]) / len(ar_diag["ev"])
+        mine = torch.tensor([own_elapsed, achieved_tflops / GEMM_INFO[args.gemm]["peak"], wait_us],
+                            dtype=torch.float64, device=dev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        every = torch.stack(every).cpu().numpy()
+        el = every[:, 0]
+        dist_diag = {
+            "world_size": dist.get_world_size(), "backend": args.dist_backend,
+            "elapsed_s_per_rank": [round(float(x), 6) for x in el],
+            "elapsed_spread": round(float((el.max() - el.min()) / el.max()), 4),
+            "gemm_frac_per_rank": [round(float(x), 4) for x in every[:, 1]],
+            "allreduce_wait_us_per_rank": [None if np.isnan(x) else round(float(x), 1) for x in every[:, 2]],
+            "allreduce_note": (f"HIP events around the fused [sum phi, count] all-reduce on the current stream over "
+                               f"{args.diag_rollouts} untimed rollouts after the timed region (includes waiting for "
+                               f"the slowest rank)"),
+            "dist_timeout_s": args.dist_timeout,
+        }
 
     # + the cost's share: RFF features, or the discriminator MLP on its input
     if args.cost == "mmd":
@@ -637,6 +709,7 @@ def main():
             },
             "step_flops_frac": round(value / world * step_flops / (peak * 1e12), 4),
             "cpu_baseline": cpu_base,
+            **({} if dist_diag is None else {"dist_diag": dist_diag}),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -375,8 +375,20 @@ def add_noise(joints, pose, vel, ra, u_rot, u_pv):
             return
         a = rnd()
         qy = np.array([math.cos(a / 2), 0.0, math.sin(a / 2), 0.0])   # AxisAngleToQuaternion((0,1,0), a)
-        q = qmul(qy, pose[3:7])   # cCharacter::RotateRoot: rot * root_rot, normalized
+        # cCharacter::RotateRoot (anim/Character.cpp:210-216): new = normalize(rot * root_rot),
+        # then the virtual cKinCharacter::SetRootRotation (KinCharacter.cpp:259-264):
+        # dq = new * root_rot^-1 and RotateOrigin(dq) (KinCharacter.cpp:300-337), which sets the
+        # root rotation to normalize(dq * root_rot) and rotates the root's linear velocity and
+        # angular velocity by dq (QuatRotVec: xyz rotated, the 4th slot of gRotDim written 0)
+        old = pose[3:7].copy()
+        new = qmul(qy, old)
+        new = new / np.linalg.norm(new)
+        dq = qmul(new, qconj(old))
+        q = qmul(dq, old)
         pose[3:7] = q / np.linalg.norm(q)
+        vel[0:3] = qrot(dq, vel[0:3])
+        vel[3:6] = qrot(dq, vel[3:6])
+        vel[6] = 0.0
         interp = float(ra["interp"])
         vel[0:3] = interp * vel[0:3]   # GetRootVel / SetRootVel (gPosDim)
         vel[3:7] = interp * vel[3:7]   # GetRootAngVel / SetRootAngVel (gRotDim = 4)

@@ -51,3 +51,18 @@ def test_failed_rank_fails_the_launch():
                          capture_output=True, text=True, timeout=120)
     assert out.returncode == 3
     assert time.time() - t0 < 30  # ranks 0 and 2 (sleeping) were stopped, not waited for
+
+
+def test_hung_collective_times_out():
+    """A rank that never joins a collective: the others' all-reduce gives up at --dist-timeout
+    (the process group's timeout), exits non-zero, and the launcher stops the hung rank -- the
+    run ends in seconds instead of blocking until an outer limit kills it."""
+    import time
+    t0 = time.time()
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--dry-run-hang-rank", "1",
+                          "--dist-timeout", "5"], env=_env(), capture_output=True, text=True, timeout=170)
+    assert out.returncode != 0
+    assert time.time() - t0 < 90, time.time() - t0
+    ok = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--dry-run-hang-rank", "5",
+                         "--dist-timeout", "30"], env=_env(), capture_output=True, text=True, timeout=170)
+    assert ok.returncode == 0, ok.stderr[-2000:]  # no hung rank: the collective completes

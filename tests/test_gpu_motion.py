@@ -187,6 +187,33 @@ def test_reset_noise_with_injected_draws_matches_oracle(setup, opts):
     assert np.abs(ref - plain).max() > 1e-3  # the noise does move the state
 
 
+def test_reset_noise_root_yaw_rotates_root_velocity(setup):
+    """Only the root-yaw draw non-zero (every other RandomRotatePoseVel draw u = 0.5 gives
+    RandDouble(-r, r) = 0), interp = 1: RotateRoot -> SetRootRotation -> RotateOrigin
+    (anim/KinCharacter.cpp:259-264, 300-337) turns the root velocities with the pose, so the
+    heading-frame entries of the device state equal the plain reset state and the world-frame
+    root entries are the plain ones rotated about y."""
+    amx, ctx, rm, J, B, M = setup
+    ra = dict(NOISE_BASE, radian=0.3, interp=1.0)
+    n = len(J)
+    base = 1 + 9 * n
+    L = 16
+    times = np.random.RandomState(8).uniform(0, M.duration, L)
+    draws = np.full((L, 48 + 2 * sum(j["size"] for j in J)), 0.5)
+    draws[:, 0] = np.linspace(0.05, 0.95, L)
+    got = rm.states(times, reset_args=ra, draws=torch.from_numpy(draws)).cpu().numpy()
+    plain = oracle_states(J, B, M, times)
+    assert rm.flags == 2   # world-frame root rotation only (the reference scene's flags)
+    for i in range(L):
+        a = -0.3 + draws[i, 0] * 0.6
+        Ry = D.rotmat(np.array([np.cos(a / 2), 0.0, np.sin(a / 2), 0.0]))
+        exp = plain[i].copy()
+        exp[4:7], exp[7:10] = Ry @ plain[i, 4:7], Ry @ plain[i, 7:10]
+        exp[base:base + 3] = Ry @ plain[i, base:base + 3]
+        exp[base + 3:base + 6] = Ry @ plain[i, base + 3:base + 6]
+        assert np.abs(got[i] - exp).max() <= 1e-10, (i, np.abs(got[i] - exp).max())
+
+
 def test_reset_noise_philox_stream(setup):
     """Without injected draws the uniforms come from Philox(seed; lane, reset#): repeatable,
     seed-dependent, finite, and zero amounts give the plain states bit for bit."""

@@ -265,3 +265,38 @@ def test_sample_points_takes_mjrl_policy(setup):
         np.testing.assert_array_equal(pa["agent_infos"]["log_std"], pb["agent_infos"]["log_std"])
     with pytest.raises(ValueError):
         amx.sample_points(env, pol, num_to_collect=10, base_seed=2 ** 32, num_workers=2)  # worker 1: seeds >= 2**32
+
+
+@pytest.mark.parametrize("update", ["optim", "data_add"])
+def test_sample_points_sees_in_place_mjrl_updates(setup, update):
+    """An in-place update of the mjrl policy's parameters (a torch optimizer step on
+    trainable_params, as behavior_cloning.py:125-132, or `p.data.add_`) keeps every tensor's
+    storage; the next sample_points must still sample with the new weights: bit-identical to a
+    fresh DevicePolicy of them."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    from amp_extensions_amd.synthetic import reset_table
+    env = amx.BatchedSimEnv(ens, reset_table(256, S, 1), lanes=128, horizon=20, record_means=True)
+    mj = _MjrlMLP(pw, log_std)
+    amx.sample_points(env, mj, num_to_collect=100, base_seed=3, num_workers=2)
+    ptrs = [p.data_ptr() for p in mj.trainable_params]
+    if update == "optim":
+        opt = torch.optim.SGD(mj.trainable_params, lr=0.05)
+        opt.zero_grad()
+        loss = sum((p * p).sum() for p in mj.trainable_params)
+        loss.backward()
+        opt.step()
+    else:
+        with torch.no_grad():
+            for p in mj.trainable_params:
+                p.data.add_(0.01)
+    assert [p.data_ptr() for p in mj.trainable_params] == ptrs  # storage kept: in place
+    b = amx.sample_points(env, mj, num_to_collect=200, base_seed=9, num_workers=2)
+    # the mean from the updated model, the noise from log_std_val as mjrl's get_action (its
+    # float64 copy is refreshed by set_param_values only, gaussian_mlp.py:53, 91, 102)
+    layers = [(l.weight.data, l.bias.data) for l in mj.model.fc_layers]
+    fresh = amx.DevicePolicy(ens.device.ctx, layers, torch.from_numpy(mj.log_std_val))
+    a = amx.sample_points(env, fresh, num_to_collect=200, base_seed=9, num_workers=2)
+    assert len(a) == len(b)
+    for pa, pb in zip(a, b):
+        np.testing.assert_array_equal(pa["actions"], pb["actions"])
+        np.testing.assert_array_equal(pa["agent_infos"]["log_std"], pb["agent_infos"]["log_std"])

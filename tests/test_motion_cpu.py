@@ -78,3 +78,34 @@ def test_state_amp_obs_oracle_equals_pose_amp_obs(g12):
             a = D.state_amp_obs(J, ee, sp, sc, local)
             b = D.amp_obs(J, B, ee, pp, vp, pc, vc, local_root=local)
             assert a.shape == (226,) and np.abs(a - b).max() <= 1e-12
+
+
+@pytest.mark.parametrize("interp", [1.0, 0.4])
+def test_pure_root_yaw_noise_keeps_heading_frame_velocities(g12, interp):
+    """RandomRotatePoseVel's root yaw goes through cKinCharacter::SetRootRotation ->
+    RotateOrigin (anim/KinCharacter.cpp:259-264, 300-337), which rotates the root's linear and
+    angular velocity with the pose: with only the yaw draw non-zero (every other rotation draw
+    u = 0.5, i.e. RandDouble(-r, r) = 0) the heading-frame part of the state equals the plain
+    reset state scaled by interp (velocities), and the world-frame root entries are the plain
+    ones rotated about y."""
+    g, char, motion, J, B, M = g12
+    world_root = bool(g["record_world_root_rot"])
+    ra = dict(noise_bef_rot=False, noise_min=0, noise_max=0, radian=0.3, rot_vel_w_pose=False,
+              vel_noise=False, interp=interp, knee_rot=False)
+    nr, npv = D.noise_draws(J, ra)
+    n = len(J)
+    base = 1 + 9 * n
+    for k, t in enumerate(np.random.RandomState(5).uniform(0, M.duration, 8)):
+        u = np.full(nr, 0.5)
+        u[0] = 0.1 + 0.1 * k
+        a = -0.3 + u[0] * 0.6
+        Ry = D.rotmat(np.array([np.cos(a / 2), 0.0, np.sin(a / 2), 0.0]))
+        s = D.reset_state(J, B, M, float(t), noise=ra, u_rot=u)
+        p = D.reset_state(J, B, M, float(t))
+        exp = p.copy()
+        exp[base:] *= interp
+        if world_root:
+            exp[4:7], exp[7:10] = Ry @ p[4:7], Ry @ p[7:10]
+            exp[base:base + 3] = Ry @ exp[base:base + 3]
+            exp[base + 3:base + 6] = Ry @ exp[base + 3:base + 6]
+        assert np.abs(s - exp).max() <= 1e-10, (t, np.abs(s - exp).max(), np.abs(s - exp).argmax())

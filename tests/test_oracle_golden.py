@@ -267,7 +267,14 @@ def test_oracle_reset_noise_structure():
         o, s = J[j]["offset"], J[j]["size"]
         np.testing.assert_allclose(p1[o:o + s], pose[o:o + s] / (np.linalg.norm(pose[o:o + s]) if s == 4 else 1.0),
                                    rtol=0, atol=1e-15)
-    np.testing.assert_allclose(v1, 0.5 * vel, rtol=0, atol=0)
+    # the joints' velocities are only interp-scaled; the root's linear and angular velocity are
+    # also turned by the root yaw (RotateRoot -> SetRootRotation -> RotateOrigin,
+    # KinCharacter.cpp:259-264, 300-337): y components and xz norms kept, the pad slot zeroed
+    np.testing.assert_allclose(v1[7:], 0.5 * vel[7:], rtol=0, atol=0)
+    for a in (0, 3):
+        assert abs(v1[a + 1] - 0.5 * vel[a + 1]) <= 1e-15
+        assert abs(math.hypot(v1[a], v1[a + 2]) - 0.5 * math.hypot(vel[a], vel[a + 2])) <= 1e-14
+    assert v1[6] == 0.0 and np.abs(v1[[0, 2, 3, 5]] - 0.5 * vel[[0, 2, 3, 5]]).max() > 1e-3
     for j in range(len(J)):
         if J[j]["type"] == 4:
             o = J[j]["offset"]
