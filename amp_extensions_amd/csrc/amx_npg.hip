@@ -995,29 +995,52 @@ __global__ __launch_bounds__(CGT) void k_npg_apply(int P, int A, const double* _
   }
 }
 
-// One CG iteration's tail in one launch: the FVP partials' column sums (amx_npg_reduce's order:
-// runs of RB blocks, then the runs) and the CG vector step (amx_npg_cg_step).  A 1024-thread
-// block takes 64 columns, one thread per (column, run) summing the run's rows, then one thread
-// per column adds the runs in order; it forms z = h + [curv p32] + damping p for its columns
-// (zbuf) and its part of p.z; the last-arriving block (agent-scope counter, self-resetting)
-// adds the parts in block order and runs the step over all P elements.
-// work = [zbuf: P | pz parts: nblk | counter].
+// One CG iteration's tail (amx_npg_reduce + amx_npg_cg_step's arithmetic) in two launches spread
+// over the chip.  The round-4 form ran the whole vector step and the serial sum of the blocks'
+// p.z parts in the last-arriving block (20 us per iteration: one CU moving 275 KB behind two
+// agent-scope fences); every launch costs ~5 us even when tiny (k_npg_curvature, one 64-thread
+// workgroup: 4.8 us under rocprofv3), so the tail is as few launches as its two grid-wide
+// dependencies allow:
+//  k_npg_cg_reduce: a 1024-thread block per 64 columns, one thread per (column, run of RB FVP
+//    blocks) summing the run's rows, one thread per column adding the runs in order (the
+//    amx_npg_reduce order: the same h bits); z = h + [curv p32] + damping p into zbuf and the
+//    block's part of p.z (its columns in order) into pzp[block];
+//  k_npg_cg_xrp: 1024 threads per block, each block owning 1024 elements.  Every wave sums the
+//    p.z parts in the same fixed order (lane l: parts l, l + 64, ...; then a butterfly whose
+//    association is the same in every lane), so every block has the same v = rdotr / p.z; every
+//    block then forms r' = r - v z for ALL P elements and sums r'.r' in one fixed order (the same
+//    bits in every block: mu = r'.r' / rdotr needs no second grid-wide step), and updates its own
+//    elements: x += v p, r' into r_out, p = r' + mu p, p32.  Block 0 writes {r'.r', live} into
+//    state_out.  r and the state alternate between two buffers (in -> out) because every block
+//    reads all of r while the others write theirs; a stopped solve (state_in live == 0) only
+//    carries r and the state over, so every later iteration stays stopped.
+// work = [zbuf: P | pz parts: ceil(P / 64)].
 constexpr int RCT = 1024, RCC = 64;  // threads, columns per block (16 run lanes per column)
-__global__ __launch_bounds__(RCT) void k_npg_reduce_cg(const double* __restrict__ part, int nb, int P, int A,
-                                                       const double* __restrict__ curv, double damping, double tol,
-                                                       double* __restrict__ x, double* __restrict__ r,
-                                                       double* __restrict__ p, float* __restrict__ p32,
-                                                       double* __restrict__ state, double* __restrict__ work) {
+constexpr int XRT = 1024;            // k_npg_cg_xrp threads (and elements owned) per block
+
+// the sum of n fixed-order parts, computed the same way by every wave that calls it (lane-strided
+// partial sums, then an xor butterfly: every lane ends with the same bits)
+__device__ inline double parts_sum(const double* __restrict__ parts, int n) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int i = lane; i < n; i += 64) s += parts[i];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o);
+  return s;
+}
+
+__global__ __launch_bounds__(RCT) void k_npg_cg_reduce(const double* __restrict__ part, int nb, int P, int A,
+                                                       const double* __restrict__ curv, double damping,
+                                                       const double* __restrict__ p, const float* __restrict__ p32,
+                                                       const double* __restrict__ state, double* __restrict__ work) {
   __shared__ double runs[RCT];  // [run][column]
-  __shared__ double red[RCT];
-  __shared__ int last;
+  __shared__ double red[RCC];
   if (state[1] == 0.0) return;  // the solve has stopped (uniform; the FVP pass was gated too)
+  double* zbuf = work;
+  double* pzp = work + P;
   const int t = threadIdx.x, cl = t & (RCC - 1), rl = t / RCC;
   const int c = blockIdx.x * RCC + cl;
   const int nruns = (nb + RB - 1) / RB;  // <= 16: the pass runs at most 256 blocks
-  double* zbuf = work;
-  double* pzp = work + P;
-  uint32_t* counter = reinterpret_cast<uint32_t*>(work + P + gridDim.x);
   if (c < P && rl < nruns) {
     const int b0 = rl * RB, b1 = min(nb, b0 + RB);
     double sr = 0.0;
@@ -1026,84 +1049,87 @@ __global__ __launch_bounds__(RCT) void k_npg_reduce_cg(const double* __restrict_
     runs[rl * RCC + cl] = sr;
   }
   __syncthreads();
-  double pl = 0.0;
-  if (rl == 0 && c < P) {
-    double h = runs[cl];
-    if (nruns > 1) {
-      h = 0.0;
-      for (int q = 0; q < nruns; ++q) h += runs[q * RCC + cl];  // amx_npg_reduce's second stage
+  if (rl == 0) {
+    double pl = 0.0;
+    if (c < P) {
+      double h = runs[cl];
+      if (nruns > 1) {
+        h = 0.0;
+        for (int q = 0; q < nruns; ++q) h += runs[q * RCC + cl];  // amx_npg_reduce's second stage
+      }
+      const double pv = p[c];
+      double z = h;
+      if (c >= P - A) z += curv[c - (P - A)] * (double)p32[c];
+      z += damping * pv;
+      zbuf[c] = z;
+      pl = pv * z;
     }
-    const double pv = p[c];
-    double z = h;
-    if (c >= P - A) z += curv[c - (P - A)] * (double)p32[c];
-    z += damping * pv;
-    zbuf[c] = z;
-    pl = pv * z;
+    red[cl] = pl;
   }
-  if (rl == 0) red[cl] = pl;  // the block's part of p.z: its columns in order
   __syncthreads();
   if (t == 0) {
     double sp = 0.0;
-    for (int q = 0; q < RCC; ++q) sp += red[q];
+    for (int q = 0; q < RCC; ++q) sp += red[q];  // the block's columns in order
     pzp[blockIdx.x] = sp;
-    __threadfence();  // zbuf and this part visible (agent scope) before the count
-    const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = old == gridDim.x - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(XRT) void k_npg_cg_xrp(int P, double tol, const double* __restrict__ state_in,
+                                                    double* __restrict__ state_out, double* __restrict__ x,
+                                                    const double* __restrict__ r_in, double* __restrict__ r_out,
+                                                    double* __restrict__ p, float* __restrict__ p32,
+                                                    const double* __restrict__ work) {
+  __shared__ double red[XRT / 64];
+  const int t = threadIdx.x;
+  if (state_in[1] == 0.0) {  // stopped: carry r and the state over to the out buffers
+    const int e = blockIdx.x * XRT + t;
+    if (e < P) r_out[e] = r_in[e];
+    if (blockIdx.x == 0 && t == 0) {
+      state_out[0] = state_in[0];
+      state_out[1] = 0.0;
     }
+    return;
   }
-  __syncthreads();
-  if (!last) return;
-  // ---- the step (amx_npg_cg_step's arithmetic, z from zbuf) by the last block: CGE elements
-  // per thread with every load in flight, as amx_npg_cg_step
-  const double rdotr = state[0];
-  // p.z: the blocks' parts in block order (RCT-part slices through LDS, summed in order)
-  const int nblk = gridDim.x;
-  double pz = 0.0;
-  for (int b0 = 0; b0 < nblk; b0 += RCT) {
-    __syncthreads();
-    red[t] = b0 + t < nblk ? pzp[b0 + t] : 0.0;
-    __syncthreads();
-    const int n = min(RCT, nblk - b0);
-    for (int q = 0; q < n; ++q) pz += red[q];
-  }
-  const double v = rdotr / pz;
-  double pv[CGE], rl_[CGE], rr = 0.0;
+  const double* zbuf = work;
+  const double rdotr = state_in[0];
+  const double v = rdotr / parts_sum(work + P, (P + RCC - 1) / RCC);
+  // r'.r' over all P elements in one fixed order (thread t: t, t + XRT, ...; waves in order)
+  // (P <= XRT * CGE: the loop unrolled so all its loads are in flight at once, the adds in order)
+  double rr = 0.0;
+  {
+    double rl[CGE], zl[CGE];
 #pragma unroll
-  for (int u = 0; u < CGE; ++u) {
-    const int e = t + u * RCT;
-    pv[u] = rl_[u] = 0.0;
-    if (e < P) {
-      pv[u] = p[e];
-      x[e] += v * pv[u];
-      const double rv = r[e] - v * zbuf[e];
-      r[e] = rv;
-      rl_[u] = rv;
+    for (int u = 0; u < CGE; ++u) {
+      const int e = t + u * XRT;
+      rl[u] = e < P ? r_in[e] : 0.0;
+      zl[u] = e < P ? zbuf[e] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < CGE; ++u) {
+      const double rv = rl[u] - v * zl[u];
       rr += rv * rv;
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) rr += __shfl_xor(rr, o);
-  __syncthreads();
   if ((t & 63) == 0) red[t >> 6] = rr;
   __syncthreads();
-  double rrs = 0.0;
-  for (int w = 0; w < RCT / 64; ++w) rrs += red[w];
-  const double mu = rrs / rdotr;
-#pragma unroll
-  for (int u = 0; u < CGE; ++u) {
-    const int e = t + u * RCT;
-    if (e < P) {
-      const double pn = rl_[u] + mu * pv[u];
-      p[e] = pn;
-      p32[e] = (float)pn;
-    }
+  rr = 0.0;
+  for (int w = 0; w < XRT / 64; ++w) rr += red[w];
+  const double mu = rr / rdotr;
+  const int e = blockIdx.x * XRT + t;
+  if (e < P) {
+    const double pv = p[e];
+    x[e] += v * pv;
+    const double rv = r_in[e] - v * zbuf[e];
+    r_out[e] = rv;
+    const double pn = rv + mu * pv;
+    p[e] = pn;
+    p32[e] = (float)pn;
   }
-  if (t == 0) {
-    state[0] = rrs;
-    state[1] = rrs < tol ? 0.0 : 1.0;
+  if (blockIdx.x == 0 && t == 0) {
+    state_out[0] = rr;
+    state_out[1] = rr < tol ? 0.0 : 1.0;
   }
 }
 
@@ -1228,20 +1254,22 @@ extern "C" int amx_npg_reduce_gated(amx_ctx* ctx, const double* partials, int bl
   return AMX_OK;
 }
 
-extern "C" long long amx_npg_reduce_cg_work(int P) {
-  const int nblk = (P + RCC - 1) / RCC;
-  return (long long)P + nblk + 1;
-}
+extern "C" long long amx_npg_cg_tail_work(int P) { return (long long)P + (P + RCC - 1) / RCC; }
 
-extern "C" int amx_npg_reduce_cg_step(amx_ctx* ctx, const double* partials, int blocks, int P, int A,
-                                      const double* curv, double damping, double tol, double* x, double* r,
-                                      double* p, float* p32, double* state, double* work, void* stream) {
-  AMX_CHECK_ARG(ctx && partials && curv && x && r && p && p32 && state && work,
-                "amx_npg_reduce_cg_step: null argument");
-  AMX_CHECK_ARG(blocks > 0 && blocks <= RB * RCT / RCC && P > A && A > 0 && P <= RCT * CGE,
-                "amx_npg_reduce_cg_step: blocks=%d (<= %d) P=%d A=%d", blocks, RB * RCT / RCC, P, A);
-  hipLaunchKernelGGL(k_npg_reduce_cg, dim3((P + RCC - 1) / RCC), dim3(RCT), 0, (hipStream_t)stream, partials, blocks,
-                     P, A, curv, damping, tol, x, r, p, p32, state, work);
+extern "C" int amx_npg_cg_tail(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
+                               double damping, double tol, double* x, const double* r_in, double* r_out, double* p,
+                               float* p32, const double* state_in, double* state_out, double* work, void* stream) {
+  AMX_CHECK_ARG(ctx && partials && curv && x && r_in && r_out && p && p32 && state_in && state_out && work,
+                "amx_npg_cg_tail: null argument");
+  AMX_CHECK_ARG(r_in != r_out && state_in != state_out, "amx_npg_cg_tail: r and the state must alternate buffers");
+  AMX_CHECK_ARG(blocks > 0 && blocks <= RB * RCT / RCC && P > A && A > 0 && P <= XRT * CGE,
+                "amx_npg_cg_tail: blocks=%d (<= %d) P=%d A=%d (P <= %d)", blocks, RB * RCT / RCC, P, A, XRT * CGE);
+  const hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_npg_cg_reduce, dim3((P + RCC - 1) / RCC), dim3(RCT), 0, s, partials, blocks, P, A, curv,
+                     damping, p, p32, state_in, work);
+  AMX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_npg_cg_xrp, dim3((P + XRT - 1) / XRT), dim3(XRT), 0, s, P, tol, state_in, state_out, x, r_in,
+                     r_out, p, p32, work);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

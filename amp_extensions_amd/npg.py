@@ -196,8 +196,9 @@ class DeviceNPG:
     def cg_solve(self, obs, act, b: torch.Tensor, hcache=None) -> torch.Tensor:
         """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with
         NPG.HVP as the operator.  Each iteration is one Fisher-vector pass + reduce and one
-        vector step, the pass's reduction folded into the step (amx_npg_reduce_cg_step: column sums
-        and z per block, the step by the last-arriving block); the early stop is the step's device-side
+        vector step, the pass's reduction folded into the step (amx_npg_cg_tail: column sums and z
+        per block, then x, r and p over the whole chip from fixed-order block parts); the early stop
+        is the step's device-side
         `live` flag (a finished solve leaves x unchanged), so no host sync between iterations.
         The FVP pass and its reduction read the same flag (amx_npg_pass_gated): after the stop
         the remaining iterations are empty launches, not Fisher-vector products.  `hcache`: the
@@ -207,24 +208,27 @@ class DeviceNPG:
         P = self.P
         dev = c.device
         b = b.to(torch.float64).contiguous()
-        x, r, p = (torch.empty(P, dtype=torch.float64, device=dev) for _ in range(3))
+        x, r, p, r2 = (torch.empty(P, dtype=torch.float64, device=dev) for _ in range(4))
         p32 = torch.empty(P, dtype=torch.float32, device=dev)
-        state = torch.empty(2, dtype=torch.float64, device=dev)
+        state, state2 = (torch.empty(2, dtype=torch.float64, device=dev) for _ in range(2))
         curv = self._ls_curvature().contiguous()
         N.check(c.lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
                                       p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_init")
         work = self._bufs.get("cg_work")
-        if work is None:  # zeroed once: its last slot is the fused step's self-resetting counter
-            work = self._bufs["cg_work"] = torch.zeros(int(c.lib.amx_npg_reduce_cg_work(P)), dtype=torch.float64,
+        if work is None:
+            work = self._bufs["cg_work"] = torch.empty(int(c.lib.amx_npg_cg_tail_work(P)), dtype=torch.float64,
                                                        device=dev)
         for _ in range(self.cg_iters):
             part = self._pass(NPG_FVP, obs, act, None, p32, gate=state,
                               hcache=hcache if obs.dtype == torch.float32 else None, reduce=False)
-            # the partials' column sums and the vector step in one launch (amx_npg_reduce_cg_step)
-            N.check(c.lib.amx_npg_reduce_cg_step(c.h, part.data_ptr(), part.shape[0], P, self.A, curv.data_ptr(),
-                                                 self.damping, self.residual_tol, x.data_ptr(), r.data_ptr(),
-                                                 p.data_ptr(), p32.data_ptr(), state.data_ptr(), work.data_ptr(),
-                                                 c.stream), "amx_npg_reduce_cg_step")
+            # the partials' column sums and the vector step (amx_npg_cg_tail: two launches); r and
+            # the state alternate buffers from one iteration to the next
+            N.check(c.lib.amx_npg_cg_tail(c.h, part.data_ptr(), part.shape[0], P, self.A, curv.data_ptr(),
+                                          self.damping, self.residual_tol, x.data_ptr(), r.data_ptr(), r2.data_ptr(),
+                                          p.data_ptr(), p32.data_ptr(), state.data_ptr(), state2.data_ptr(),
+                                          work.data_ptr(), c.stream), "amx_npg_cg_tail")
+            r, r2 = r2, r
+            state, state2 = state2, state
         return x
 
     def surrogate_kl(self, obs, act, adv_w, new_theta) -> tuple[float, float]:

@@ -355,16 +355,20 @@ int amx_npg_curvature(amx_ctx* ctx, const float* theta, int P, int A, double* cu
 int amx_npg_apply_step(amx_ctx* ctx, int P, int A, const double* vpg, const double* npg, const float* theta,
                        int use_alpha, double alpha, double n_step_size, float min_log_std, float* new_theta,
                        double* scal, void* stream);
-/* amx_npg_reduce (the FVP pass's partials, the same summation order) and amx_npg_cg_step in one
- * launch: every block sums its columns and forms their z and p.z part, the last-arriving block
- * adds the parts in block order and runs the vector step (so p.z sums in another order than
- * amx_npg_cg_step's).  work: caller-owned fp64 [amx_npg_reduce_cg_work(P)], ZEROED once before
- * first use (its last slot is a self-resetting arrival counter); returns at once after the early
- * stop (state[1] == 0). */
-long long amx_npg_reduce_cg_work(int P);
-int amx_npg_reduce_cg_step(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
-                           double damping, double tol, double* x, double* r, double* p, float* p32, double* state,
-                           double* work, void* stream);
+/* amx_npg_reduce (the FVP pass's partials, the same summation order) and amx_npg_cg_step
+ * (cg_solve.py:3-23: one iteration after the Fisher-vector product) in two launches over the
+ * chip: the column sums with z and the blocks' p.z parts; then x, r, p and the state, every block
+ * forming v = rdotr / p.z and r'.r' itself in one fixed order (so p.z and r.r sum in another order
+ * than amx_npg_cg_step's).  The residual and the state alternate between two caller buffers
+ * (iteration i reads r_in / state_in and writes r_out / state_out; the next swaps them: every
+ * block reads all of r); x, p, p32 are updated in place.  A stopped solve (state_in[1] == 0)
+ * copies r and the state over and changes nothing else.  work: caller-owned fp64
+ * [amx_npg_cg_tail_work(P)], no state kept between calls.  Replaces round 4's
+ * amx_npg_reduce_cg_step (one launch, the step by the last-arriving block). */
+long long amx_npg_cg_tail_work(int P);
+int amx_npg_cg_tail(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
+                    double damping, double tol, double* x, const double* r_in, double* r_out, double* p, float* p32,
+                    const double* state_in, double* state_out, double* work, void* stream);
 int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, double* r, double* p, float* p32,
                     double* state, void* stream);
 int amx_npg_cg_step(amx_ctx* ctx, int P, int A, const double* h, const double* curv, double damping,

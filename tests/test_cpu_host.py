@@ -48,15 +48,15 @@ def test_abi_version_and_errors(lib):
 
 
 def test_round4_entry_points_validate_without_gpu(lib):
-    """The round-4 NPG / noise entry points refuse bad arguments before any launch, and the
-    fused CG step's workspace size is pure host arithmetic (P + ceil(P / 64) + 1 doubles)."""
-    assert lib.amx_npg_reduce_cg_work(8616) == 8616 + 135 + 1
-    assert lib.amx_npg_reduce_cg_work(64) == 64 + 1 + 1
+    """The round-4/5 NPG / noise entry points refuse bad arguments before any launch, and the CG
+    tail's workspace size is pure host arithmetic (P + ceil(P / 64) doubles)."""
+    assert lib.amx_npg_cg_tail_work(8616) == 8616 + 135
+    assert lib.amx_npg_cg_tail_work(64) == 64 + 1
     assert lib.amx_npg_curvature(None, None, 10, 4, None, None) == -1
     assert lib.amx_npg_apply_step(None, 10, 4, None, None, None, 0, 0.0, 0.1, -2.0, None, None, None) == -1
     assert b"amx_npg_apply_step" in lib.amx_last_error()
-    assert lib.amx_npg_reduce_cg_step(None, None, 1, 10, 4, None, 0.0, 0.0, None, None, None, None, None, None,
-                                      None) == -1
+    assert lib.amx_npg_cg_tail(None, None, 1, 10, 4, None, 0.0, 0.0, None, None, None, None, None, None, None,
+                               None, None) == -1
     assert lib.amx_npg_pass_ex(None, 1, 64, None, 1, 197, None, 1, 36, None, None, None, 32, None, None, None,
                                None) == -1
 

@@ -224,12 +224,13 @@ def test_npg_fvp_theta_cache_bit_identical(N):
         assert torch.equal(h0, h1), float((h0 - h1).abs().max())
 
 
-def test_npg_fused_reduce_cg_step_matches_separate():
-    """amx_npg_reduce_cg_step (the FVP partials' column sums + the CG vector step in one launch,
-    the step by the last-arriving block) against amx_npg_reduce + amx_npg_cg_step from the same
-    state, three iterations: the same h (the reduction's order is kept), p.z summed in block order
-    instead of the 1024-thread tree -- x, r, p within 1e-12 of the scale; the counter self-resets
-    (a second solve from the same start reproduces the first bit for bit)."""
+def test_npg_cg_tail_matches_separate():
+    """amx_npg_cg_tail (the FVP partials' column sums + the CG vector step in two launches spread
+    over the chip) against amx_npg_reduce + amx_npg_cg_step from the same state, three iterations:
+    the same h (the reduction's order is kept), p.z and r.r summed from fixed-order block parts
+    instead of the 1024-thread tree -- x, r, p within 1e-12 of the scale; a second solve from the
+    same start reproduces the first bit for bit (deterministic: every block forms the same v and
+    r.r); a stopped solve (tol above r.r) carries the stop over and leaves x, r, p untouched."""
     from amp_extensions_amd.policy import init_mlp_policy_params
     from amp_extensions_amd.npg import pack_policy, NPG_FVP
     S, A, N = 197, 36, 3000
@@ -240,23 +241,25 @@ def test_npg_fused_reduce_cg_step_matches_separate():
     c, lib, P = npg.ctx, npg.ctx.lib, npg.P
     b = torch.from_numpy(rs.randn(P)).to(DEV)
     curv = npg._ls_curvature()
-    work = torch.zeros(int(lib.amx_npg_reduce_cg_work(P)), dtype=torch.float64, device=DEV)
+    work = torch.empty(int(lib.amx_npg_cg_tail_work(P)), dtype=torch.float64, device=DEV)
 
-    def solve(fused):
-        x, r, p = (torch.empty(P, dtype=torch.float64, device=DEV) for _ in range(3))
+    def solve(fused, iters=3, tol=0.0):
+        x, r, p, r2 = (torch.empty(P, dtype=torch.float64, device=DEV) for _ in range(4))
         p32 = torch.empty(P, dtype=torch.float32, device=DEV)
-        st = torch.empty(2, dtype=torch.float64, device=DEV)
+        st, st2 = (torch.empty(2, dtype=torch.float64, device=DEV) for _ in range(2))
         assert lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(), p32.data_ptr(),
                                    st.data_ptr(), c.stream) == 0
-        for _ in range(3):
+        for _ in range(iters):
             if fused:
                 part = npg._pass(NPG_FVP, o, a, None, p32, gate=st, reduce=False)
-                assert lib.amx_npg_reduce_cg_step(c.h, part.data_ptr(), part.shape[0], P, A, curv.data_ptr(),
-                                                  npg.damping, 0.0, x.data_ptr(), r.data_ptr(), p.data_ptr(),
-                                                  p32.data_ptr(), st.data_ptr(), work.data_ptr(), c.stream) == 0
+                assert lib.amx_npg_cg_tail(c.h, part.data_ptr(), part.shape[0], P, A, curv.data_ptr(), npg.damping,
+                                           tol, x.data_ptr(), r.data_ptr(), r2.data_ptr(), p.data_ptr(),
+                                           p32.data_ptr(), st.data_ptr(), st2.data_ptr(), work.data_ptr(),
+                                           c.stream) == 0
+                r, r2, st, st2 = r2, r, st2, st
             else:
                 h = npg._pass(NPG_FVP, o, a, None, p32, gate=st)
-                assert lib.amx_npg_cg_step(c.h, P, A, h.data_ptr(), curv.data_ptr(), npg.damping, 0.0, x.data_ptr(),
+                assert lib.amx_npg_cg_step(c.h, P, A, h.data_ptr(), curv.data_ptr(), npg.damping, tol, x.data_ptr(),
                                            r.data_ptr(), p.data_ptr(), p32.data_ptr(), st.data_ptr(), c.stream) == 0
         torch.cuda.synchronize()
         return [t.cpu().double().numpy() for t in (x, r, p, st)]
@@ -266,6 +269,13 @@ def test_npg_fused_reduce_cg_step_matches_separate():
         assert close(v, u, 1e-12), np.abs(u - v).max()
     assert sep[3][1] == fus[3][1] and close(fus[3][:1], sep[3][:1], 1e-12)
     for u, v in zip(fus, fus2):
+        assert np.array_equal(u, v)
+    # early stop: with tol above the first r.r the first tail stops the solve; the later
+    # iterations (gated FVP passes, tails that only carry the state) change nothing
+    one = solve(True, iters=1, tol=1e300)
+    four = solve(True, iters=4, tol=1e300)
+    assert one[3][1] == 0.0 and four[3][1] == 0.0
+    for u, v in zip(one[:3], four[:3]):
         assert np.array_equal(u, v)
 
 
