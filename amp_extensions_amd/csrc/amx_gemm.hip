@@ -68,11 +68,6 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef OUT80
 #define OUT80 1
 #endif
-// OUT160 (A/B builds): 1 = the 160 x 224 output tile split over K in two (one workgroup per
-// CU) where its tiles are exactly half the CUs (5120 lanes x 4 members: the N = 4 / 8 shares)
-#ifndef OUT160
-#define OUT160 0
-#endif
 // RFF_OCC3 (A/B builds): 1 = the RFF pass on 128 x 128 tiles at three workgroups per CU (H128rff3)
 // when its tiles exceed one round at two per CU
 #ifndef RFF_OCC3
@@ -1572,10 +1567,6 @@ using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, tr
 // groups * rows / 80 == CUs (5120 lanes x 4 members: the N = 4 / 8 per-rank shares) -- no
 // stream-K partial tiles, the A panel read once
 using H80x224 = TileH3<1, 7, 1, 1, 1, 2, true, true, true, 5, 2, true, true, true, true>;  // + DEEPA
-// 160 x 224 output tiles, 14 waves of 80 x 32 (two row waves share each W fragment staged in LDS:
-// half the weight-panel bytes per MFMA of the 80-row tile), each tile's K range split in two
-// segments over one workgroup per CU (stream-K; the second segment's last arriver sums P0 + P1)
-using H160x224 = TileH3<2, 7, 1, 1, 1, 2, true, true, true, 5, 2, true, true, true, true>;  // + DEEPA
 
 
 // output layer, 256-row stream-K tiles (amx_set_out_tile 4): 8 waves of 64 x 112 on 16x16x32
@@ -2064,14 +2055,6 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
         return launch_h3<EPI_UNNORM, H256x224>(a, s);
       }
     }
-#if OUT160
-    if (rows % 160 == 0 && 2LL * groups * (rows / 160) == ctx->n_cus && ctx->split_scratch && ctx->split_cnt &&
-        ctx->split_ncnt >= groups * (rows / 160) &&
-        ctx->split_floats >= (long long)groups * (rows / 160) * 2 * 160 * 224) {
-      a.ksplit = 2; a.streamk = ctx->n_cus; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
-      return launch_h3<EPI_UNNORM, H160x224>(a, s);
-    }
-#endif
 #if OUT80
     if (rows % 80 == 0 && (long long)groups * (rows / 80) == ctx->n_cus) return launch_h3<EPI_UNNORM, H80x224>(a, s);
 #endif
@@ -2188,13 +2171,8 @@ extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, 
   nc = nc > nc_lb ? nc : nc_lb;
   const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
   const long long f2 = (long long)tiles2 * ksplit2 * 256 * 224;
-  // the 160-row output tiles split in two (OUT160)
-  const int tiles160 = rows % 160 == 0 && 2LL * groups * (rows / 160) == ctx->n_cus ? groups * (rows / 160) : 0;
-  const long long f160 = (long long)tiles160 * 2 * 160 * 224;
-  nc = nc > tiles160 ? nc : tiles160;
   if (n_counters) *n_counters = nc;
   long long f = fo > fh ? fo : fh;
   f = f > f2 ? f : f2;
-  f = f > f160 ? f : f160;
   return f > f_lb ? f : f_lb;
 }
