@@ -2169,9 +2169,9 @@ extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, 
   int nc = tiles > tiles_h ? tiles : tiles_h;
   nc = nc > tiles2 ? nc : tiles2;
   nc = nc > nc_lb ? nc : nc_lb;
+  if (n_counters) *n_counters = nc;
   const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
   const long long f2 = (long long)tiles2 * ksplit2 * 256 * 224;
-  if (n_counters) *n_counters = nc;
   long long f = fo > fh ? fo : fh;
   f = f > f2 ? f : f2;
   return f > f_lb ? f : f_lb;
