@@ -13,6 +13,9 @@ import re
 from . import _build
 
 _HEADER = os.path.join(_build.INCLUDE, "amx_hip.h")
+# entry points of include/amx_hip_experimental.h: bound only when the library was built with
+# AMX_EXPERIMENTAL=1 (the default library does not export them)
+EXPERIMENTAL = ("amx_set_lb_stage", "amx_assemble_input_limbs", "amx_gemm_bias_act_lb", "amx_gemm_out_unnorm_lb")
 
 c_int, c_ll, c_dbl, c_flt, c_u64, c_u32, vp = C.c_int, C.c_longlong, C.c_double, C.c_float, C.c_uint64, C.c_uint32, C.c_void_p
 ip = C.POINTER(C.c_int)
@@ -180,6 +183,8 @@ def load(path: str | None = None, build_if_missing: bool = False):
     except OSError as e:
         raise AmxNativeError(f"cannot load {path}: {e}") from e
     for name, (res, args) in SIGNATURES.items():
+        if name in EXPERIMENTAL and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -188,6 +193,11 @@ def load(path: str | None = None, build_if_missing: bool = False):
     if path == _build.LIB_PATH:
         _LIB = lib
     return lib
+
+
+def has_experimental(lib) -> bool:
+    """The library was built with AMX_EXPERIMENTAL=1 (the limb-format forward is present)."""
+    return all(hasattr(lib, n) for n in EXPERIMENTAL)
 
 
 def check(rc: int, what: str = "") -> None:

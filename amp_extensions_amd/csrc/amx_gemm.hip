@@ -65,6 +65,13 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #define H3_EXP 0
 #endif
 // OUT80 (A/B builds): 1 = the 80 x 224 output tile where it makes exactly one tile per CU
+// AMX_EXPERIMENTAL (build: AMX_EXPERIMENTAL=1 python -m amp_extensions_amd._build): the
+// measured-slower A/B alternates -- the LDS-DMA ring output tile (amx_set_out_tile 2 / 3), the
+// 256 x 224 stream-K output tile (4), the 128 x 256 RFF tile (RFF_TILE) and, in its own source
+// (experimental/amx_gemm_lb.hip), the limb-format forward.  Off in the shipped library.
+#ifndef AMX_EXPERIMENTAL
+#define AMX_EXPERIMENTAL 0
+#endif
 #ifndef OUT80
 #define OUT80 1
 #endif
@@ -1223,6 +1230,11 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
 
 // fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
 // [g][rows]: one wave per row (max |w| over K, then the split)
+#if AMX_EXPERIMENTAL
+#endif  // AMX_EXPERIMENTAL
+
+// fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
+// [g][rows]: one wave per row (max |w| over K, then the split)
 // ==== output layer on an LDS-DMA ring =======================================================
 // The output layer (N = S <= 240 columns, K = k0 + 4H = 2304) reads every activation row once
 // (277 MB per forward at 8192 lanes x 4 members), and its register-staged 128 x 224 tile
@@ -1569,9 +1581,11 @@ using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, tr
 using H80x224 = TileH3<1, 7, 1, 1, 1, 2, true, true, true, 5, 2, true, true, true, true>;  // + DEEPA
 
 
+#if AMX_EXPERIMENTAL
 // output layer, 256-row stream-K tiles (amx_set_out_tile 4): 8 waves of 64 x 112 on 16x16x32
 // (28 blocks); A + W fetched per FLOP 0.68x the 128 x 224 tile's
 using H256x224 = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 4, 7, true, true, true>;
+#endif
 using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
 using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 
@@ -1630,6 +1644,7 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   return AMX_OK;
 }
 
+#if AMX_EXPERIMENTAL
 template <class TL>
 int launch_ring(GemmArgs& a, hipStream_t stream) {
   a.tiles_m = a.rows / TL::BM;
@@ -1642,6 +1657,8 @@ int launch_ring(GemmArgs& a, hipStream_t stream) {
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
+
+#endif
 
 int check_common(const char* fn, int groups, int rows, int K, const float* A, int lda, const float* W,
                  int ldw) {
@@ -2017,6 +2034,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   // 13..15; 3: 8 waves of 32 x 112; measured slower than the register-staged tile):
   // one tile per workgroup, or stream-K at the lane counts whose 128-row tiles are fewer than
   // the CUs (streamk_tiles), as the register-staged tile
+#if AMX_EXPERIMENTAL
   const int nb16 = (n_valid + 15) / 16;
   const int ring = (ctx->out_tile != 2 && ctx->out_tile != 3) || K % 32 != 0 || nb16 < 13 || nb16 > 15 ? 0
                    : ctx->out_tile == 3 ? (nb16 <= 14 ? 3 : 0) : 2;
@@ -2036,6 +2054,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
       default: return launch_ring<TileRing<8, 1, 1, 15>>(a, s);
     }
   }
+#endif
   // weight rows padded to round_up(S, 128) (amx_layout n_out_pad); S <= 224 runs one 224-wide tile
   const int n32 = amx::round_up(n_valid, 32);
   // one wave of row-block tiles RB x (N/2) when rows = RB * n_cus / (2 groups), RB in {128..224}
@@ -2046,6 +2065,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
+#if AMX_EXPERIMENTAL
     if (ctx->out_tile == 4) {  // 256 x 224 tiles, stream-K over the CUs
       int nwg = 0, ksplit = 0;
       const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K, 256);
@@ -2055,6 +2075,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
         return launch_h3<EPI_UNNORM, H256x224>(a, s);
       }
     }
+#endif
 #if OUT80
     if (rows % 80 == 0 && (long long)groups * (rows / 80) == ctx->n_cus) return launch_h3<EPI_UNNORM, H80x224>(a, s);
 #endif
@@ -2119,7 +2140,7 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
 #if RFF_OCC3
     if ((long long)(rows / 128) * (F / 128) > 2LL * ctx->n_cus) return launch_h3<EPI_RFF, H128rff3>(a, (hipStream_t)stream);
 #endif
-#if RFF_TILE == 1
+#if AMX_EXPERIMENTAL && RFF_TILE == 1
     if (F % 256 == 0 && (rows / 128) * (F / 256) >= ctx->n_cus) return launch_h3<EPI_RFF, H128x256>(a, (hipStream_t)stream);
 #endif
     return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
@@ -2135,7 +2156,11 @@ extern "C" int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf) {
 
 extern "C" int amx_set_out_tile(amx_ctx* ctx, int tile) {
   AMX_CHECK_ARG(ctx, "amx_set_out_tile: null ctx");
+#if AMX_EXPERIMENTAL
   AMX_CHECK_ARG(tile >= 0 && tile <= 4, "amx_set_out_tile: tile=%d not in 0..4", tile);
+#else
+  AMX_CHECK_ARG(tile >= 0 && tile <= 1, "amx_set_out_tile: tile=%d (2-4 need an AMX_EXPERIMENTAL=1 build)", tile);
+#endif
   ctx->out_tile = tile;
   return AMX_OK;
 }
@@ -2160,12 +2185,14 @@ extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, 
                           ? streamk_hidden(ctx, groups, rows, ctx->H, ctx->k0_pad + (ctx->L - 1) * ctx->H, &nwg_h,
                                            &ksplit_h)
                           : 0;
+  int nwg2 = 0, ksplit2 = 0, tiles2 = 0, nc_lb = 0;
+  long long f_lb = 0;
+#if AMX_EXPERIMENTAL
   // the 256-row output tiles (amx_set_out_tile 4)
-  int nwg2 = 0, ksplit2 = 0;
-  const int tiles2 = streamk_tiles(ctx, groups, rows, &nwg2, &ksplit2, ctx->k0_pad + ctx->L * ctx->H, 256);
-  // the limb-format forward's stream-K shapes (amx_gemm_lb.hip)
-  int nc_lb = 0;
-  const long long f_lb = amx::lb_split_floats(ctx, groups, rows, &nc_lb);
+  tiles2 = streamk_tiles(ctx, groups, rows, &nwg2, &ksplit2, ctx->k0_pad + ctx->L * ctx->H, 256);
+  // the limb-format forward's stream-K shapes (experimental/amx_gemm_lb.hip)
+  f_lb = amx::lb_split_floats(ctx, groups, rows, &nc_lb);
+#endif
   int nc = tiles > tiles_h ? tiles : tiles_h;
   nc = nc > tiles2 ? nc : tiles2;
   nc = nc > nc_lb ? nc : nc_lb;

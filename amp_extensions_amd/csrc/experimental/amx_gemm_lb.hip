@@ -1,5 +1,6 @@
-// The ensemble's dense-connect forward on limb-format activations ("lb" = limbs), the default
-// f16x3 path of DeviceEnsemble (milo/milo/dynamics.py:216-233, 422-433: BasicMLP's hidden
+// EXPERIMENTAL (built only with AMX_EXPERIMENTAL=1: measured slower than the f32-format forward,
+// DESIGN.md section 6 round 4).  The ensemble's dense-connect forward on limb-format activations
+// ("lb" = limbs), DeviceEnsemble(act_format="limbs") (milo/milo/dynamics.py:216-233, 422-433: BasicMLP's hidden
 // layers write relu(x W^T + b) as a new column slice of the concatenated row, the output layer
 // reads the whole row).
 //
@@ -30,6 +31,7 @@
 // Same three limb products per 16x16x32 block and K-tile as h3_tile: (a1,b0), (a0,b1), (a0,b0).
 #include "amx_common.h"
 #include "amx_h3.h"
+#include "amx_hip_experimental.h"
 
 #include <type_traits>
 

@@ -169,6 +169,9 @@ class DeviceEnsemble:
         if act_format == "limbs" and not lb_ok:
             raise ValueError("act_format='limbs' needs gemm='f16x3', a hidden width that is a multiple of 256, "
                              "S + A <= 1024 and at most 23 hidden chunks of 128 columns")
+        if act_format == "limbs" and not N.has_experimental(ctx.lib):
+            raise N.AmxNativeError("act_format='limbs' is an experimental A/B path: rebuild the library with "
+                                   "AMX_EXPERIMENTAL=1 python -m amp_extensions_amd._build")
         self.limbs = act_format == "limbs"
         # exponent slots per row: f32 format x0, h0 .. h_{L-1}; limbs x0 + one per 128 hidden columns
         self.n_slots = 1 + ctx.L * ctx.Hp // 128 if self.limbs else ctx.L + 1

@@ -82,9 +82,10 @@ def parse():
                         "the 16-bit MFMA pipe (both fp32-level error), or f32 MFMA")
     p.add_argument("--act-format", choices=["f32", "limbs"], default="f32",
                    help="f16x3 activation rows: f32 (split by every consumer, amx_gemm_*_h3; default) or limbs "
-                        "(split once by the producer, amx_gemm_*_lb; measured slower, DESIGN §6 round 4)")
+                        "(split once by the producer, amx_gemm_*_lb; measured slower, DESIGN §6 round 4; needs a "
+                        "library built with AMX_EXPERIMENTAL=1)")
     p.add_argument("--lb-stage", type=int, choices=[0, 1], default=0,
-                   help="limb forward's K-loop staging: 0 registers, 1 LDS-DMA (A/B)")
+                   help="limb forward's K-loop staging: 0 registers, 1 LDS-DMA (A/B; AMX_EXPERIMENTAL=1 build)")
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)

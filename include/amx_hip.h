@@ -195,39 +195,6 @@ int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int 
                            const int* row_exp, long long strideRexp, int rexp_slots, int k_shared,
                            void* stream);
 
-/* Limb-format activations (the default f16x3 ensemble forward, csrc/amx_gemm_lb.hip): every
- * activation row is stored as scaled fp16 limb pairs in the fp32 row's bytes -- granules of 16
- * columns [limb0 16 x f16 | limb1 16 x f16], value = (limb0 + limb1) * 2^(E - 14) -- with one
- * exponent E per row and chunk: slot 0 = the x0 slice [0, k0), slot c >= 1 = columns
- * [k0 + 128 (c - 1), k0 + 128 c) of the hidden slices (row_exp [g][slots][rexp_ld]).  Each value
- * is split once, by its producer; the consumer's K loop copies bytes (LDS-DMA) and rescales its
- * fp32 accumulators by 2^(E_prev - E_next) at chunk boundaries.
- * amx_assemble_input_limbs: x0 (amx_assemble_input's values, dynamics.py:225-227) as limbs +
- * slot 0 of every model (stride_m 0: one copy in model 0's rows, read by every model through
- * k_shared = k0). */
-int amx_assemble_input_limbs(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
-                             long long stride_m, int ldk, int B, int* row_exp, long long strideRexp,
-                             void* stream);
-/* A/B option of the limb forward's K loop: 0 (default) register-staged, 1 LDS-DMA (slower). */
-int amx_set_lb_stage(amx_ctx* ctx, int stage);
-/* One dense-connect hidden layer of every member (BasicMLP.forward, dynamics.py:427-430) on
- * limb-format rows: reads columns [0, K) (chunks 0 .. (K - k0)/128), writes relu(x W^T + b) as
- * limbs into columns [col_off, col_off + N) and their chunk exponents into row_exp_out (the
- * slot of the first output chunk, group 0; strideRexp / rexp_ld as row_exp).  W2 / w_exp:
- * amx_split_f16x2 images.  k_shared: 0 or k0 (x0 read from group 0's rows). */
-int amx_gemm_bias_act_lb(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
-                         long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
-                         long long strideWexp, const float* bias, long long strideBias, float* C, int ldc,
-                         long long strideC, int col_off, int act, const int* row_exp, long long strideRexp,
-                         long long rexp_ld, int* row_exp_out, int k0, int k_shared, void* stream);
-/* The output layer + un-normalisation (DynamicsModel.forward, dynamics.py:228-232) on
- * limb-format rows: preds = (x W^T + b) * sd_d + mu_d, fp32. */
-int amx_gemm_out_unnorm_lb(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A, int lda,
-                           long long strideA, const uint16_t* W2, long long strideW2, const int* w_exp,
-                           long long strideWexp, const float* bias, long long strideBias, float* preds, int ldp,
-                           long long strideP, const int* row_exp, long long strideRexp, long long rexp_ld, int k0,
-                           int k_shared, void* stream);
-
 /* f16x3 form of amx_rff_features (RBFLinearCost.get_rep, milo/milo/linear_cost.py:64-71):
  * W2/w_exp = amx_split_f16x2 image of the [F][K] RFF weight, row_exp [rows] = exponents of x's
  * rows (amx_step_rexp, or amx_row_exponents with one slot); same epilogue and outputs. */
@@ -516,7 +483,9 @@ int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint
  * limb products per 16 x 16 block in the same K order over the same stream-K segments.
  * 4 = 256 x 224 tiles, stream-K over the CUs at every lane count whose 256-row tiles are fewer
  * than the CUs (S in 129..224, needs the split workspace, which amx_split_workspace_floats also
- * sizes for it): different K segments, so equal to 1 to fp32 rounding, not bit for bit. */
+ * sizes for it): different K segments, so equal to 1 to fp32 rounding, not bit for bit.
+ * Tiles 2-4 are measured slower and exist only in an AMX_EXPERIMENTAL=1 build
+ * (amx_hip_experimental.h); the default library accepts 0 and 1 and refuses 2-4. */
 int amx_set_out_tile(amx_ctx* ctx, int tile);
 
 /* Floats to allocate for the packed policy weight image for hidden widths H1, H2 (host query;

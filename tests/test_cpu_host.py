@@ -25,8 +25,13 @@ def test_library_exports_every_header_symbol(lib):
     raw = ctypes.CDLL(_build.LIB_PATH)
     for s in syms:
         assert hasattr(raw, s), s
-    # the Python binding declares exactly the header's functions
-    assert sorted(_native.SIGNATURES) == syms
+    # the Python binding declares exactly the header's functions, plus the experimental
+    # header's (bound only when the library was built with AMX_EXPERIMENTAL=1)
+    exp = _native.header_symbols(os.path.join(_build.INCLUDE, "amx_hip_experimental.h"))
+    assert sorted(exp) == sorted(_native.EXPERIMENTAL) and not set(exp) & set(syms)
+    assert sorted(_native.SIGNATURES) == sorted(syms + exp)
+    # the shipped library is the default build: the experimental entry points are not exported
+    assert not any(hasattr(raw, s) for s in exp) or _build.EXPERIMENTAL
 
 
 def test_library_is_gfx950_code_object():

@@ -13,7 +13,8 @@ import torch
 
 from oracle import milo_ref as R
 
-pytestmark = pytest.mark.gpu
+# experimental A/B path: runs against an AMX_EXPERIMENTAL=1 build, skipped on the shipped library
+pytestmark = [pytest.mark.gpu, pytest.mark.experimental]
 DEV = "cuda"
 
 
