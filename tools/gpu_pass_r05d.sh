@@ -21,3 +21,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r05d_5
 done
 cd "$R"
 for g in on off; do python tools/trace_timeline.py gpurun_out/prof_r05d_5k_$g/run_kernel_trace.csv > gpurun_out/r05d_timeline_5k_$g.txt; tail -12 gpurun_out/r05d_timeline_5k_$g.txt; done
+bash tools/ab_bench.sh "t0 t1 f1" 3 --steps 20 --warmup 5 | tee gpurun_out/r05d_trans_ab_8k.txt
+bash tools/ab_bench.sh "t0 t1 f1" 3 --total-samples 5000 --expert-rows 6250 --steps 50 --warmup 10 | tee gpurun_out/r05d_trans_ab_5k.txt
