@@ -38,6 +38,7 @@ class ResetNoise(C.Structure):
 
 
 AMX_NOISE_ROT_SLOTS = 48
+RFF_PART_ROWS = 32  # AMX_RFF_PART_ROWS: rows per fp64 column partial of the RFF features
 
 # name -> (restype, argtypes); must match include/amx_hip.h exactly.
 SIGNATURES = {

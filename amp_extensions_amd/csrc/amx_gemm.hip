@@ -46,6 +46,11 @@ struct Tile {
 
 // LDS of the RFF epilogue: the staged BM x (BN + 4) f32 tile
 constexpr size_t rff_epi_lds(int bm, int bn) { return (size_t)bm * (bn + 4) * 4; }
+// rows of the M16 RFF epilogue's staging pass: the whole tile when its [BM][BN + 4] floats fit
+// 80 KB, else the largest multiple of 32 rows that does (the 160 x 256 tile: 64 rows)
+constexpr int rff_m16_rows(int bm, int bn) {
+  return rff_epi_lds(bm, bn) <= 80 * 1024 ? bm : (int)((80 * 1024) / ((size_t)(bn + 4) * 4 * 32)) * 32;
+}
 
 // ---- epilogue (shared by the f32 and the bf16x6 main loops: the 32x32 C/D register map
 // is dtype-independent on gfx950) ---------------------------------------------------------
@@ -169,15 +174,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
     // The staged epilogue below in two passes of the 64 rows of one wave row (wm = pass), so
     // the staging takes 64 x 132 floats (33.8 KB) and the tile's 41.5 KB of BK-16 stage
     // buffers set the LDS: three workgroups per CU.  Thread (c, part): column c, rows
-    // 32 part .. + 31 of each pass; its fp64 sum runs over pass 0's rows, then pass 1's, and
-    // the two parts are added in part order (deterministic).
+    // 32 part .. + 31 of each pass: one fp64 partial per 32-row group (AMX_RFF_PART_ROWS),
+    // summed in row order.
     static_assert(BM == 128 && BN == 128 && TL::NT == 256 && TL::WM == 2 && TM * 32 == 64, "RFF half epilogue");
     constexpr int CLD = BN + 4;
     float* Cs = smem;  // [64][CLD]
     const int c = t & (BN - 1), part = t / BN;
     const int col = tn * BN + c;
     const float bv = a.bias[col];
-    double csum = 0.0;
     float* Cg = a.C;
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
@@ -192,31 +196,30 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
               Cs[r * CLD + wn * TN * 32 + n * 32 + li] = acc[m][n][e];
             }
       }
-      const uint64_t vmask = row_valid_mask(a, tm * BM + pass * 64 + part * 32, 32);
+      const int row0 = tm * BM + pass * 64 + part * 32;
+      const uint64_t vmask = row_valid_mask(a, row0, 32);
       __syncthreads();
+      double csum = 0.0;
 #pragma unroll 8
       for (int i = 0; i < 32; ++i) {
         const int r = part * 32 + i;
-        const int row = tm * BM + pass * 64 + r;
         const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
         const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
-        Cg[(long long)row * a.ldc + col] = phi;
+        Cg[(long long)(row0 + i) * a.ldc + col] = phi;
         csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
       }
+      a.col_partials[(long long)(row0 / AMX_RFF_PART_ROWS) * a.N + col] = csum;
       __syncthreads();
     }
-    double* red = reinterpret_cast<double*>(smem);  // [2][BN]
-    red[part * BN + c] = csum;
-    __syncthreads();
-    if (part == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[BN + c];
   } else {  // EPI_RFF (128 x 128 or 128 x 64 tiles of 256 threads)
     static_assert(BM == 128 && (BN == 128 || BN == 64) && TL::NT == 256, "RFF epilogue tiles");
     // Stage the raw BM x BN tile through LDS, then one column per thread over BM / PARTS rows:
     // coalesced phi rows, the cos of 8 rows in flight (unroll 8: 94-101 vs 102-112 us for the
-    // 40 960-row pass, same bits; full unrolling is slower), and the fp64 column sum of the
-    // valid rows in fixed row order, the PARTS part sums added in part order (deterministic;
-    // 2 parts at BN 128, 4 at BN 64).
+    // 40 960-row pass, same bits; full unrolling is slower), and one fp64 partial per 32-row
+    // group (AMX_RFF_PART_ROWS) of the valid rows in row order (2 groups per thread at BN 128,
+    // 1 at BN 64).
     constexpr int CLD = BN + 4, PARTS = 256 / BN, PR = BM / PARTS;
+    static_assert(PR % AMX_RFF_PART_ROWS == 0, "whole partial groups per thread");
     float* Cs = smem;  // [BM][CLD] (rff_epi_lds), reuses the stage buffers (last barrier passed)
 #pragma unroll
     for (int n = 0; n < TN; ++n)
@@ -234,32 +237,26 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x16 (&acc)[TL::TM
     __syncthreads();
     const int col = tn * BN + c;
     const float bv = a.bias[col];
-    double csum = 0.0;
     float* Cg = a.C;
+#pragma unroll
+    for (int q = 0; q < PR / AMX_RFF_PART_ROWS; ++q) {
+      double csum = 0.0;
 #pragma unroll 8
-    for (int i = 0; i < PR; ++i) {
-      const int r = part * PR + i;
-      const int row = tm * BM + r;
-      const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
+      for (int i = q * AMX_RFF_PART_ROWS; i < (q + 1) * AMX_RFF_PART_ROWS; ++i) {
+        const int r = part * PR + i;
+        const int row = tm * BM + r;
+        const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
 #if RFF_EXP == 1
-      const float phi = z * a.rff_scale;
+        const float phi = z * a.rff_scale;
 #else
-      const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
+        const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
 #endif
 #if RFF_EXP != 2
-      Cg[(long long)row * a.ldc + col] = phi;
+        Cg[(long long)row * a.ldc + col] = phi;
 #endif
-      csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
-    }
-    __syncthreads();
-    double* red = reinterpret_cast<double*>(smem);  // [PARTS][BN]
-    red[part * BN + c] = csum;
-    __syncthreads();
-    if (part == 0) {
-      double sum = red[c];
-#pragma unroll
-      for (int q = 1; q < PARTS; ++q) sum += red[q * BN + c];
-      a.col_partials[(long long)tm * a.N + col] = sum;
+        csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
+      }
+      a.col_partials[(long long)((tm * BM + part * PR) / AMX_RFF_PART_ROWS + q) * a.N + col] = csum;
     }
   }
 }
@@ -694,10 +691,13 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
   const int* wexp = a.w_exp + (long long)g * a.strideWexp;
   float* Cg = a.C + (long long)g * a.strideC;
   if constexpr (EPI == EPI_RFF) {  // the 32x32 path's RFF epilogue on the 16x16 accumulator layout
-    // 128 x 128 tiles of 256 threads or 128 x 256 tiles of 512: one column per thread, two halves
-    // of 64 rows (the 128-row block's partial sums: col_partials[row / 128][f])
-    constexpr int BN = TL::BN, CLD = BN + 4;
-    static_assert(TL::BM == 128 && (BN == 128 || BN == 256) && TL::NT == 2 * BN, "RFF epilogue tiles");
+    // The tile staged through LDS in passes of RP rows (all of it when it fits the launch's
+    // LDS, rff_m16_rows), then one column per thread: the NT / BN threads of a column take the
+    // 32-row groups g = part, part + NT / BN, ... (wave-uniform: BN >= 64), each group's phi
+    // rows coalesced and its fp64 partial (AMX_RFF_PART_ROWS) summed in row order.
+    constexpr int BM = TL::BM, BN = TL::BN, CLD = BN + 4, P = TL::NT / BN, RP = rff_m16_rows(BM, BN);
+    static_assert(TL::NT % BN == 0 && BN >= 64 && BM % AMX_RFF_PART_ROWS == 0 && RP % AMX_RFF_PART_ROWS == 0 &&
+                      RP % 16 == 0, "RFF epilogue tiles");
     // un-scale in place (exact powers of two) while sExp (in the stage area) is readable
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
@@ -711,36 +711,41 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
         acc[m][n][3] = __builtin_amdgcn_ldexpf(acc[m][n][3], ev.w + ec);
       }
     }
-    __syncthreads();
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    float* Cs = smem;  // [128][CLD] over the stage buffers
-#pragma unroll
-    for (int m = 0; m < MB; ++m)
-#pragma unroll
-      for (int n = 0; n < NB; ++n)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          Cs[(lrow0 + m * 16 + 4 * lq + j) * CLD + wn * TL::WCOLS + n * 16 + lc] = acc[m][n][j];
-    const int t = threadIdx.x, c = t % BN, half = t / BN;
-    const uint64_t vmask = row_valid_mask(a, tm * 128 + half * 64, 64);  // as the 32x32 path's epilogue
-    __syncthreads();
+    float* Cs = smem;  // [RP][CLD] over the stage buffers
+    const int t = threadIdx.x, c = t % BN, part = t / BN;
     const int col = tn * BN + c;
     const float bv = a.bias[col];
-    double csum = 0.0;
-#pragma unroll 2
-    for (int i = 0; i < 64; ++i) {
-      const int r = half * 64 + i;
-      const int row = tm * 128 + r;
-      const float z = Cs[r * CLD + c] + bv;       // nn.Linear: x W^T + b
-      const float phi = rff_cos(z) * a.rff_scale;  // torch.cos(.) * np.sqrt(2/F)
-      a.C[(long long)row * a.ldc + col] = phi;
-      csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
+#pragma unroll
+    for (int r0 = 0; r0 < BM; r0 += RP) {
+      __syncthreads();  // the stage buffers (or the previous pass) are free
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+        const int rb = lrow0 + m * 16;  // a 16-row block lies wholly in one pass (RP % 16 == 0)
+        if (rb >= r0 && rb < r0 + RP) {
+#pragma unroll
+          for (int n = 0; n < NB; ++n)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              Cs[(rb - r0 + 4 * lq + j) * CLD + wn * TL::WCOLS + n * 16 + lc] = acc[m][n][j];
+        }
+      }
+      __syncthreads();
+      constexpr int GP = (RP < BM ? RP : BM) / AMX_RFF_PART_ROWS;  // groups per pass
+      for (int gl = part; gl < GP && r0 + gl * AMX_RFF_PART_ROWS < BM; gl += P) {
+        const int row0 = tm * BM + r0 + gl * AMX_RFF_PART_ROWS;
+        const uint64_t vmask = row_valid_mask(a, row0, AMX_RFF_PART_ROWS);
+        double csum = 0.0;
+#pragma unroll 8
+        for (int i = 0; i < AMX_RFF_PART_ROWS; ++i) {
+          const float z = Cs[(gl * AMX_RFF_PART_ROWS + i) * CLD + c] + bv;  // nn.Linear: x W^T + b
+          const float phi = rff_cos(z) * a.rff_scale;                       // torch.cos(.) * np.sqrt(2/F)
+          a.C[(long long)(row0 + i) * a.ldc + col] = phi;
+          csum += ((vmask >> i) & 1u) ? (double)phi : 0.0;
+        }
+        a.col_partials[(long long)(row0 / AMX_RFF_PART_ROWS) * a.N + col] = csum;
+      }
     }
-    __syncthreads();
-    double* red = reinterpret_cast<double*>(smem);
-    if (half == 1) red[c] = csum;
-    __syncthreads();
-    if (half == 0) a.col_partials[(long long)tm * a.N + col] = csum + red[c];
     return;
   }
   if constexpr (EPI == EPI_BIAS_ACT) {
@@ -1574,6 +1579,13 @@ using H128rff3 = TileH3<2, 2, 2, 2, 3, 1>;
 // the workgroups; the same column-partial layout [rows / 128][F])
 using H128x64k32 = TileH3<4, 1, 1, 2, 2, 2>;
 using H128 = TileH3<2, 2, 2, 2>;  // K not a multiple of 32 (BK 16)
+// RFF features on 160-row tiles (32-row column partials, AMX_RFF_PART_ROWS): 160 x 256, 8 waves
+// of 80 x 64 (the 5120-lane hidden tile's waves), one per CU -- 40 960 rows x 512 features are
+// 512 tiles, exactly two rounds (the 128 x 128 tiles at three per CU: 1280 in 1.67 rounds):
+// 88.5 -> 76.2 us under rocprofv3, same box (profiles/r05e_rff160_ab.txt).  (A 160 x 64 tile,
+// 4 waves of 80 x 32 at two per CU -- 5120 rows in one round of 256 tiles -- took 25.1 us
+// against the 128 x 64 tile's 23.1 and was dropped.)
+using H160x256r = TileH3<2, 4, 1, 1, 1, 2, true, true, true, 5, 4, true, true, true>;
 using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, true, true>;  // + DEEPA (-2 %)
 // 80 x 224 output tiles, 7 waves of 80 x 32 (16x16x32 form, split schedule): one tile per CU when
 // groups * rows / 80 == CUs (5120 lanes x 4 members: the N = 4 / 8 per-rank shares) -- no
@@ -1636,8 +1648,11 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   const int tiles = a.tiles_m * a.tiles_n * a.groups;
   const int nwg = a.streamk ? a.streamk : tiles;  // stream-K: a.streamk workgroups
   if (tiles == 0) return AMX_OK;
-  // (the three-per-CU RFF tile stages its epilogue in two 64-row passes)
-  constexpr size_t rff_lds = TL::OCC >= 3 ? rff_epi_lds(TL::BM / 2, TL::BN) : rff_epi_lds(TL::BM, TL::BN);
+  // (the three-per-CU RFF tile stages its epilogue in two 64-row passes, the M16 tiles in
+  // passes of rff_m16_rows)
+  constexpr size_t rff_lds = TL::M16      ? rff_epi_lds(rff_m16_rows(TL::BM, TL::BN), TL::BN)
+                             : TL::OCC >= 3 ? rff_epi_lds(TL::BM / 2, TL::BN)
+                                            : rff_epi_lds(TL::BM, TL::BN);
   constexpr size_t lds = (EPI == EPI_RFF && TL::LDS < rff_lds) ? rff_lds : TL::LDS;
   hipLaunchKernelGGL((k_gemm_h3<EPI, TL>), dim3(nwg), dim3(TL::NT), lds, stream, a);
   AMX_CHECK_LAUNCH();
@@ -2135,6 +2150,9 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
   a.rows = rows; a.N = F; a.K = K; a.groups = 1;
   a.n_valid = n_valid; a.rff_scale = scale; a.col_partials = col_partials; a.row_mask = row_mask;
   if (K % 32 == 0) {
+    // 160 x 256 tiles where they fill the CUs in whole rounds (see H160x256r)
+    if (rows % 160 == 0 && F % 256 == 0 && ((long long)(rows / 160) * (F / 256)) % ctx->n_cus == 0)
+      return launch_h3<EPI_RFF, H160x256r>(a, (hipStream_t)stream);
     // (at 40 960 rows the 128 x 128 tile is faster: 121 vs 145 us under the profiler)
     if ((rows / 128) * (F / 128) < ctx->n_cus && F % 64 == 0) return launch_h3<EPI_RFF, H128x64k32>(a, (hipStream_t)stream);
 #if RFF_OCC3

@@ -454,10 +454,14 @@ class RffMap:
     def features(self, x: torch.Tensor, rows: int, n_valid: int, phi: torch.Tensor, partials: torch.Tensor,
                  row_mask: torch.Tensor | None = None, ldx: int | None = None,
                  row_exp: torch.Tensor | None = None) -> None:
-        """phi rows + fp64 column partials of x's `rows` rows.  f16x3: `row_exp` [rows] int32 =
-        the rows' exponents (amx_step_rexp writes them for the rollout's [s, s'] rows); None
-        computes them here (amx_row_exponents)."""
+        """phi rows + fp64 column partials [rows / 32][F] (one per 32-row group, AMX_RFF_PART_ROWS)
+        of x's `rows` rows.  f16x3: `row_exp` [rows] int32 = the rows' exponents (amx_step_rexp
+        writes them for the rollout's [s, s'] rows); None computes them here (amx_row_exponents)."""
         c = self.ctx
+        if partials.dtype != torch.float64 or partials.numel() < rows // N.RFF_PART_ROWS * self.F:
+            raise ValueError(f"partials must be fp64 with room for [{rows // N.RFF_PART_ROWS}][{self.F}] "
+                             f"(one row per {N.RFF_PART_ROWS} feature rows), got {tuple(partials.shape)} "
+                             f"{partials.dtype}")
         ldx = self.Kp if ldx is None else ldx
         if self.W2 is not None:
             if row_exp is None:
@@ -490,9 +494,9 @@ class RffMap:
         xp = torch.zeros(rows, self.Kp, dtype=torch.float32, device=c.device)
         xp[:n, :self.D] = x.to(c.device, torch.float32)
         phi = torch.empty(rows, self.F, dtype=torch.float32, device=c.device)
-        part = torch.empty(rows // 128, self.F, dtype=torch.float64, device=c.device)
+        part = torch.empty(rows // N.RFF_PART_ROWS, self.F, dtype=torch.float64, device=c.device)
         self.features(xp, rows, n, phi, part)
         tot = torch.empty(self.F, dtype=torch.float64, device=c.device)
-        N.check(c.lib.amx_sum_partials(c.h, part.data_ptr(), rows // 128, self.F, tot.data_ptr(), c.stream),
+        N.check(c.lib.amx_sum_partials(c.h, part.data_ptr(), rows // N.RFF_PART_ROWS, self.F, tot.data_ptr(), c.stream),
                 "amx_sum_partials")
         return phi[:n], tot

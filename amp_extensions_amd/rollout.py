@@ -131,7 +131,7 @@ class RolloutEngine:
             self.cost_rexp = z(K, Bp, dt=torch.int32)
         if isinstance(cost, RBFLinearCost):
             self.phi = z(K, Bp, cost.feature_dim)
-            self.partials = z(K, Bp // 128, cost.feature_dim, dt=torch.float64)
+            self.partials = z(K, Bp // N.RFF_PART_ROWS, cost.feature_dim, dt=torch.float64)
         self.t = 0              # steps taken in the current rollout
         self.step_counter = 0   # global step counter (policy RNG stream)
         # graph mode: the counter of a captured rollout's step t is dev_step[0] + t, and the graph
@@ -399,7 +399,7 @@ class RolloutEngine:
             if self.cost_rexp is not None and self.cost_type == "ss":
                 rexp = self.cost_rexp[t0:t1].view(rows)
             cost.map.features(x, rows, rows, self.phi[t0:t1].view(rows, -1),
-                              self.partials[t0:t1].view(rows // 128, -1), row_mask=mask, row_exp=rexp)
+                              self.partials[t0:t1].view(rows // N.RFF_PART_ROWS, -1), row_mask=mask, row_exp=rexp)
         elif isinstance(cost, GAILCost):
             rexp = None
             if self.cost_rexp is not None and self.cost_type == "ss":
@@ -435,7 +435,7 @@ class RolloutEngine:
         message); phi_sum is a view of its first F slots."""
         self.score()
         c, cost = self.ctx, self.cost
-        n_parts = self.t * (self.Bp // 128)
+        n_parts = self.t * (self.Bp // N.RFF_PART_ROWS)
         N.check(c.lib.amx_feature_message(c.h, self.partials.data_ptr(), n_parts, cost.feature_dim,
                                           float(self.t * self.B), self._fbuf.data_ptr(), c.stream),
                 "amx_feature_message")

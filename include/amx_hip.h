@@ -504,11 +504,17 @@ int amx_policy_pack(amx_ctx* ctx, const float* W1, const float* b1, int H1, cons
 
 /* ---- MILO RFF MMD cost -------------------------------------------------------- */
 
+/* Rows per fp64 column partial of the RFF features (round 5: 32, was 128): col_partials has
+ * rows / AMX_RFF_PART_ROWS rows, so the feature pass may use 160- and 80-row tiles that fill the
+ * CUs in whole rounds (40 960 rows: 512 tiles of 160 x 256; 5 120 rows: 256 tiles of 160 x 64). */
+#define AMX_RFF_PART_ROWS 32
+
 /* RBFLinearCost.get_rep (milo/milo/linear_cost.py:64-71) on MFMA:
  * phi[r][f] = cos(sum_k x[r][k] W[f][k] + b[f]) * scale, scale = (float)sqrt(2/F),
- * plus fp64 column sums of the tile's valid rows (r < n_valid and (row_mask==NULL or
- * row_mask[r])) into col_partials[r/128][f] — the per-rank share of the global
- * feature mean of fit_cost (:84-94).  rows % 128 == 0, F % 128 == 0. */
+ * plus fp64 column sums of each 32-row group's valid rows (r < n_valid and (row_mask==NULL or
+ * row_mask[r])) into col_partials[r/AMX_RFF_PART_ROWS][f] — the per-rank share of the global
+ * feature mean of fit_cost (:84-94); amx_feature_message / amx_sum_partials add the
+ * rows / AMX_RFF_PART_ROWS partial rows in order.  rows % 128 == 0, F % 128 == 0. */
 int amx_rff_features(amx_ctx* ctx, int rows, int n_valid, int F, int K, const float* x, int ldx,
                      const float* W, int ldw, const float* b, float scale, float* phi, int ldphi,
                      double* col_partials, const uint8_t* row_mask, void* stream);

@@ -247,7 +247,7 @@ def test_f16x3_rff_features_in_rollout():
     rows = K * eng.Bp
     x = eng.cost_in[:K].reshape(rows, -1)
     phi2 = torch.empty_like(eng.phi[:K].reshape(rows, -1))
-    part2 = torch.empty_like(eng.partials[:K].reshape(rows // 128, -1))
+    part2 = torch.empty_like(eng.partials[:K].reshape(rows // 32, -1))
     cost.map.features(x, rows, rows, phi2, part2)  # exponents recomputed in a separate pass
     torch.cuda.synchronize()
     phi = eng.phi[:K].reshape(rows, -1)
@@ -259,7 +259,7 @@ def test_f16x3_rff_features_in_rollout():
     arg = np.abs(xd) @ np.abs(W).T
     err = np.abs(phi.double().cpu().numpy() - ref) / np.sqrt(2.0 / 512)
     assert (err <= 4e-7 * arg + 1e-6).all(), float((err - 4e-7 * arg).max())
-    got = eng.partials[:K].reshape(rows // 128, -1).double().sum(0).cpu().numpy()
+    got = eng.partials[:K].reshape(rows // 32, -1).double().sum(0).cpu().numpy()
     np.testing.assert_allclose(got, phi.double().cpu().numpy().sum(0), rtol=1e-9, atol=1e-9)
 
 
@@ -363,14 +363,15 @@ def test_output_stream_k_deterministic_and_close_to_unsplit(B):
     assert d <= 1e-6 * max(1.0, p0.abs().max().item()), d
 
 
-@pytest.mark.parametrize("rows", [40960, 21504, 20480, 10240, 5120])
+@pytest.mark.parametrize("rows", [40960, 21504, 20480, 12288, 10240, 5120, 2048])
 def test_rff_features_every_tile_shape(rows):
-    """amx_rff_features_h3 on each of its tiles -- 40 960 / 21 504 / 20 480 / 10 240 rows: 128 x 128
-    (RFF_TILE 1 builds: 128 x 256 16x16x32 tiles at the first three); 5 120: 128 x 64 -- against
-    phi = cos(x W^T + b)
-    sqrt(2/F) in fp64 (linear_cost.py:64-71, tolerance as test_f16x3_rff_features_in_rollout), the
-    column partials against the fp64 sums of the valid phi rows of each 128-row block
-    (n_valid and row_mask both applied), and bit-identical on a second launch."""
+    """amx_rff_features_h3 on each of its tiles -- 40 960 / 20 480 rows: 160 x 256 (whole rounds at
+    one per CU, the epilogue staged in 64-row passes); 21 504: 128 x 128 at three per CU; 12 288 /
+    10 240: 128 x 128 at two; 5 120 / 2 048: 128 x 64 --
+    against phi = cos(x W^T + b) sqrt(2/F) in fp64 (linear_cost.py:64-71, tolerance as
+    test_f16x3_rff_features_in_rollout), the column partials against the fp64 sums of the valid
+    phi rows of each 32-row group (AMX_RFF_PART_ROWS; n_valid and row_mask both applied), and
+    bit-identical on a second launch."""
     import amp_extensions_amd as amx
     K, F = 416, 512
     ctx = amx.AmxContext(197, 36, n_models=1, hidden=128, n_hidden=1, feat_dim=F, device=DEV)
@@ -394,7 +395,7 @@ def test_rff_features_every_tile_shape(rows):
     outs = []
     for _ in range(2):
         phi = torch.empty(rows, F, device=DEV)
-        part = torch.empty(rows // 128, F, dtype=torch.float64, device=DEV)
+        part = torch.empty(rows // 32, F, dtype=torch.float64, device=DEV)
         assert lib.amx_rff_features_h3(h, rows, n_valid, F, K, xd.data_ptr(), K, W2.data_ptr(), wexp.data_ptr(),
                                        rexp.data_ptr(), bd.data_ptr(), ctypes.c_float(scale), phi.data_ptr(), F,
                                        part.data_ptr(), md.data_ptr(), st) == 0
@@ -408,5 +409,5 @@ def test_rff_features_every_tile_shape(rows):
     err = np.abs(phi - ref) / scale
     assert (err <= 4e-7 * arg + 1e-6).all(), float((err - 4e-7 * arg).max())
     valid = (mask.numpy() > 0) & (np.arange(rows) < n_valid)
-    want = (phi * valid[:, None]).reshape(rows // 128, 128, F).sum(1)
+    want = (phi * valid[:, None]).reshape(rows // 32, 32, F).sum(1)
     np.testing.assert_allclose(part, want, rtol=1e-12, atol=1e-12)

@@ -34,7 +34,7 @@ for rows in (40960, 5120):
     x = torch.zeros(rows, rff.Kp, device="cuda")
     x[:, :2 * S] = 0.5 * torch.randn(rows, 2 * S, generator=g).cuda()
     phi = torch.empty(rows, 512, device="cuda")
-    part = torch.empty((rows + 127) // 128, 512, dtype=torch.float64, device="cuda")
+    part = torch.empty((rows + 127) // 128 * 4, 512, dtype=torch.float64, device="cuda")  # 32-row partials
     rff.features(x, rows, rows, phi, part)
     torch.cuda.synchronize()
     h.update(phi.cpu().numpy().tobytes())

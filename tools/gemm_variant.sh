@@ -6,8 +6,8 @@ set -e
 tag=$1; shift
 cd "$(dirname "$0")/.."
 python3 -c "from amp_extensions_amd import _build; _build.build(verbose=False)"
-objs=$(ls amp_extensions_amd/build/*.o | grep -v amx_gemm.o)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-pass-failed -I include "$@" \
+objs=$(python3 -c "from amp_extensions_amd import _build; print(' '.join(_build._obj(s) for s in _build.sources() if not s.endswith('amx_gemm.hip')))")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Wno-pass-failed -I include -I amp_extensions_amd/csrc "$@" \
   -c -o /tmp/amx_gemm_$tag.o amp_extensions_amd/csrc/amx_gemm.hip
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o amp_extensions_amd/libamx_hip_$tag.so $objs /tmp/amx_gemm_$tag.o
 echo "built amp_extensions_amd/libamx_hip_$tag.so"

@@ -31,7 +31,7 @@ def main():
     n = min(len(f), len(w))
     f, w = sorted(f[-n:]), sorted(w[-n:])
     fm, wm = f[n // 2], w[n // 2]
-    alg = rows * K * 4 + F * K * 4 + rows * F * 4 + (rows // 128) * F * 8
+    alg = rows * K * 4 + F * K * 4 + rows * F * 4 + (rows // 32) * F * 8
     hbm = (2 * fm + wm) * 1024
     print(f"RFF pass {rows} rows K {K} F {F}: {n} dispatches; median FETCH_SIZE {fm:.0f} KB (x2 = "
           f"{2 * fm / 1024:.1f} MB), WRITE_SIZE {wm:.0f} KB ({wm / 1024:.1f} MB); HBM {hbm / 1e6:.1f} MB per launch "

@@ -21,7 +21,7 @@ for tag in sys.argv[1:]:
     assert lib.amx_split_f16x2(ctx_h, 1, 512, K, W.data_ptr(), K, 0, W2.data_ptr(), 512 * 2 * K, wexp.data_ptr(), 512, st) == 0
     rexp = torch.empty(rows, dtype=torch.int32, device=dev)
     assert lib.amx_row_exponents(ctx_h, 1, rows, K, x.data_ptr(), K, 0, rexp.data_ptr(), rows, 1, st) == 0
-    phi = torch.empty(rows, 512, device=dev); part = torch.empty(rows // 128, 512, dtype=torch.float64, device=dev)
+    phi = torch.empty(rows, 512, device=dev); part = torch.empty(rows // 32, 512, dtype=torch.float64, device=dev)
     def run():
         assert lib.amx_rff_features_h3(ctx_h, rows, rows, 512, K, x.data_ptr(), K, W2.data_ptr(), wexp.data_ptr(),
                                        rexp.data_ptr(), b.data_ptr(), ctypes.c_float(0.0625), phi.data_ptr(), 512,
