@@ -282,3 +282,28 @@ def test_host_policy_noise_matches_numpy_legacy_stream(lib):
                 np.testing.assert_array_equal(out[:, lane], want)
     bad = np.array([L], np.int32)
     assert lib.amx_mt_seed(st.ctypes.data, L, bad.ctypes.data, seeds.ctypes.data, 1) != 0
+
+
+def test_host_policy_noise_many_lanes(lib):
+    """Chunks of >= 32 lanes are split over host threads: every lane's stream stays
+    bit-identical to numpy's legacy RandomState over repeated calls, independent of how the lanes
+    were dealt to the threads."""
+    L, K, A = 300, 4, 36
+    st = np.zeros((L, _native.AMX_MT_STATE_BYTES), np.uint8)
+    slots = np.arange(L, dtype=np.int32)
+    seeds = (12345 + 7 * np.arange(L)).astype(np.uint32)
+    assert lib.amx_mt_seed(st.ctypes.data, L, slots.ctypes.data, seeds.ctypes.data, L) == 0
+    rss = [np.random.RandomState(int(x)) for x in seeds]
+    out = np.full((K, L, A), np.nan)
+    for rep in range(4):
+        assert lib.amx_mt_policy_noise(st.ctypes.data, L, slots.ctypes.data, L, K, A, out.ctypes.data, L * A, A) == 0
+        for lane in (0, 1, 31, 32, 150, 299):
+            want = np.empty((K, A))
+            for k in range(K):
+                rss[lane].uniform()
+                want[k] = rss[lane].randn(A)
+            np.testing.assert_array_equal(out[:, lane], want)
+        for lane in set(range(L)) - {0, 1, 31, 32, 150, 299}:  # keep the reference streams in step
+            for k in range(K):
+                rss[lane].uniform()
+                rss[lane].randn(A)
