@@ -15,7 +15,8 @@ from . import _build
 _HEADER = os.path.join(_build.INCLUDE, "amx_hip.h")
 # entry points of include/amx_hip_experimental.h: bound only when the library was built with
 # AMX_EXPERIMENTAL=1 (the default library does not export them)
-EXPERIMENTAL = ("amx_set_lb_stage", "amx_assemble_input_limbs", "amx_gemm_bias_act_lb", "amx_gemm_out_unnorm_lb")
+EXPERIMENTAL = ("amx_set_lb_stage", "amx_assemble_input_limbs", "amx_gemm_bias_act_lb", "amx_gemm_out_unnorm_lb",
+                "amx_forward_h3_rows", "amx_forward_h3", "amx_fwd_weight_image")
 
 c_int, c_ll, c_dbl, c_flt, c_u64, c_u32, vp = C.c_int, C.c_longlong, C.c_double, C.c_float, C.c_uint64, C.c_uint32, C.c_void_p
 ip = C.POINTER(C.c_int)
@@ -75,6 +76,10 @@ SIGNATURES = {
                                      vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp, c_ll, c_int, vp, c_int, vp]),
     "amx_gemm_out_unnorm_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll,
                                        vp, c_ll, vp, c_int, c_ll, vp, c_ll, c_int, c_int, vp]),
+    "amx_forward_h3_rows": (c_int, [vp, c_int, c_int]),
+    "amx_fwd_weight_image": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp]),
+    "amx_forward_h3": (c_int, [vp, c_int, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, vp, vp, c_int, vp, c_int,
+                               c_ll, vp, c_ll, c_int, vp]),
     "amx_set_motion": (c_int, [vp, vp, c_ll]),
     "amx_motion_duration": (c_dbl, [vp]),
     "amx_motion_states": (c_int, [vp, vp, c_int, c_int, vp, c_ll, vp]),
@@ -197,7 +202,7 @@ def load(path: str | None = None, build_if_missing: bool = False):
 
 
 def has_experimental(lib) -> bool:
-    """The library was built with AMX_EXPERIMENTAL=1 (the limb-format forward is present)."""
+    """The library was built with AMX_EXPERIMENTAL=1 (the limb-format and one-launch forwards are present)."""
     return all(hasattr(lib, n) for n in EXPERIMENTAL)
 
 

@@ -22,6 +22,29 @@
 
 #include <type_traits>
 
+// H3_TRACE (diagnostic builds, tools/h3_trace.py): thread 0 of every workgroup of an f16x3
+// launch stamps the device realtime clock (100 MHz) at the phases of its tile -- 0 entry, 1 row
+// exponents read, 2 K loop entered, 3 K loop done, 4 epilogue issued, 5 its stores drained --
+// into h3_trace_buf[K / 512 % 5][block] (the forward's five layers: K 256 .. 2304)
+#ifndef H3_TRACE
+#define H3_TRACE 0
+#endif
+#if H3_TRACE
+__device__ unsigned long long h3_trace_buf[5][1024][8];
+#define H3_STAMP(a, ph)                                                                        \
+  do {                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 1024)                                                 \
+      h3_trace_buf[((a).K / 512) % 5][blockIdx.x][ph] = __builtin_amdgcn_s_memrealtime();      \
+  } while (0)
+extern "C" int amx_h3_trace_read(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(h3_trace_buf), sizeof(h3_trace_buf)) == hipSuccess ? 0 : -1;
+}
+#else
+#define H3_STAMP(a, ph) \
+  do {                  \
+  } while (0)
+#endif
+
 namespace {
 
 
@@ -92,7 +115,7 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef RFF_TILE
 #define RFF_TILE 0
 #endif
-// RFF_EXP (diagnostic builds, tools/gemm_variant.sh): 1 = no cos, 2 = no phi store
+// RFF_EXP (diagnostic builds, tools/src_variant.sh): 1 = no cos, 2 = no phi store
 #ifndef RFF_EXP
 #define RFF_EXP 0
 #endif
@@ -871,6 +894,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     }
   }
   __syncthreads();
+  H3_STAMP(a, 1);
 
   // staging maps: A chunk q = t + NT*j -> row q/CPR, k 4*(q%CPR); W chunk q -> row q/CPR,
   // 16-B piece q%CPR (the image's [granule][limb][16] order is the LDS row's order)
@@ -1133,6 +1157,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     load_a(std::integral_constant<int, 1>{}, kb + 1);
     load_w(kb + 1);
     load_a(std::integral_constant<int, 0>{}, kb + 2);
+    H3_STAMP(a, 2);
     auto kstep = [&](int kt, auto par) {  // buffer par; pieces publish tile kt+1 from set par^1
       constexpr int P = decltype(par)::value;
       __syncthreads();  // tile kt visible in buffer P; buffer P^1 (tile kt-1) fully read
@@ -1146,6 +1171,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       kstep(kt, std::integral_constant<int, 0>{});
       if (kt + 1 < ke) kstep(kt + 1, std::integral_constant<int, 1>{});
     }
+    H3_STAMP(a, 3);
     if constexpr (EPI == EPI_UNNORM) {
       if (nseg > 1) {
         __syncthreads();  // the stage buffers are free: one int of LDS for the last-arriver flag
@@ -1153,6 +1179,11 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       }
     }
     finish(acc);
+#if H3_TRACE
+    H3_STAMP(a, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    H3_STAMP(a, 5);
+#endif
     return;
   }
   if constexpr (TL::LATE) {
@@ -1160,6 +1191,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     load(kb);
     publish(0);
     load(kb + 1);
+    H3_STAMP(a, 2);
     for (int kt = kb; kt < ke; ++kt) {
       const int cur = (kt - kb) & 1;
       __syncthreads();  // tile kt visible in buffer cur; buffer cur^1 (tile kt-1) fully read
@@ -1178,6 +1210,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       __builtin_amdgcn_sched_barrier(0);
       compute(cur * STAGE);
     }
+    H3_STAMP(a, 3);
     // (the 256 x 256 hidden tile is launched one tile per workgroup only: no combine code, whose
     // registers it cannot spare)
     if constexpr (TL::M16 && (EPI == EPI_UNNORM || (EPI == EPI_BIAS_ACT && !(BM == 256 && TL::BN == 256)))) {
@@ -1187,6 +1220,11 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
       }
     }
     finish(acc);
+#if H3_TRACE
+    H3_STAMP(a, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    H3_STAMP(a, 5);
+#endif
     return;
   }
   load(0);
@@ -1212,6 +1250,7 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
 template <int EPI, class TL>
 __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
   if (a.timer_role == 1 && blockIdx.x == 0 && threadIdx.x == 0) a.timer[0] = __builtin_amdgcn_s_memrealtime();
+  H3_STAMP(a, 0);
   const int nk = a.K / TL::BK;
   if (a.streamk) {
     const long long U = (long long)a.tiles_m * a.tiles_n * a.groups * nk, G = gridDim.x;

@@ -13,6 +13,7 @@ inert), so any BasicMLP config runs on the same 128x128 MFMA tiles.
 from __future__ import annotations
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -212,6 +213,28 @@ class DeviceEnsemble:
         elif gemm == "f16x3":
             sp = [split_f16x2(ctx, W) for W in self.W]
             self.W2, self.wexp = [x[0] for x in sp], [x[1] for x in sp]
+        # f16x3 forward: "layers" (default) -- one launch per layer; "fused" -- the whole forward in
+        # one launch (amx_forward_h3, an AMX_EXPERIMENTAL=1 build) at the lane counts whose row
+        # blocks fill the CUs in one round, the per-layer launches elsewhere.  Same bits (whole-K
+        # output tiles); measured equal at the N = 8 share.  Env AMX_FORWARD.
+        self.forward_mode = os.environ.get("AMX_FORWARD", "layers")
+        if self.forward_mode not in ("fused", "layers"):
+            raise ValueError(f"AMX_FORWARD must be 'fused' or 'layers', got {self.forward_mode!r}")
+        self._fw_ptrs = None
+        self._fw_rows = {}
+        self.W2f = None
+        if self.W2 is not None and Hp == 512 and 1 <= L <= 8 and hasattr(ctx.lib, "amx_fwd_weight_image"):
+            # the one-launch forward reads its weights in fragment order (amx_fwd_weight_image)
+            self.W2f = []
+            for i, w in enumerate(self.W2):
+                rows, K2 = w.shape[1], w.shape[2]
+                wf = torch.empty_like(w)
+                N.check(ctx.lib.amx_fwd_weight_image(ctx.h, M, rows, K2 // 2, w.data_ptr(), wf.data_ptr(),
+                                                     ctx.stream), "amx_fwd_weight_image")
+                self.W2f.append(wf)
+            vp = N.C.c_void_p * (L + 1)
+            self._fw_ptrs = (vp(*[w.data_ptr() for w in self.W2f]), vp(*[w.data_ptr() for w in self.wexp]),
+                             vp(*[b.data_ptr() for b in self.b]))
         ctx.set_normalizers(norms)
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
@@ -307,9 +330,28 @@ class DeviceEnsemble:
         self._mlp(buf, preds, Bp, s, rexp, row_exponents=assembled, k_shared=k_shared)
         return preds
 
+    def fused_rows(self, Bp: int) -> int:
+        """Rows per workgroup of the one-launch forward at Bp padded lanes (0: per-layer launches)."""
+        r = self._fw_rows.get(Bp)
+        if r is None:
+            c = self.ctx
+            ok = (self._fw_ptrs is not None and c.Hp == 512 and 1 <= c.L <= 8 and c.k0_pad % 64 == 0
+                  and c.n_out_pad in (128, 256))
+            r = int(c.lib.amx_forward_h3_rows(c.h, c.M, Bp)) if ok else 0
+            self._fw_rows[Bp] = r
+        return r
+
     def _mlp_h3(self, buf, preds, Bp, s, rexp, k_shared=0):
         c = self.ctx
         sA, sR, L = Bp * c.ldk, (c.L + 1) * Bp, c.L
+        if self.forward_mode == "fused" and self._fw_ptrs is None:
+            raise N.AmxNativeError("forward_mode='fused' is an experimental A/B path: rebuild the library with "
+                                   "AMX_EXPERIMENTAL=1 python -m amp_extensions_amd._build")
+        if self.forward_mode == "fused" and self.fused_rows(Bp):
+            N.check(c.lib.amx_forward_h3(c.h, c.M, Bp, c.k0_pad, c.Hp, L, buf.data_ptr(), c.ldk, sA, *self._fw_ptrs,
+                                         c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, rexp.data_ptr(), sR, k_shared,
+                                         s), "amx_forward_h3")
+            return
         for i in range(L):
             K = c.k0_pad + i * c.Hp
             N.check(c.lib.amx_gemm_bias_act_h3(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),

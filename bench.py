@@ -84,6 +84,10 @@ def parse():
                    help="f16x3 activation rows: f32 (split by every consumer, amx_gemm_*_h3; default) or limbs "
                         "(split once by the producer, amx_gemm_*_lb; measured slower, DESIGN §6 round 4; needs a "
                         "library built with AMX_EXPERIMENTAL=1)")
+    p.add_argument("--forward", choices=["fused", "layers"], default="layers",
+                   help="f16x3 forward: one launch per layer (default), or the whole forward in one launch "
+                        "(amx_forward_h3) at the lane counts whose row blocks fill the CUs in one round (A/B, "
+                        "measured equal at the N = 8 share; needs a library built with AMX_EXPERIMENTAL=1)")
     p.add_argument("--lb-stage", type=int, choices=[0, 1], default=0,
                    help="limb forward's K-loop staging: 0 registers, 1 LDS-DMA (A/B; AMX_EXPERIMENTAL=1 build)")
     p.add_argument("--expert-rows", type=int, default=50000)
@@ -420,6 +424,7 @@ def main():
     ens_w = init_ensemble_weights(S, A, hidden, M, base_seed=100)
     ctx = amx.AmxContext(S, A, n_models=M, hidden=512, n_hidden=4, feat_dim=512, device=dev)
     ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm, act_format=args.act_format)
+    ens.forward_mode = args.forward
     if args.lb_stage:
         ctx.lib.amx_set_lb_stage(ctx.h, args.lb_stage)
     thr = ens.compute_threshold(st.to(dev), at.to(dev))
@@ -594,7 +599,8 @@ def main():
         ctx.gemm_timer(False)
     shard_note = (f"; expert cost over {args.expert_rows}/{world} expert rows per rank, its fp64 sum all-reduced "
                   f"off the critical path" if shard else "")
-    per_fwd = ctx.L + 1  # GEMM launches per forward
+    fused = ens.forward_mode == "fused" and ens.W2 is not None and not ens.limbs and ens.fused_rows((B + 127) // 128 * 128) > 0
+    per_fwd = 1 if fused else ctx.L + 1  # GEMM launches per forward
     launches = n_fwd * per_fwd
     flops_per_fwd = ens.mlp_flops_per_sample() * B
     if args.mode == "paths":

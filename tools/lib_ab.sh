@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of library builds (tools/gemm_variant.sh) on one box: for each round and each tag, install
+# A/B of library builds (tools/src_variant.sh) on one box: for each round and each tag, install
 # libamx_hip_<tag>.so as the library and run the given command; restores base at the end.
 # usage: tools/lib_ab.sh "<tags>" <rounds> <cmd...>   (run on the GPU box, from the repo root)
 set -e
