@@ -41,6 +41,13 @@ for _ in range(reps):
     out = npg.train_from_arrays(obs_d, act_d, adv_d)
 torch.cuda.synchronize()
 gpu_ms = (time.perf_counter() - t0) / reps * 1e3
+# the update alone, as a training loop runs it: consecutive updates, no parameter restore in
+# between (set_param_values' copies, clamp and policy re-sync are the harness's, not the update's)
+t0 = time.perf_counter()
+for _ in range(reps):
+    npg.train_from_arrays(obs_d, act_d, adv_d)
+torch.cuda.synchronize()
+upd_ms = (time.perf_counter() - t0) / reps * 1e3
 # one Fisher-vector product alone
 v = torch.randn(npg.P, dtype=torch.float64, device="cuda")
 obs32 = obs_d.contiguous()
@@ -55,6 +62,11 @@ torch.cuda.synchronize()
 fvp_us = e0.elapsed_time(e1) / 20 * 1e3
 print(f"device NPG update, N={N} S={S} A={A}: {gpu_ms:.2f} ms per update (VPG + 10 CG FVPs + eval), "
       f"{fvp_us:.1f} us per public HVP call (fp64 observations); alpha {out['alpha']:.4g}, kl {out['kl_dist']:.4g}")
+print(f"  consecutive updates (no set_param_values between them): {upd_ms:.3f} ms per update, its one host sync "
+      f"(the infos' python floats) included")
+npg.set_param_values(p0)  # the comparison below: one update from p0
+npg.train_from_arrays(obs_d, act_d, adv_d)
+torch.cuda.synchronize()
 torch.set_num_threads(threads)
 shapes = R.policy_param_shapes(S, A, (32, 32))
 t0 = time.perf_counter()
