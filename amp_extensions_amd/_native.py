@@ -102,6 +102,7 @@ SIGNATURES = {
     "amx_npg_apply_step": (c_int, [vp, c_int, c_int, vp, vp, vp, c_int, c_dbl, c_dbl, c_flt, vp, vp, vp]),
     "amx_npg_pass_ex": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp, vp, vp]),
     "amx_npg_cg_init": (c_int, [vp, c_int, vp, vp, vp, vp, vp, vp, vp]),
+    "amx_npg_cg_init_ls": (c_int, [vp, c_int, c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "amx_npg_cg_step": (c_int, [vp, c_int, c_int, vp, vp, c_dbl, c_dbl, vp, vp, vp, vp, vp, vp]),
     "amx_step": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, c_int, vp]),
     "amx_step_rexp": (c_int, [vp, vp, c_int, c_ll, vp, vp, vp, vp, vp, vp, vp, c_int, vp, vp, c_int, vp]),

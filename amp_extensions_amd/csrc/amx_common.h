@@ -53,7 +53,10 @@ struct amx_ctx {
   int step_act_w8;           // amx_set_step_act_occupancy: k_step_act at two workgroups per CU (A/B)
   double* d_npg_scratch;     // amx_npg_reduce's run sums
   size_t npg_scratch_bytes;
+  double* d_whiten_part;     // amx_adv_whiten's per-block (count, sum, M2): AMX_WHITEN_MAXB x 3
 };
+
+constexpr int AMX_WHITEN_MAXB = 1024;  // amx_adv_whiten: most workgroups of its first pass
 
 namespace amx {
 

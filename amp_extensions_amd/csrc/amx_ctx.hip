@@ -54,6 +54,13 @@ extern "C" amx_ctx* amx_create(int device, int S, int A, int n_models, int hidde
     amx::set_error("amx_create: hipMalloc of normalizers failed");
     return nullptr;
   }
+  // amx_adv_whiten's per-block partials (allocated here: the launch stays graph-capturable)
+  if (hipMalloc((void**)&c->d_whiten_part, sizeof(double) * 3 * AMX_WHITEN_MAXB) != hipSuccess) {
+    (void)hipFree(c->d_norm);
+    free(c);
+    amx::set_error("amx_create: hipMalloc of the whitening partials failed");
+    return nullptr;
+  }
   return c;
 }
 
@@ -62,6 +69,7 @@ extern "C" int amx_destroy(amx_ctx* c) {
   if (c->d_norm) (void)hipFree(c->d_norm);
   if (c->d_motion) (void)hipFree(c->d_motion);
   if (c->d_npg_scratch) (void)hipFree(c->d_npg_scratch);
+  if (c->d_whiten_part) (void)hipFree(c->d_whiten_part);
   free(c);
   return AMX_OK;
 }

@@ -125,93 +125,105 @@ __global__ __launch_bounds__(256) void k_gae(Grid g, const uint8_t* __restrict__
   }
 }
 
-// (adv - mean) / (std + eps) over the grid's rows: one 1024-thread block, fixed order
-// (thread-strided partial sums, then an LDS tree), two passes as np.mean / np.std.
-__global__ __launch_bounds__(1024) void k_adv_whiten(Grid g, const double* __restrict__ adv, double eps,
-                                                     double* __restrict__ out, double* __restrict__ stats) {
-  __shared__ double red[1024];
-  __shared__ double s_mean, s_std;
-  const long long total = (long long)g.T * g.L;
-  // a flat vector (one row of L, no lengths / bases: DeviceNPG's whitening): element i is row i
-  // and every element counts -- the same thread-strided order without the 64-bit index division
-  const bool flat = g.T == 1 && g.len == nullptr && g.base == nullptr;
-  double s = 0.0, cnt = 0.0;
+// (adv - mean) / (std + eps) over the grid's rows (np.mean / np.std, population std), in two
+// launches over the whole chip: the flat element range is cut into nb contiguous chunks of `ch`
+// elements (a multiple of 1024; a fixed partition: deterministic), and
+//   k_whiten_part: workgroup b reduces its chunk's count, sum and -- about its own mean, a second
+//     pass over the chunk (L1/L2-resident) -- sum of squared deviations M2_b (fixed order: thread
+//     strides, waves, then the 16 wave parts in order) into part[b];
+//   k_whiten_apply: every workgroup combines the nb parts in block order (Chan et al.'s pairwise
+//     update: mean = sum / n, M2 = sum_b M2_b + n_b (mean_b - mean)^2; the same bits in every
+//     workgroup), std = sqrt(M2 / n), and writes its chunk; workgroup 0 writes stats.
+// (Round 4's one-workgroup form: 25 us for 40 960 advantages, profiles/r05c_npg_timeline.txt.)
+constexpr int WCH = 4096;  // elements per workgroup when the chunks fit AMX_WHITEN_MAXB workgroups
+
+__device__ inline bool whiten_elem(const Grid& g, bool flat, long long i, long long end, long long& r) {
+  if (i >= end) return false;
   if (flat) {
-#pragma unroll 8
-    for (long long i = threadIdx.x; i < total; i += 1024) {
-      s += adv[i];
+    r = i;
+    return true;
+  }
+  const int t = (int)(i / g.L), l = (int)(i % g.L);
+  if (t >= g.length(l)) return false;
+  r = g.row(t, l);
+  return true;
+}
+
+// fixed-order sum over the workgroup's 1024 threads (wave butterflies, then the 16 wave parts)
+__device__ inline double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) s += red[w];
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void k_whiten_part(Grid g, const double* __restrict__ adv, long long ch,
+                                                      double* __restrict__ part) {
+  __shared__ double red[16];
+  const long long total = (long long)g.T * g.L;
+  const bool flat = g.T == 1 && g.len == nullptr && g.base == nullptr;
+  const long long c0 = (long long)blockIdx.x * ch, c1 = c0 + ch < total ? c0 + ch : total;
+  double s = 0.0, cnt = 0.0;
+  for (long long i = c0 + threadIdx.x; i < c1; i += 1024) {
+    long long r = 0;
+    if (whiten_elem(g, flat, i, c1, r)) {
+      s += adv[r];
       cnt += 1.0;
     }
-  } else {
-    for (long long i = threadIdx.x; i < total; i += 1024) {
-      const int t = (int)(i / g.L), l = (int)(i % g.L);
-      if (t < g.length(l)) {
-        s += adv[g.row(t, l)];
-        cnt += 1.0;
-      }
-    }
   }
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  const double sum = red[0];
-  __syncthreads();
-  red[threadIdx.x] = cnt;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  const double n = red[0];
-  if (threadIdx.x == 0) s_mean = n > 0.0 ? sum / n : 0.0;
-  __syncthreads();
-  const double mean = s_mean;
+  const double sum = block_sum(s, red);
+  const double n = block_sum(cnt, red);
+  const double m = n > 0.0 ? sum / n : 0.0;
   double q = 0.0;
-  if (flat) {
-#pragma unroll 8
-    for (long long i = threadIdx.x; i < total; i += 1024) {
-      const double d = adv[i] - mean;
+  for (long long i = c0 + threadIdx.x; i < c1; i += 1024) {
+    long long r = 0;
+    if (whiten_elem(g, flat, i, c1, r)) {
+      const double d = adv[r] - m;
       q += d * d;
     }
-  } else {
-    for (long long i = threadIdx.x; i < total; i += 1024) {
-      const int t = (int)(i / g.L), l = (int)(i % g.L);
-      if (t < g.length(l)) {
-        const double d = adv[g.row(t, l)] - mean;
-        q += d * d;
-      }
-    }
   }
-  __syncthreads();
-  red[threadIdx.x] = q;
-  __syncthreads();
-  for (int o = 512; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
+  const double m2 = block_sum(q, red);
   if (threadIdx.x == 0) {
-    s_std = n > 0.0 ? sqrt(red[0] / n) : 0.0;
-    if (stats) {
-      stats[0] = mean;
-      stats[1] = s_std;
+    part[3 * blockIdx.x] = n;
+    part[3 * blockIdx.x + 1] = sum;
+    part[3 * blockIdx.x + 2] = m2;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_whiten_apply(Grid g, const double* __restrict__ adv,
+                                                       const double* __restrict__ part, int nb, long long ch,
+                                                       double eps, double* __restrict__ out,
+                                                       double* __restrict__ stats) {
+  const long long total = (long long)g.T * g.L;
+  const bool flat = g.T == 1 && g.len == nullptr && g.base == nullptr;
+  double n = 0.0, sum = 0.0;
+  for (int b = 0; b < nb; ++b) {  // every thread the same fixed order (broadcast loads)
+    n += part[3 * b];
+    sum += part[3 * b + 1];
+  }
+  const double mean = n > 0.0 ? sum / n : 0.0;
+  double m2 = 0.0;
+  for (int b = 0; b < nb; ++b) {
+    const double nbk = part[3 * b];
+    if (nbk > 0.0) {
+      const double d = part[3 * b + 1] / nbk - mean;
+      m2 += part[3 * b + 2] + nbk * d * d;
     }
   }
-  __syncthreads();
-  const double den = s_std + eps;
-  if (flat) {
-#pragma unroll 8
-    for (long long i = threadIdx.x; i < total; i += 1024) out[i] = (adv[i] - mean) / den;
-  } else {
-    for (long long i = threadIdx.x; i < total; i += 1024) {
-      const int t = (int)(i / g.L), l = (int)(i % g.L);
-      if (t < g.length(l)) {
-        const long long r = g.row(t, l);
-        out[r] = (adv[r] - mean) / den;
-      }
-    }
+  const double sd = n > 0.0 ? sqrt(m2 / n) : 0.0;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && stats) {
+    stats[0] = mean;
+    stats[1] = sd;
+  }
+  const double den = sd + eps;
+  const long long c0 = (long long)blockIdx.x * ch, c1 = c0 + ch < total ? c0 + ch : total;
+  for (long long i = c0 + threadIdx.x; i < c1; i += 1024) {
+    long long r = 0;
+    if (whiten_elem(g, flat, i, c1, r)) out[r] = (adv[r] - mean) / den;
   }
 }
 
@@ -273,8 +285,16 @@ extern "C" int amx_adv_whiten(amx_ctx* ctx, int T, int L, const int32_t* len, co
   int rc = check_grid("amx_adv_whiten", T, L, stride);
   if (rc) return rc;
   AMX_CHECK_ARG(adv && out, "amx_adv_whiten: null pointer");
+  const long long total = (long long)T * L;
+  long long ch = WCH;  // chunk per workgroup: WCH, or larger (multiples of 1024) beyond MAXB workgroups
+  if ((total + ch - 1) / ch > AMX_WHITEN_MAXB) ch = ((total + AMX_WHITEN_MAXB - 1) / AMX_WHITEN_MAXB + 1023) / 1024 * 1024;
+  const long long nb = total > 0 ? (total + ch - 1) / ch : 1;
   Grid g{T, L, len, base, stride};
-  hipLaunchKernelGGL(k_adv_whiten, dim3(1), dim3(1024), 0, (hipStream_t)stream, g, adv, eps, out, stats);
+  hipLaunchKernelGGL(k_whiten_part, dim3((int)nb), dim3(1024), 0, (hipStream_t)stream, g, adv, ch,
+                     ctx->d_whiten_part);
+  AMX_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_whiten_apply, dim3((int)nb), dim3(1024), 0, (hipStream_t)stream, g, adv, ctx->d_whiten_part,
+                     (int)nb, ch, eps, out, stats);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

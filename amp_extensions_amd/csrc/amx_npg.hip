@@ -862,10 +862,21 @@ __device__ double cg_block_sum(double v, double* red) {
   return s;
 }
 
+__device__ inline double npg_ls_curvature(float log_std) {
+  const double e = exp((double)log_std);
+  const double sq = e * e, eps = 1e-8;
+  const double den = 2.0 * sq + eps;
+  return (8.0 * sq * sq - 4.0 * sq * eps) / (den * den);
+}
+
+// (theta / curv non-null: also the log_std curvature of k_npg_curvature, one launch fewer)
 __global__ __launch_bounds__(CGT) void k_npg_cg_init(int P, const double* __restrict__ b, double* __restrict__ x,
                                                      double* __restrict__ r, double* __restrict__ p,
-                                                     float* __restrict__ p32, double* __restrict__ state) {
+                                                     float* __restrict__ p32, double* __restrict__ state, int A,
+                                                     const float* __restrict__ theta, double* __restrict__ curv) {
   __shared__ double red[CGT / 64];
+  if (curv)
+    for (int d = threadIdx.x; d < A; d += CGT) curv[d] = npg_ls_curvature(theta[P - A + d]);
   double rr = 0.0;
 #pragma unroll
   for (int u = 0; u < CGE; ++u) {
@@ -948,10 +959,7 @@ __global__ __launch_bounds__(64) void k_npg_curvature(const float* __restrict__ 
                                                       double* __restrict__ curv) {
   const int d = blockIdx.x * 64 + threadIdx.x;
   if (d >= A) return;
-  const double e = exp((double)theta[P - A + d]);
-  const double sq = e * e, eps = 1e-8;
-  const double den = 2.0 * sq + eps;
-  curv[d] = (8.0 * sq * sq - 4.0 * sq * eps) / (den * den);
+  curv[d] = npg_ls_curvature(theta[P - A + d]);
 }
 
 // The NPG step after the CG (npg_cg.py:141-163): gdot = vpg . npg (fixed-order block sum);
@@ -1296,7 +1304,19 @@ extern "C" int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, 
                                double* state, void* stream) {
   AMX_CHECK_ARG(ctx && b && x && r && p && p32 && state, "amx_npg_cg_init: null argument");
   AMX_CHECK_ARG(P > 0 && P <= CGT * CGE, "amx_npg_cg_init: P=%d (<= %d)", P, CGT * CGE);
-  hipLaunchKernelGGL(k_npg_cg_init, dim3(1), dim3(CGT), 0, (hipStream_t)stream, P, b, x, r, p, p32, state);
+  hipLaunchKernelGGL(k_npg_cg_init, dim3(1), dim3(CGT), 0, (hipStream_t)stream, P, b, x, r, p, p32, state, 0,
+                     nullptr, nullptr);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_npg_cg_init_ls(amx_ctx* ctx, int P, int A, const float* theta, double* curv, const double* b,
+                                  double* x, double* r, double* p, float* p32, double* state, void* stream) {
+  AMX_CHECK_ARG(ctx && theta && curv && b && x && r && p && p32 && state, "amx_npg_cg_init_ls: null argument");
+  AMX_CHECK_ARG(P > 0 && P <= CGT * CGE && A > 0 && A < P, "amx_npg_cg_init_ls: P=%d A=%d (P <= %d)", P, A,
+                CGT * CGE);
+  hipLaunchKernelGGL(k_npg_cg_init, dim3(1), dim3(CGT), 0, (hipStream_t)stream, P, b, x, r, p, p32, state, A, theta,
+                     curv);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

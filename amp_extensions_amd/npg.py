@@ -115,9 +115,10 @@ class DeviceNPG:
         # one block per CU (the pass kernel holds ~140 KB of LDS): one wave of blocks
         return max(32, int(math.ceil(n / 256 / 32)) * 32)
 
-    def _pass(self, mode, obs, act, adv, vec, gate=None, hcache=None, reduce=True):
-        """One pass (amx_npg_pass_ex) and its block-order reduction; reduce=False returns the
-        [blocks][width] partials instead (the CG folds their reduction into its step)."""
+    def _pass(self, mode, obs, act, adv, vec, gate=None, hcache=None, reduce=True, out=None):
+        """One pass (amx_npg_pass_ex) and its block-order reduction (into `out` when given);
+        reduce=False returns the [blocks][width] partials instead (the CG folds their reduction
+        into its step)."""
         c = self.ctx
         n = obs.shape[0]
         rpb = self._rows_per_block(n)
@@ -137,7 +138,8 @@ class DeviceNPG:
                 "amx_npg_pass")
         if not reduce:
             return part
-        out = torch.empty(width, dtype=torch.float64, device=c.device)
+        if out is None:
+            out = torch.empty(width, dtype=torch.float64, device=c.device)
         N.check(c.lib.amx_npg_reduce_gated(c.h, part.data_ptr(), nb, width, out.data_ptr(), g, c.stream),
                 "amx_npg_reduce")
         return out
@@ -211,9 +213,10 @@ class DeviceNPG:
         x, r, p, r2 = (torch.empty(P, dtype=torch.float64, device=dev) for _ in range(4))
         p32 = torch.empty(P, dtype=torch.float32, device=dev)
         state, state2 = (torch.empty(2, dtype=torch.float64, device=dev) for _ in range(2))
-        curv = self._ls_curvature().contiguous()
-        N.check(c.lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
-                                      p32.data_ptr(), state.data_ptr(), c.stream), "amx_npg_cg_init")
+        curv = torch.empty(self.A, dtype=torch.float64, device=dev)  # the log_std curvature, same launch
+        N.check(c.lib.amx_npg_cg_init_ls(c.h, P, self.A, self.theta.data_ptr(), curv.data_ptr(), b.data_ptr(),
+                                         x.data_ptr(), r.data_ptr(), p.data_ptr(), p32.data_ptr(), state.data_ptr(),
+                                         c.stream), "amx_npg_cg_init_ls")
         work = self._bufs.get("cg_work")
         if work is None:
             work = self._bufs["cg_work"] = torch.empty(int(c.lib.amx_npg_cg_tail_work(P)), dtype=torch.float64,
@@ -256,18 +259,21 @@ class DeviceNPG:
         npg = self.cg_solve(obs, act, vpg, hcache=hc)
         # gdot, the step size and the clamped new parameters in one launch (amx_npg_apply_step)
         new = torch.empty(self.P, dtype=torch.float32, device=c.device)
-        scal = torch.empty(3, dtype=torch.float64, device=c.device)
+        # [alpha, n_step_size, gdot | surr, kl]: the step kernel and the eval reduction write the
+        # two ends of one buffer, read back in one copy (no concatenation kernel)
+        res = torch.empty(5, dtype=torch.float64, device=c.device)
+        scal = res[:3]
         use_alpha = self.alpha is not None
         N.check(c.lib.amx_npg_apply_step(c.h, self.P, self.A, vpg.data_ptr(), npg.data_ptr(), self.theta.data_ptr(),
                                          int(use_alpha), float(self.alpha) if use_alpha else 0.0,
                                          float(self.n_step_size), self.min_log_std, new.data_ptr(),
                                          scal.data_ptr(), c.stream), "amx_npg_apply_step")
-        tot = self._pass(NPG_EVAL, obs, act, adv, new)
+        self._pass(NPG_EVAL, obs, act, adv, new, out=res[3:])
         self.theta = new  # already float32 with the log_std clamp (set_param_values' form)
         if self.policy is not None:
             self.policy.sync_from(*self._layers_view())
         # the update's one host sync: the reference's infos are python floats
-        alpha_h, delta_h, surr_h, kl_h = torch.cat([scal[:2], tot]).tolist()
+        alpha_h, delta_h, _, surr_h, kl_h = res.tolist()
         return {"vpg_grad": vpg, "npg_grad": npg, "alpha": alpha_h, "delta": delta_h, "surr_before": 0.0,
                 "surr_after": surr_h / n, "kl_dist": kl_h / n, "advantages": adv}
 

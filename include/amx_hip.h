@@ -338,6 +338,9 @@ int amx_npg_cg_tail(amx_ctx* ctx, const double* partials, int blocks, int P, int
                     const double* state_in, double* state_out, double* work, void* stream);
 int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, double* r, double* p, float* p32,
                     double* state, void* stream);
+/* amx_npg_cg_init + amx_npg_curvature (theta's log_std block -> curv [A]) in one launch. */
+int amx_npg_cg_init_ls(amx_ctx* ctx, int P, int A, const float* theta, double* curv, const double* b, double* x,
+                       double* r, double* p, float* p32, double* state, void* stream);
 int amx_npg_cg_step(amx_ctx* ctx, int P, int A, const double* h, const double* curv, double damping,
                     double residual_tol, double* x, double* r, double* p, float* p32, double* state,
                     void* stream);

@@ -300,3 +300,33 @@ def test_npg_pass_input_dtypes_bit_identical():
         a64 = npg._pass(mode, obs64, act64, adv, v).cpu().numpy()
         a32 = npg._pass(mode, obs64.float().contiguous(), act64.float().contiguous(), adv, v).cpu().numpy()
         np.testing.assert_array_equal(a64, a32)
+
+
+def test_npg_cg_init_ls_matches_separate():
+    """amx_npg_cg_init_ls (the CG start + the log_std curvature in one launch) writes the same
+    bits as amx_npg_cg_init followed by amx_npg_curvature."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy
+    S, A = 197, 36
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=7, init_log_std=-0.4)
+    npg = make(S, A, pack_policy(layers, ls))
+    c, lib, P = npg.ctx, npg.ctx.lib, npg.P
+    b = torch.from_numpy(np.random.RandomState(3).randn(P)).to(DEV)
+    outs = []
+    for fused in (False, True):
+        x, r, p = (torch.full((P,), 7.0, dtype=torch.float64, device=DEV) for _ in range(3))
+        p32 = torch.empty(P, dtype=torch.float32, device=DEV)
+        st = torch.empty(2, dtype=torch.float64, device=DEV)
+        if fused:
+            curv = torch.empty(A, dtype=torch.float64, device=DEV)
+            assert lib.amx_npg_cg_init_ls(c.h, P, A, npg.theta.data_ptr(), curv.data_ptr(), b.data_ptr(),
+                                          x.data_ptr(), r.data_ptr(), p.data_ptr(), p32.data_ptr(), st.data_ptr(),
+                                          c.stream) == 0
+        else:
+            assert lib.amx_npg_cg_init(c.h, P, b.data_ptr(), x.data_ptr(), r.data_ptr(), p.data_ptr(),
+                                       p32.data_ptr(), st.data_ptr(), c.stream) == 0
+            curv = npg._ls_curvature()
+        torch.cuda.synchronize()
+        outs.append([t.cpu().double().numpy() for t in (x, r, p, p32, st, curv)])
+    for u, v in zip(*outs):
+        assert np.array_equal(u, v)
