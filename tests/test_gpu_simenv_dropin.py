@@ -187,3 +187,40 @@ def test_sample_points_custom_time_motion(setup):
     eng = next(iter(benv.engine.__dict__["_sampler_engines"].values()))
     assert eng.reset_time_max == pytest.approx(0.35)
     assert len(dev_paths) > 0
+
+
+def test_sample_points_with_reset_noise(setup):
+    """sample_points with reset_args noise on (AddNoise on every motion reset, row a5; ADVICE
+    r04): the paths' first observations are finite and perturbed away from the plain reset states
+    of their (seeded) reset times, and the env's CURRENT noise setting reaches the sampler's cached
+    engine -- after set_reset_noise(None) the same call starts every trajectory at the plain
+    reset state again.  (With noise on the draws come from Philox(engine seed; lane, reset#), not
+    from the trajectory seed: sampler.py documents that those paths depend on the lane count.)"""
+    amx, ens, ens_w, norms, args, J, bodies, M = setup
+    ra = dict(RUN_PY_RESET_ARGS, custom_time=True, time_max=0.35, noise_max=0.1, radian=0.2)
+    benv = amx.BatchedSimEnv(ens, None, lanes=64, deepmimic_args=args, reset_args=ra, seed=3, horizon=6,
+                             record_means=True)
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    pol = amx.DevicePolicy(ens.ctx, pw, log_std)
+    W, N, base = 2, 40, 4
+
+    def starts(paths):
+        q, k, out = int(np.ceil(N / W)), 0, []
+        for i in range(W):
+            tot, j = 0, 0
+            while tot < q:
+                j += 1
+                t = R.gym_np_random(12345 + base * i + j).uniform(low=0, high=0.35)
+                out.append(_rel(paths[k]["observations"][0], DR.reset_state(J, bodies, M, t)))
+                tot += len(paths[k]["rewards"])
+                k += 1
+        assert k == len(paths)
+        return np.array(out)
+
+    noisy = amx.sample_points(benv, pol, num_to_collect=N, base_seed=base, num_workers=W)
+    assert all(np.isfinite(p["observations"]).all() for p in noisy)
+    d = starts(noisy)
+    assert (d > 1e-3).mean() > 0.9, d  # perturbed (pose noise up to 0.1, root yaw up to 0.2 rad)
+    benv.engine.set_reset_noise(None)
+    plain = amx.sample_points(benv, pol, num_to_collect=N, base_seed=base, num_workers=W)
+    assert starts(plain).max() <= 1e-10
