@@ -138,3 +138,21 @@ def test_engine_advantages_vs_oracle(setup, B, K, horizon):
     aw = out["advantages_whitened"].cpu().numpy()
     exp = (adv - adv.mean()) / (adv.std() + 1e-6)
     np.testing.assert_allclose(aw, exp, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4097, 40960, 5_000_003])
+def test_whitening_sizes(setup, n):
+    """amx_adv_whiten over the chip (per-block count / sum / M2 combined in block order): sizes
+    around its 4096-element chunk and past AMX_WHITEN_MAXB x 4096 elements (the chunk grows), in
+    place (out aliases adv), against numpy's mean / population std at 1e-12; deterministic."""
+    amx, ctx = setup
+    from amp_extensions_amd.gae import whiten_grid
+    x = np.random.RandomState(n % 1000).randn(n) * 3.0 + 0.7
+    d = torch.from_numpy(x).to(DEV)
+    out, stats = whiten_grid(ctx, n, 1, d.clone(), 1, eps=1e-6)  # in place
+    out2, _ = whiten_grid(ctx, n, 1, d.clone(), 1, eps=1e-6, out=torch.empty_like(d))
+    torch.cuda.synchronize()
+    ref = (x - x.mean()) / (x.std() + 1e-6)
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(stats.cpu().numpy(), [x.mean(), x.std()], rtol=1e-12, atol=1e-14)
+    assert torch.equal(out, out2)
