@@ -81,17 +81,6 @@ extern "C" int amx_fwd_trace_read(unsigned long long* host) {
   } while (0)
 #endif
 
-// FW_STREAM (A/B builds, with FW_CT and FW_NOUTER): 1 = half of each hidden slice (every wave's
-// column blocks 2 and 3) goes into LDS at the epilogue and is written out over the next layer's
-// first four K-tiles (each boundary's store burst halved); 0 = the whole slice stored at once
-#ifndef FW_STREAM
-#define FW_STREAM 1
-#endif
-// the n-outer schedule keeps all MB m-blocks' A fragments live up to this MB, halves above it
-// (the streamed slice's registers do not fit beside five blocks' fragments)
-#ifndef FW_MH_ALL
-#define FW_MH_ALL (FW_STREAM ? 4 : 5)
-#endif
 // FW_NOUTER (A/B builds): 1 = the n-outer K-tile schedule (see ktile); 0 = m-outer
 #ifndef FW_NOUTER
 #define FW_NOUTER 1
@@ -138,16 +127,6 @@ __global__ __launch_bounds__(FW_NT, 1) void k_forward_h3(FwdArgs a) {
   __shared__ uint32_t sMax[FW_MAXL][BM];
   __shared__ __attribute__((aligned(16))) float sBias[2][FW_H];
   __shared__ __attribute__((aligned(16))) int sWexp[2][FW_H];
-#if FW_STREAM && FW_CT && FW_NOUTER
-  // the streamed half of the last slice: [row][wave * 32 + x] = column wave * 64 + 32 + x
-  constexpr bool STREAM = true;
-  constexpr int SHL = FW_H / 2 + 4;  // floats per row (16-B aligned, rows 16 B off the bank pattern)
-  __shared__ __attribute__((aligned(16))) float sH[BM * SHL];
-  // per K-tile while streaming: float4 chunks per thread, 4 K-tiles (BM rows x 64 chunks)
-  constexpr int SPER = (BM * 64 / FW_NT + 3) / 4;
-#else
-  constexpr bool STREAM = false;
-#endif
 
   if (a.timer && blockIdx.x == 0 && threadIdx.x == 0) a.timer[0] = __builtin_amdgcn_s_memrealtime();
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -259,45 +238,23 @@ __global__ __launch_bounds__(FW_NT, 1) void k_forward_h3(FwdArgs a) {
             hf8, __builtin_amdgcn_raw_buffer_load_b128(rsW, w_lane, (((cb16 + n) * nk + kt) * 2 + l) * 1024, 0));
   };
 
-  // the slice being streamed: its column offset and the member's row block (rsC of the layer before)
-  int s_col = -1;
-  __amdgpu_buffer_rsrc_t rsS = __builtin_amdgcn_make_buffer_rsrc(
-      a.C + (long long)g * a.strideA + rowbase * a.lda, 0, 0x7ffffff0, 0x00020000);
-  // chunk u of K-tile kt's share (one float4 per call: the LDS read and its store back to back)
-  auto stream_piece = [&](int kt, int u) {
-#if FW_STREAM && FW_CT && FW_NOUTER
-    if (s_col < 0 || u >= SPER) return;
-    const int c = t + FW_NT * (kt * SPER + u);  // chunk: row c / 64, float4 c % 64
-    if (c < BM * 64) {
-      const int r = c >> 6, q = c & 63;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(&sH[r * SHL + 4 * q]);
-      const int col = (q >> 3) * 64 + 32 + (q & 7) * 4;
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsS, (r * a.lda + col) * 4, s_col * 4, 0);
-    }
-#else
-    (void)kt;
-    (void)u;
-#endif
-  };
-
   f32x4 acc[MB][NBH];
   const int koff = (lane >> 5) * 32 + ((lane >> 4) & 1) * 8;  // the lane's k within an LDS A row
   const uint16_t* const a_frag = sA + lc * FW_LD + koff;
   // one K-tile (parity P: LDS buffer P, W registers gb[P])
-  auto ktile = [&](auto par, auto nb, int kt, auto strm) {
+  auto ktile = [&](auto par, auto nb, int kt) {
     constexpr int P = decltype(par)::value, NB = decltype(nb)::value;
-    constexpr bool STRM = decltype(strm)::value;  // one of the first four K-tiles: stream a chunk
     __syncthreads();  // A tile kt visible in buffer P; buffer P^1 (tile kt-1) fully read
     const uint16_t* As = a_frag + P * (BM * FW_LD);
     const int kn = kt + 2 < nk ? kt + 2 : nk - 1;
 #if FW_NOUTER
     {
-      // n-outer over halves of the m-blocks (the whole tile at MB <= FW_MH_ALL): the half's A fragments
+      // n-outer over halves of the m-blocks (the whole tile at MB <= 5): the half's A fragments
       // read up front, then per column block n its MFMAs; in the last half block n's W registers
       // are dead after its MFMAs, so its loads for tile kt + 2 go right behind them, and the A
       // publish / loads sit between the first blocks (the MFMA pipe never waits on a staging
       // phase).  Every accumulator still sees p = 0, 1, 2 per K-tile in K-tile order.
-      constexpr int MH = MB <= FW_MH_ALL ? MB : (MB + 1) / 2, NH = (MB + MH - 1) / MH;
+      constexpr int MH = MB <= 5 ? MB : (MB + 1) / 2, NH = (MB + MH - 1) / MH;
       constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
@@ -328,12 +285,6 @@ __global__ __launch_bounds__(FW_NT, 1) void k_forward_h3(FwdArgs a) {
           if (h == 0 && n == 0) publish(ra, P ^ 1);
           if (h == 0 && n == (NB > 1 ? 1 : 0)) loadA(ra, kn);
           if (h == NH - 1) {
-            // (a streamed chunk before block n's W loads: those retire behind it, in order, by
-            // the next K-tile's MFMAs -- two barriers before any wave loads the slice)
-            if constexpr (STRM) {
-              stream_piece(kt, n);
-              __builtin_amdgcn_sched_barrier(0);
-            }
 #pragma unroll
             for (int l = 0; l < 2; ++l)
               gb[P][n][l] = __builtin_bit_cast(
@@ -379,17 +330,9 @@ __global__ __launch_bounds__(FW_NT, 1) void k_forward_h3(FwdArgs a) {
     for (int m = 0; m < MB; ++m)
 #pragma unroll
       for (int n = 0; n < NBH; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // nk is even (K % 64 == 0) and >= 8; the first four K-tiles also write out the streamed half
-    // of the previous slice (a separate copy of the loop body: no branch in the main loop)
-    constexpr std::integral_constant<bool, STREAM> strm{};
-    constexpr std::integral_constant<bool, false> nostrm{};
-    for (int kt = 0; kt < 4; kt += 2) {
-      ktile(std::integral_constant<int, 0>{}, nb, kt, strm);
-      ktile(std::integral_constant<int, 1>{}, nb, kt + 1, strm);
-    }
-    for (int kt = 4; kt < nk; kt += 2) {
-      ktile(std::integral_constant<int, 0>{}, nb, kt, nostrm);
-      ktile(std::integral_constant<int, 1>{}, nb, kt + 1, nostrm);
+    for (int kt = 0; kt < nk; kt += 2) {  // nk is even (K % 64 == 0)
+      ktile(std::integral_constant<int, 0>{}, nb, kt);
+      ktile(std::integral_constant<int, 1>{}, nb, kt + 1);
     }
   };
   // the next layer's first tiles (A 0 -> rn... published after the exponents are updated)
@@ -460,14 +403,8 @@ __global__ __launch_bounds__(FW_NT, 1) void k_forward_h3(FwdArgs a) {
             const uint32_t b = __float_as_uint(x) & 0x7fffffffu;
             q = q > b ? q : b;
           }
-          if (STREAM && n >= 2) {
-#if FW_STREAM && FW_CT && FW_NOUTER
-            *reinterpret_cast<f32x4*>(&sH[(m * 16 + lc) * SHL + wave * 32 + (n - 2) * 16 + 4 * lq]) = v;
-#endif
-          } else {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsC, c_lane,
-                                                   (m * 16 * a.lda + col_off + n * 16) * 4, 0);
-          }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsC, c_lane,
+                                                 (m * 16 * a.lda + col_off + n * 16) * 4, 0);
         }
         // max over the 4 lanes lq holding the row's other columns, then over the waves (ds_max)
         uint32_t o = (uint32_t)__shfl_xor((int)q, 16);
@@ -508,7 +445,6 @@ __global__ __launch_bounds__(FW_NT, 1) void k_forward_h3(FwdArgs a) {
 #endif
     }
     store_bias(l + 1);  // the next layer's bias / exponents (sBias[par ^ 1]: last read a layer ago)
-    s_col = col_off;    // the next layer's first K-tiles write out this slice's LDS half
 #if FW_DRAIN
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slice is in memory before any wave reads it
 #endif
