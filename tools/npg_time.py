@@ -4,6 +4,7 @@ reference's torch-CPU NPG on the same data (host cores, torch threads as given).
 
 usage: python tools/npg_time.py [N] [S] [A] [cpu_threads]
 """
+import hashlib
 import os
 import sys
 import time
@@ -67,6 +68,8 @@ print(f"  consecutive updates (no set_param_values between them): {upd_ms:.3f} m
 npg.set_param_values(p0)  # the comparison below: one update from p0
 npg.train_from_arrays(obs_d, act_d, adv_d)
 torch.cuda.synchronize()
+print(f"  parameters after one update from p0: sha1 {hashlib.sha1(npg.get_param_values().tobytes()).hexdigest()[:16]} "
+      f"(equal across builds = bit-identical updates)")
 torch.set_num_threads(threads)
 shapes = R.policy_param_shapes(S, A, (32, 32))
 t0 = time.perf_counter()
