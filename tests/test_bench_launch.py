@@ -66,3 +66,21 @@ def test_hung_collective_times_out():
     ok = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--dry-run-hang-rank", "5",
                          "--dist-timeout", "30"], env=_env(), capture_output=True, text=True, timeout=170)
     assert ok.returncode == 0, ok.stderr[-2000:]  # no hung rank: the collective completes
+
+
+def test_plan_lanes_per_rank_shares():
+    """The lane x step plans of the 40 000-sample rollout per rank: lane counts that are
+    multiples of 1024 in [4096, max_lanes] covering the share, and the shapes the GPU share tests
+    pin (8192 x 5, 7168 x 3, 5120 x 2, 5120 x 1 at N = 1 / 2 / 4 / 8)."""
+    import math
+    sys.path.insert(0, ROOT)
+    import bench
+    expect = {1: (8192, 5), 2: (7168, 3), 4: (5120, 2), 8: (5120, 1)}
+    for n, plan in expect.items():
+        share = math.ceil(40000 / n)
+        assert bench.plan_lanes(share, 8192) == plan
+    for share in (1, 999, 4096, 5000, 12345, 40000, 65536, 100000):
+        for cap in (4096, 8192, 16384, 40960):
+            L, T = bench.plan_lanes(share, cap)
+            assert L % 1024 == 0 and 4096 <= L <= max(cap, 4096) and L * T >= share
+    assert bench.plan_lanes(40000, 8192, lanes=4096) == (4096, 10)  # configs[1]'s 4096 envs
