@@ -101,8 +101,8 @@ def parse():
                         "of CPU work per run on a 16-core share)")
     p.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL on ROCm) or gloo (rehearsal)")
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                   help="replay the whole rollout as captured HIP graph(s); auto: when a rank's rollout is "
-                        "small (< 16 384 samples) and host launch overhead would show")
+                   help="replay the whole rollout as captured HIP graph(s); auto = off: eager launches measured "
+                        "faster at every per-rank share on ROCm 7 (profiles/r05z_graph_vs_eager.txt)")
     p.add_argument("--fuse-assembly", choices=["on", "off"], default="off",
                    help="f16x3: the policy launch also writes the ensemble's x0 slice (RolloutEngine.fuse_assembly)")
     p.add_argument("--overlap", choices=["on", "off"], default="off",
@@ -529,9 +529,11 @@ def main():
     # 5.6 us gap before the first and after the last GEMM of every step (rocprofv3 trace,
     # profiles/r02_event_gaps.txt) -- 2 % of the timed region.  The other GEMM paths keep
     # HIP events.
+    # (auto: eager.  Round 2 replayed small per-rank rollouts as graphs to hide the host launch
+    # cost; on the round-5 kernels eager launches are 1.6-1.9 % faster at the N = 4 / 8 shares and
+    # 1 % at N = 1, profiles/r05z_graph_vs_eager.txt: the host stays ahead of the GPU either way.)
     graph = None
-    use_graph = args.mode == "engine" and (args.graph == "on" or (args.graph == "auto" and B * T < 16384 and
-                                                                  args.gemm == "f16x3"))
+    use_graph = args.mode == "engine" and args.graph == "on"
     if use_graph and args.gemm != "f16x3":
         raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
     timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
