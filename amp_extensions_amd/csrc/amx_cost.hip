@@ -36,26 +36,37 @@ __device__ inline double wave_sum(double v) {
 // out[f] = sum_p partials[p][f].  Block = 64 columns x 16 waves; wave w sums its contiguous
 // chunk of parts in ascending order, then the 16 chunk sums are added in wave order:
 // the result is deterministic (fixed association) and the dependent-add chain is n/16 long.
-__global__ __launch_bounds__(1024) void k_sum_partials(const double* __restrict__ partials, int n_parts, int F,
-                                                       double* __restrict__ out) {
-  __shared__ double red[16][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int f = blockIdx.x * 64 + lane;
-  const int per = (n_parts + 15) / 16;
-  const int p0 = w * per, p1 = min(n_parts, p0 + per);
+// Column sums of fp64 partial rows [n_parts][F] in a fixed order: a 1024-thread block per 16
+// columns, thread (g = t / 16, c = t % 16) summing the contiguous run of rows g*per .. of column
+// c in row order (64 runs per column: 20 rows each for the 40 960-row rollout's 1280 partial
+// rows, where 16 runs of 80 rows made the pass a chain of ten load round trips on 8 CUs), then
+// the 64 run sums added in run order.  Shared by k_sum_partials and k_feature_message, so both
+// give the same bits.
+constexpr int CS_COLS = 16, CS_RUNS = 64;
+__device__ inline void colsum_parts(const double* __restrict__ partials, int n_parts, int F, double* __restrict__ out) {
+  __shared__ double red[CS_RUNS][CS_COLS];
+  const int c = threadIdx.x % CS_COLS, g = threadIdx.x / CS_COLS;
+  const int f = blockIdx.x * CS_COLS + c;
+  const int per = (n_parts + CS_RUNS - 1) / CS_RUNS;
+  const int p0 = g * per, p1 = min(n_parts, p0 + per);
   double s = 0.0;
   if (f < F) {
 #pragma unroll 8
     for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];  // 8 loads in flight, same add order
   }
-  red[w][lane] = s;
+  red[g][c] = s;
   __syncthreads();
-  if (w == 0 && f < F) {
+  if (g == 0 && f < F) {
     double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][lane];
+#pragma unroll 8
+    for (int i = 0; i < CS_RUNS; ++i) t += red[i][c];
     out[f] = t;
   }
+}
+
+__global__ __launch_bounds__(1024) void k_sum_partials(const double* __restrict__ partials, int n_parts, int F,
+                                                       double* __restrict__ out) {
+  colsum_parts(partials, n_parts, F, out);
 }
 
 // w = (float)(sum/count) - phi_e ; mmd = dot(w, w).  One block; F <= 4096.
@@ -350,24 +361,7 @@ __global__ __launch_bounds__(256) void k_mmd_relabel(RelabelArgs a) {
 // sample count in slot F of the same message, so the all-reduce / fit read one buffer.
 __global__ __launch_bounds__(1024) void k_feature_message(const double* __restrict__ partials, int n_parts, int F,
                                                           double count, double* __restrict__ out) {
-  __shared__ double red[16][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int f = blockIdx.x * 64 + lane;
-  const int per = (n_parts + 15) / 16;
-  const int p0 = w * per, p1 = min(n_parts, p0 + per);
-  double s = 0.0;
-  if (f < F) {
-#pragma unroll 8
-    for (int p = p0; p < p1; ++p) s += partials[(long long)p * F + f];  // 8 loads in flight, same add order
-  }
-  red[w][lane] = s;
-  __syncthreads();
-  if (w == 0 && f < F) {
-    double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += red[i][lane];
-    out[f] = t;
-  }
+  colsum_parts(partials, n_parts, F, out);
   if (blockIdx.x == 0 && threadIdx.x == 0) out[F] = count;
 }
 
@@ -416,8 +410,8 @@ __global__ __launch_bounds__(256) void k_amp_reward(const float* __restrict__ h,
 extern "C" int amx_sum_partials(amx_ctx* ctx, const double* partials, int n_parts, int F, double* out,
                                 void* stream) {
   AMX_CHECK_ARG(ctx && partials && out && n_parts >= 0 && F > 0, "amx_sum_partials: bad argument");
-  hipLaunchKernelGGL(k_sum_partials, dim3((F + 63) / 64), dim3(1024), 0, (hipStream_t)stream, partials, n_parts,
-                     F, out);
+  hipLaunchKernelGGL(k_sum_partials, dim3((F + CS_COLS - 1) / CS_COLS), dim3(1024), 0, (hipStream_t)stream, partials,
+                     n_parts, F, out);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
@@ -551,8 +545,8 @@ extern "C" int amx_cost_rows(amx_ctx* ctx, const double* x0, long long ld0, int 
 extern "C" int amx_feature_message(amx_ctx* ctx, const double* partials, int n_parts, int F, double count,
                                    double* out, void* stream) {
   AMX_CHECK_ARG(ctx && partials && out && n_parts >= 0 && F > 0 && count >= 0.0, "amx_feature_message: bad argument");
-  hipLaunchKernelGGL(k_feature_message, dim3((F + 63) / 64), dim3(1024), 0, (hipStream_t)stream, partials, n_parts,
-                     F, count, out);
+  hipLaunchKernelGGL(k_feature_message, dim3((F + CS_COLS - 1) / CS_COLS), dim3(1024), 0, (hipStream_t)stream,
+                     partials, n_parts, F, count, out);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }
