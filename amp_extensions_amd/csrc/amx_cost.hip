@@ -229,9 +229,9 @@ __device__ inline void rows_dot(const float4 (&p)[R][NC > 0 ? NC : 1], const flo
 // k_mmd_relabel = k_mmd_fit + k_mmd_reward + k_expert_cost + k_sum_small: every block derives
 // the witness w from the (all-reduced) [sum phi | count] message into LDS (the same fp64
 // divide and fp32 subtraction as k_mmd_fit, so every block holds identical bits); block 0 also
-// publishes w and w.w; blocks [0, nr) score R rollout rows per wave, blocks [nr, nr + ne)
-// the expert rows b*4 + wave + k*4ne (k_expert_cost's assignment and per-wave order, R per
-// round trip).  Each wave issues its first rows' loads before the witness prologue.  The
+// publishes w and w.w; blocks [0, ne) take the expert rows b*4 + wave + k*4ne (k_expert_cost's
+// assignment and per-wave order, R per round trip), blocks [ne, ne + nr) score R rollout rows
+// per wave.  Each wave issues its first rows' loads before the witness prologue.  The
 // expert partials are handed to the last-arriving expert block (agent-scope counter,
 // cdna_hip_programming.md §5 split-K form: sc1 partial stores drained before the relaxed
 // counter add, one acquire in the reducer), which sums them in index order (deterministic)
@@ -253,10 +253,14 @@ __global__ __launch_bounds__(256) void k_mmd_relabel(RelabelArgs a) {
   __shared__ double red[256];
   __shared__ int last;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const bool roll = (int)blockIdx.x < a.nr;
+  // blocks [0, ne) take the expert rows (several row batches each: dispatched first, so their
+  // longer chains overlap the rollout blocks instead of trailing them), [ne, ne + nr) the
+  // rollout rows (one batch each)
+  const bool roll = (int)blockIdx.x >= a.ne;
   // this wave's first rows, in flight during the prologue
-  const int eb = blockIdx.x - a.nr;
-  const int r0 = roll ? (blockIdx.x * 4 + wave) * R : eb * 4 + wave;
+  const int eb = roll ? 0 : (int)blockIdx.x;
+  const int rb = roll ? (int)blockIdx.x - a.ne : 0;
+  const int r0 = roll ? (rb * 4 + wave) * R : eb * 4 + wave;
   const int step = roll ? 1 : a.ne * 4;
   const float* base = roll ? a.phi : a.erows;
   const int ld = roll ? a.ldphi : a.lde;
