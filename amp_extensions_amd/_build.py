@@ -41,35 +41,16 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (need ROCm); cannot build libamx_hip.so")
 
 
-# AMX_EXPERIMENTAL=1 in the environment: also compile csrc/experimental/*.hip (the measured-
-# slower A/B alternates: the limb-format forward) and -DAMX_EXPERIMENTAL=1 (the ring / 256 x 224
-# output tiles, the 128 x 256 RFF tile).  The shipped library is built without them.
-EXPERIMENTAL = os.environ.get("AMX_EXPERIMENTAL", "0") not in ("", "0")
-STAMP = os.path.join(PKG_DIR, "build", "experimental.flag")
-
-
 def sources() -> list[str]:
-    src = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
-    if EXPERIMENTAL:
-        src += sorted(glob.glob(os.path.join(CSRC, "experimental", "*.hip")))
-    return src
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
 def _deps() -> list[str]:
     return sources() + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
 
 
-def _flag_changed() -> bool:
-    """True when the last build used the other AMX_EXPERIMENTAL setting (everything rebuilds)."""
-    try:
-        with open(STAMP) as f:
-            return f.read().strip() != str(int(EXPERIMENTAL))
-    except OSError:
-        return True
-
-
 def up_to_date() -> bool:
-    if not os.path.exists(LIB_PATH) or _flag_changed():
+    if not os.path.exists(LIB_PATH):
         return False
     t = os.path.getmtime(LIB_PATH)
     return all(os.path.getmtime(p) <= t for p in _deps())
@@ -85,10 +66,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if not force and up_to_date():
         return LIB_PATH
     os.makedirs(os.path.join(PKG_DIR, "build"), exist_ok=True)
-    force = force or _flag_changed()
     hdr_t = max((os.path.getmtime(p) for p in _deps() if not p.endswith(".hip")), default=0.0)
-    cc = [_hipcc(), *[f for f in HIPCC_FLAGS if f != "-shared"], "-I", INCLUDE, "-I", CSRC,
-          f"-DAMX_EXPERIMENTAL={int(EXPERIMENTAL)}"]
+    cc = [_hipcc(), *[f for f in HIPCC_FLAGS if f != "-shared"], "-I", INCLUDE, "-I", CSRC]
     procs = []
     for src in sources():
         obj = _obj(src)
@@ -114,8 +93,6 @@ def build(force: bool = False, verbose: bool = True) -> str:
     if res.returncode != 0:
         raise RuntimeError(f"hipcc link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
     os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    with open(STAMP, "w") as f:
-        f.write(str(int(EXPERIMENTAL)))
     return LIB_PATH
 
 

@@ -13,10 +13,9 @@ import re
 from . import _build
 
 _HEADER = os.path.join(_build.INCLUDE, "amx_hip.h")
-# entry points of include/amx_hip_experimental.h: bound only when the library was built with
-# AMX_EXPERIMENTAL=1 (the default library does not export them)
-EXPERIMENTAL = ("amx_set_lb_stage", "amx_assemble_input_limbs", "amx_gemm_bias_act_lb", "amx_gemm_out_unnorm_lb",
-                "amx_forward_h3_rows", "amx_forward_h3", "amx_fwd_weight_image")
+# AMX_ABI_VERSION of include/amx_hip.h (2: RFF column partials per 32 rows, AMX_RFF_PART_ROWS;
+# the measured-slower A/B entry points removed)
+ABI_VERSION = 2
 
 c_int, c_ll, c_dbl, c_flt, c_u64, c_u32, vp = C.c_int, C.c_longlong, C.c_double, C.c_float, C.c_uint64, C.c_uint32, C.c_void_p
 ip = C.POINTER(C.c_int)
@@ -53,12 +52,6 @@ SIGNATURES = {
                                     c_int, c_int, c_dbl, c_int, c_dbl]),
     "amx_assemble_input": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp]),
     "amx_assemble_input_rexp": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp, c_ll, c_ll, c_int, vp]),
-    "amx_set_lb_stage": (c_int, [vp, c_int]),
-    "amx_assemble_input_limbs": (c_int, [vp, vp, vp, c_int, vp, c_ll, c_int, c_int, vp, c_ll, vp]),
-    "amx_gemm_bias_act_lb": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll, vp, c_ll,
-                                     vp, c_int, c_ll, c_int, c_int, vp, c_ll, c_ll, vp, c_int, c_int, vp]),
-    "amx_gemm_out_unnorm_lb": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll, vp, c_ll,
-                                       vp, c_int, c_ll, vp, c_ll, c_ll, c_int, c_int, vp]),
     "amx_gemm_bias_act": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
                                   vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp]),
     "amx_gemm_out_unnorm": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll,
@@ -76,10 +69,6 @@ SIGNATURES = {
                                      vp, c_ll, vp, c_int, c_ll, c_int, c_int, vp, c_ll, c_int, vp, c_int, vp]),
     "amx_gemm_out_unnorm_h3": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, c_ll, vp, c_ll,
                                        vp, c_ll, vp, c_int, c_ll, vp, c_ll, c_int, c_int, vp]),
-    "amx_forward_h3_rows": (c_int, [vp, c_int, c_int]),
-    "amx_fwd_weight_image": (c_int, [vp, c_int, c_int, c_int, vp, vp, vp]),
-    "amx_forward_h3": (c_int, [vp, c_int, c_int, c_int, c_int, c_int, vp, c_int, c_ll, vp, vp, vp, c_int, vp, c_int,
-                               c_ll, vp, c_ll, c_int, vp]),
     "amx_set_motion": (c_int, [vp, vp, c_ll]),
     "amx_motion_duration": (c_dbl, [vp]),
     "amx_motion_states": (c_int, [vp, vp, c_int, c_int, vp, c_ll, vp]),
@@ -124,7 +113,6 @@ SIGNATURES = {
     "amx_set_gemm_timer": (c_int, [vp, vp]),
     "amx_split_workspace_floats": (c_ll, [vp, c_int, c_int, ip]),
     "amx_set_split_workspace": (c_int, [vp, vp, c_ll, vp, c_int]),
-    "amx_set_out_tile": (c_int, [vp, c_int]),
     "amx_policy_blob_floats": (c_ll, [vp, c_int, c_int]),
     "amx_policy_pack": (c_int, [vp, vp, vp, c_int, vp, vp, c_int, vp, vp, vp, vp]),
     "amx_rff_features": (c_int, [vp, c_int, c_int, c_int, c_int, vp, c_int, vp, c_int, vp, c_flt, vp, c_int,
@@ -190,21 +178,14 @@ def load(path: str | None = None, build_if_missing: bool = False):
     except OSError as e:
         raise AmxNativeError(f"cannot load {path}: {e}") from e
     for name, (res, args) in SIGNATURES.items():
-        if name in EXPERIMENTAL and not hasattr(lib, name):
-            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.amx_abi_version() != 1:
+    if lib.amx_abi_version() != ABI_VERSION:
         raise AmxNativeError("libamx_hip ABI version mismatch")
     if path == _build.LIB_PATH:
         _LIB = lib
     return lib
-
-
-def has_experimental(lib) -> bool:
-    """The library was built with AMX_EXPERIMENTAL=1 (the limb-format and one-launch forwards are present)."""
-    return all(hasattr(lib, n) for n in EXPERIMENTAL)
 
 
 def check(rc: int, what: str = "") -> None:

@@ -18,6 +18,14 @@ import torch.nn as nn
 from . import _native as N
 from .engine import AmxContext, RffMap, round_up, split_bf16x3, split_f16x2
 
+
+def device_discrepancy(ensemble, states, actions) -> torch.Tensor:
+    """get_action_discrepancy (dynamics.py:154-165) left on the GPU, for any ensemble the
+    surfaces accept (this package's DynamicsEnsemble / DeviceEnsemble, or the reference's own
+    object, converted once: ensemble.as_device_ensemble)."""
+    from .ensemble import as_device_ensemble
+    return as_device_ensemble(ensemble).get_action_discrepancy(states, actions)
+
 # cost-input row of a transition (linear_cost.py:115-127, gail_cost.py:258-268); "amp" is
 # the AMP observation of (s, s') (SceneImitateAMP::BuildAMPObs, via a ReferenceMotion)
 INPUT_TYPES = ("ss", "sa", "sas", "s", "amp")
@@ -300,7 +308,7 @@ class RBFLinearCost:
         """linear_cost.py:111-152: cost [T, 1] and the info dict."""
         x = cost_input(self.input_type, states, actions, next_states, self.motion)
         phi = self.get_rep(x)
-        disc = ensemble.get_action_discrepancy(states, actions)
+        disc = device_discrepancy(ensemble, states, actions)
         reward, ipm, wb = self._values(phi, disc, ensemble.threshold)
         cost = -reward
         rff_cost = self.get_costs(x)
@@ -462,7 +470,7 @@ class GAILCost:
         """gail_cost.py:254-279: cost = (1-lambda) * input cost - lambda * disagreement."""
         x = cost_input(self.input_type, states, actions, next_states, self.motion)
         xp, rows, n = self._pad(x)
-        disc = ensemble.get_action_discrepancy(states, actions)
+        disc = device_discrepancy(ensemble, states, actions)
         reward = self.rewards_from_input(xp, rows, n, disc)
         input_cost = self.get_costs(x)
         lam = np.float32(self.lambda_b)

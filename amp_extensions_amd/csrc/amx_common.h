@@ -48,8 +48,6 @@ struct amx_ctx {
   long long split_floats;
   uint32_t* split_cnt;       //   and its per-tile arrival counters (zero when idle)
   int split_ncnt;
-  int out_tile;              // amx_set_out_tile: output-layer tile of the f16x3 forward (0 = default)
-  int lb_stage;              // amx_set_lb_stage: limb forward's K-loop staging (0 registers, 1 LDS-DMA; A/B)
   int step_act_w8;           // amx_set_step_act_occupancy: k_step_act at two workgroups per CU (A/B)
   double* d_npg_scratch;     // amx_npg_reduce's run sums
   size_t npg_scratch_bytes;
@@ -81,9 +79,6 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 #define AMX_CHECK_LAUNCH() AMX_CHECK_HIP(hipGetLastError())
-
-// split-K scratch (floats) the limb-format GEMMs may use at this shape (amx_gemm_lb.hip)
-long long lb_split_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters);
 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 static inline int round_up(int x, int m) { return (x + m - 1) / m * m; }

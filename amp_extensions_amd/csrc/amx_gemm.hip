@@ -93,13 +93,6 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #define H3_EXP 0
 #endif
 // OUT80 (A/B builds): 1 = the 80 x 224 output tile where it makes exactly one tile per CU
-// AMX_EXPERIMENTAL (build: AMX_EXPERIMENTAL=1 python -m amp_extensions_amd._build): the
-// measured-slower A/B alternates -- the LDS-DMA ring output tile (amx_set_out_tile 2 / 3), the
-// 256 x 224 stream-K output tile (4), the 128 x 256 RFF tile (RFF_TILE) and, in its own source
-// (experimental/amx_gemm_lb.hip), the limb-format forward.  Off in the shipped library.
-#ifndef AMX_EXPERIMENTAL
-#define AMX_EXPERIMENTAL 0
-#endif
 #ifndef OUT80
 #define OUT80 1
 #endif
@@ -107,13 +100,6 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 // when its tiles exceed one round at two per CU
 #ifndef RFF_OCC3
 #define RFF_OCC3 1
-#endif
-// RFF_TILE (A/B builds): 1 = the 128 x 256 16x16x32 split-schedule tile (H128x256) for the RFF
-// pass where it fills the CUs -- measured equal to the 128 x 128 tiles at 40 960 rows (95 us) and
-// 1 us slower at 20 480 (profiles/r04h_rff_ab.txt): both run the pass in ceil(2.5) = 3 rounds of
-// one CU's worth of tiles, so the default stays 0
-#ifndef RFF_TILE
-#define RFF_TILE 0
 #endif
 // RFF_EXP (diagnostic builds, tools/src_variant.sh): 1 = no cos, 2 = no phi store
 #ifndef RFF_EXP
@@ -1274,268 +1260,6 @@ __global__ __launch_bounds__(TL::NT, TL::OCC) void k_gemm_h3(GemmArgs a) {
 
 // fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
 // [g][rows]: one wave per row (max |w| over K, then the split)
-#if AMX_EXPERIMENTAL
-#endif  // AMX_EXPERIMENTAL
-
-// fp32 [g][rows][K] -> scaled 2-limb f16 image [g][rows][K/16][2][16] + row exponents
-// [g][rows]: one wave per row (max |w| over K, then the split)
-// ==== output layer on an LDS-DMA ring =======================================================
-// The output layer (N = S <= 240 columns, K = k0 + 4H = 2304) reads every activation row once
-// (277 MB per forward at 8192 lanes x 4 members), and its register-staged 128 x 224 tile
-// (h3_tile, 14 waves at the 128-VGPR cap) keeps A two K-tiles and W one K-tile ahead: its time
-// per K-tile (~1.2-1.9 us) barely depends on the rows per tile, i.e. the loop waits on loads.
-// (Measured: bit-identical but not faster -- the compute loop of 8 waves alone, with no DMA,
-// takes about as long as the whole register-staged layer, and the ring's two K-tiles of A in
-// flight hide no more HBM latency than the staged tile's; DESIGN §6.  Kept as an A/B option,
-// amx_set_out_tile 2 / 3, tested bit-identical.)
-// Here both operands arrive by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no LDS write pass)
-// into a ring of R = 3 slots, two K-tiles ahead of the MFMAs:
-//   slot = [A: BM rows x 32 f32, raw | W: BN rows x (2 granules x 2 limbs x 16 f16)], 128-B rows
-//   whose 16-B chunks are XOR-swizzled by (row >> 1) & 7 -- on the DMA's per-lane SOURCE
-//   address (its destination is lane-linear) and on the fragment read -- so the 16 rows of a
-//   ds_read_b128 lane group land on distinct bank slots.
-// Each wave splits its own A fragments (8 f32 per lane and 16-row block: the row-exponent
-// scale and the two fp16 limbs of split2, as h3_tile's staging) and issues the same three limb
-// products per 16 x 16 block and K-tile in the same order as h3_tile, so a tile whose K range
-// is not split carries the same bits as the register-staged tile.
-// Per K-tile: a counted vmcnt (the next tile's DMA stays in flight) + lgkmcnt(0) + s_barrier;
-// the DMA of tile t + 2 into the slot tile t - 1 used; then tile t's fragments and MFMAs.
-// Only LDS-DMA is in flight in the K loop (an ordinary global load there would make hipcc wait
-// vmcnt(0)); the row exponents are loaded before it, the epilogue operands after it.
-// Waves: WM x WN, each MB x NB blocks of 16 x 16; the default is 8 waves of 16 x 16*NB (one A
-// block per wave: no A fragment is split twice).
-template <int WM_, int WN_, int MB_, int NB_>
-struct TileRing {
-  static constexpr int WM = WM_, WN = WN_, MB = MB_, NB = NB_;
-  static constexpr int NW = WM * WN, NT = NW * 64;
-  static constexpr int WROWS = MB * 16, WCOLS = NB * 16;
-  static constexpr int BM = WM * WROWS, BN = WN * WCOLS, BK = 32;
-  static constexpr int A_BYTES = BM * 128, W_BYTES = BN * 128, SLOT = A_BYTES + W_BYTES;
-  static constexpr int R = 3;                           // ring slots: two K-tiles in flight
-  static constexpr int PA = A_BYTES / 1024, P = SLOT / 1024;  // 1-KB DMA pieces per K-tile (A first)
-  static constexpr int PMAX = (P + NW - 1) / NW;        // pieces of the first (P % NW or all) waves
-  static constexpr int PFULL = P % NW == 0 ? NW : P % NW;
-  static constexpr size_t LDS = (size_t)R * SLOT;
-  static_assert(BM % 8 == 0 && BN % 8 == 0 && PMAX >= 2 && LDS <= 160 * 1024, "ring tile");
-};
-
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef const __attribute__((address_space(1))) void glb_void_t;
-
-// counted wait for this wave's DMA pieces of the current K-tile (IN_FLIGHT: the next tile's
-// N pieces may stay outstanding), every LDS read retired, then the workgroup barrier
-template <int N>
-__device__ __forceinline__ void ring_wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-}
-
-template <class TL>
-__device__ __forceinline__ void ring_tile(const GemmArgs& a, int tile, int kb, int ke, int seg, int nseg) {
-  constexpr int MB = TL::MB, NB = TL::NB, NW = TL::NW;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  char* const lds = reinterpret_cast<char*>(smem);
-  int g, tm, tn;
-  tile_coords(a, tile, g, tm, tn);
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int wm = wave / TL::WN, wn = wave % TL::WN;
-  const int lr = lane & 15, q = lane >> 4;
-  // fragment rows start at multiples of 16, so the lane's chunk swizzle is (lr >> 1) & 7
-  const int sw = (lr >> 1) & 7;
-
-  // scale exponents of the lane's A fragment rows (max over the row-exponent slots this
-  // launch reads; h3_tile's sExp), loaded before any DMA is in flight
-  int a_sh[MB];
-  {
-    const int* re = a.row_exp + (long long)g * a.strideRexp + (long long)tm * TL::BM;
-    const long long slot = (long long)a.tiles_m * TL::BM;
-#pragma unroll
-    for (int m = 0; m < MB; ++m) {
-      const int r = wm * TL::WROWS + m * 16 + lr;
-      int e = -100;
-      for (int s = 0; s < a.rexp_slots; ++s) {
-        const int v = re[s * slot + r];
-        e = v > e ? v : e;
-      }
-      a_sh[m] = HSC - e;
-    }
-  }
-
-  // DMA pieces of this wave: p = wave + NW i (i < PMAX, p < P); A pieces first (i < PA / NW).
-  // A piece = 8 rows x 128 B: lane -> row (lane >> 3) of the 8, physical chunk lane & 7, which
-  // holds the row's logical chunk (lane & 7) ^ ((row >> 1) & 7); the lane's source address of
-  // K-tile kt is its K-tile-0 address + 128 kt bytes (32 f32 of A, 2 x 2 x 16 f16 of W), the
-  // A rows of the shared x0 slice (kt < k_shared / 32) read from group 0's rows
-  constexpr int PI_A = TL::PA / NW;
-  static_assert(TL::PA % NW == 0, "A pieces per wave");
-  const long long ldw2 = 2LL * a.K;
-  const char* src[TL::PMAX];
-  {
-    const char* Ab = reinterpret_cast<const char*>(a.A + (long long)g * a.strideA + (long long)tm * TL::BM * a.lda);
-    const char* Wb = reinterpret_cast<const char*>(a.W2 + (long long)g * a.strideW2 + (long long)tn * TL::BN * ldw2);
-    const int prow = lane >> 3, pch = lane & 7;
-#pragma unroll
-    for (int i = 0; i < TL::PMAX; ++i) {
-      const int p = wave + NW * i;
-      const int r = (i < PI_A ? p : p - TL::PA) * 8 + prow;
-      const int c = pch ^ ((r >> 1) & 7);
-      src[i] = i < PI_A ? Ab + ((long long)r * a.lda + 4 * c) * 4 : Wb + ((long long)r * ldw2 + 8 * c) * 2;
-    }
-  }
-  const long long x0_back = (long long)g * a.strideA * 4;  // bytes from group g's rows to group 0's
-  const int nks = a.k_shared / TL::BK;
-  auto issue = [&](int kt, int slot) {
-    char* base = lds + slot * TL::SLOT + wave * 1024;
-    const long long ka = (long long)kt * 128 - (kt < nks ? x0_back : 0), kw = (long long)kt * 128;
-#pragma unroll
-    for (int i = 0; i < TL::PMAX; ++i) {
-      if (wave + NW * i < TL::P)
-        __builtin_amdgcn_global_load_lds((glb_void_t*)(src[i] + (i < PI_A ? ka : kw)),
-                                         (lds_void_t*)(base + NW * i * 1024), 16, 0, 0);
-    }
-  };
-  const bool full = wave < TL::PFULL;  // this wave issues PMAX pieces per K-tile (else PMAX - 1)
-  auto wait_tile = [&](bool next_in_flight) {
-    if (!next_in_flight) ring_wait_barrier<0>();
-    else if (full) ring_wait_barrier<TL::PMAX>();
-    else ring_wait_barrier<TL::PMAX - 1>();
-  };
-
-  f32x4 acc[MB][NB];
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int n = 0; n < NB; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // the lane's byte offsets: A k = 8q..8q+7 (f32 chunks 2q, 2q+1); W limb l of the same k
-  // ([granule][limb][16] rows: chunk 4 (q >> 1) + 2 l + (q & 1))
-  const int ca0 = ((2 * q) ^ sw) * 16, ca1 = ((2 * q + 1) ^ sw) * 16;
-  const int cw0 = ((4 * (q >> 1) + (q & 1)) ^ sw) * 16, cw1 = ((4 * (q >> 1) + 2 + (q & 1)) ^ sw) * 16;
-  const int a_off = (wm * TL::WROWS + lr) * 128, w_off = TL::A_BYTES + (wn * TL::WCOLS + lr) * 128;
-  // W fragment reads run WPF blocks ahead of their MFMAs (pinned by sched_barrier: hipcc
-  // otherwise waits for each block's reads right before its three MFMAs)
-  constexpr int WPF = NB < 4 ? NB : 4;
-  auto compute = [&](int slot) {
-    const char* S0 = lds + slot * TL::SLOT;
-    f32x4 xa[MB][2];
-    f16x8 wb[NB][2];
-#pragma unroll
-    for (int m = 0; m < MB; ++m) {
-      const char* ar = S0 + a_off + m * 16 * 128;
-      xa[m][0] = *reinterpret_cast<const f32x4*>(ar + ca0);
-      xa[m][1] = *reinterpret_cast<const f32x4*>(ar + ca1);
-    }
-#pragma unroll
-    for (int n = 0; n < WPF; ++n) {
-      const char* wr = S0 + w_off + n * 16 * 128;
-      wb[n][0] = *reinterpret_cast<const f16x8*>(wr + cw0);
-      wb[n][1] = *reinterpret_cast<const f16x8*>(wr + cw1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    f16x8 ah[MB], al[MB];
-#pragma unroll
-    for (int m = 0; m < MB; ++m) {
-      f32x4 x0 = xa[m][0], x1 = xa[m][1];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        x0[i] = __builtin_amdgcn_ldexpf(x0[i], a_sh[m]);
-        x1[i] = __builtin_amdgcn_ldexpf(x1[i], a_sh[m]);
-      }
-      u32x2 h0, l0, h1, l1;
-      split2(x0, h0, l0);
-      split2(x1, h1, l1);
-      ah[m] = __builtin_bit_cast(f16x8, u32x4{h0.x, h0.y, h1.x, h1.y});
-      al[m] = __builtin_bit_cast(f16x8, u32x4{l0.x, l0.y, l1.x, l1.y});
-    }
-#pragma unroll
-    for (int n = 0; n < NB; ++n) {
-      if (n + WPF < NB) {
-        const char* wr = S0 + w_off + (n + WPF) * 16 * 128;
-        wb[n + WPF][0] = *reinterpret_cast<const f16x8*>(wr + cw0);
-        wb[n + WPF][1] = *reinterpret_cast<const f16x8*>(wr + cw1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // per block: (a1, b0), (a0, b1), (a0, b0) -- h3_tile's order
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[m], wb[n][0], acc[m][n], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], wb[n][1], acc[m][n], 0, 0, 0);
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[m], wb[n][0], acc[m][n], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  issue(kb, 0);
-  if (kb + 1 < ke) issue(kb + 1, 1);
-  int slot = 0;  // (kt - kb) % R
-  for (int kt = kb; kt < ke; ++kt) {
-    wait_tile(kt + 1 < ke);
-    if (kt + 2 < ke) issue(kt + 2, slot == 0 ? 2 : slot - 1);  // the slot tile kt - 1 used
-    compute(slot);
-    slot = slot == 2 ? 0 : slot + 1;
-  }
-  if (nseg > 1) {
-    __syncthreads();  // the ring is free: one int of LDS for the last-arriver flag
-    if (!split_combine<TL>(a, acc, tile, seg, nseg, reinterpret_cast<int*>(smem))) return;
-  }
-  // EPI_UNNORM (epilogue_h3_m16's): the exponents of the lane's accumulator rows 4q + j of
-  // each block come from the lanes whose fragment rows they are (lane 4q + j)
-  int er[MB][4];
-#pragma unroll
-  for (int m = 0; m < MB; ++m)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) er[m][j] = HSC - __shfl(a_sh[m], 4 * q + j);
-  const float* bias = a.bias + (long long)g * a.strideBias;
-  const int* wexp = a.w_exp + (long long)g * a.strideWexp;
-  float* Cg = a.C + (long long)g * a.strideC;
-  const int row0 = tm * TL::BM + wm * TL::WROWS, col0 = tn * TL::BN + wn * TL::WCOLS;
-#pragma unroll
-  for (int n = 0; n < NB; ++n) {
-    const int col = col0 + n * 16 + lr;
-    if (col < a.n_valid) {
-      const float bv = bias[col];
-      const float sc = a.scale[col], sh = a.shift[col];
-      const int ec = wexp[col] - 2 * HSC;
-#pragma unroll
-      for (int m = 0; m < MB; ++m)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = row0 + m * 16 + 4 * q + j;
-          const float y = __builtin_amdgcn_ldexpf(acc[m][n][j], er[m][j] + ec) + bv;
-          const float prod = y * sc;  // two roundings, as torch's (y*scale)+mean
-          Cg[(long long)row * a.ldc + col] = prod + sh;
-        }
-    }
-  }
-}
-
-// one tile per workgroup (XCD-contiguous order), or stream-K as k_gemm_h3
-template <class TL>
-__global__ __launch_bounds__(TL::NT, 1) void k_gemm_ring(GemmArgs a) {
-  const int nk = a.K / TL::BK;
-  if (a.streamk) {
-    const long long U = (long long)a.tiles_m * a.tiles_n * a.groups * nk, G = gridDim.x;
-    const int v = xcd_logical((int)G, (int)blockIdx.x);
-    long long u = (long long)v * U / G;
-    const long long uend = ((long long)v + 1) * U / G;
-    while (u < uend) {
-      const int tile = (int)(u / nk), kb = (int)(u - (long long)tile * nk);
-      const int ke = (uend - u) < (long long)(nk - kb) ? kb + (int)(uend - u) : nk;
-      const long long u0 = (long long)tile * nk;
-      const int wf = (int)(((u0 + 1) * G - 1) / U), wl = (int)(((u0 + nk) * G - 1) / U);
-      ring_tile<TL>(a, tile, kb, ke, v - wf, wl - wf + 1);
-      u += ke - kb;
-      __syncthreads();  // LDS reuse by the next segment
-    }
-  } else {
-    ring_tile<TL>(a, xcd_logical(a.tiles_m * a.tiles_n * a.groups, (int)blockIdx.x), 0, nk, 0, 1);
-  }
-  if (a.timer_role == 2) gemm_timer_end(a);
-}
-
 __global__ __launch_bounds__(256) void k_split_f16x2(const float* __restrict__ W, int ldw, long long strideW,
                                                      int rows, int K, uint16_t* __restrict__ W2, long long strideW2,
                                                      int* __restrict__ w_exp, long long strideWexp) {
@@ -1632,11 +1356,6 @@ using H128x224 = TileH3<2, 7, 2, 1, 4, 2, true, true, true, 0, 0, true, true, tr
 using H80x224 = TileH3<1, 7, 1, 1, 1, 2, true, true, true, 5, 2, true, true, true, true>;  // + DEEPA
 
 
-#if AMX_EXPERIMENTAL
-// output layer, 256-row stream-K tiles (amx_set_out_tile 4): 8 waves of 64 x 112 on 16x16x32
-// (28 blocks); A + W fetched per FLOP 0.68x the 128 x 224 tile's
-using H256x224 = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 4, 7, true, true, true>;
-#endif
 using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
 using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
 
@@ -1698,21 +1417,6 @@ int launch_h3(GemmArgs& a, hipStream_t stream) {
   return AMX_OK;
 }
 
-#if AMX_EXPERIMENTAL
-template <class TL>
-int launch_ring(GemmArgs& a, hipStream_t stream) {
-  a.tiles_m = a.rows / TL::BM;
-  a.tiles_n = 1;
-  a.N = TL::BN;
-  const int tiles = a.tiles_m * a.groups;
-  const int nwg = a.streamk ? a.streamk : tiles;  // stream-K: a.streamk workgroups
-  if (tiles == 0) return AMX_OK;
-  hipLaunchKernelGGL((k_gemm_ring<TL>), dim3(nwg), dim3(TL::NT), TL::LDS, stream, a);
-  AMX_CHECK_LAUNCH();
-  return AMX_OK;
-}
-
-#endif
 
 int check_common(const char* fn, int groups, int rows, int K, const float* A, int lda, const float* W,
                  int ldw) {
@@ -2084,31 +1788,6 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
   a.shift = ctx->d_norm + 2 * S + 2 * Ad;  // mu_d
   a.scale = ctx->d_norm + 3 * S + 2 * Ad;  // sd_d
   const hipStream_t s = (hipStream_t)stream;
-  // the LDS-DMA ring tile (amx_set_out_tile 2: 8 waves of 16 x 16 NB, NB = ceil(S / 16) in
-  // 13..15; 3: 8 waves of 32 x 112; measured slower than the register-staged tile):
-  // one tile per workgroup, or stream-K at the lane counts whose 128-row tiles are fewer than
-  // the CUs (streamk_tiles), as the register-staged tile
-#if AMX_EXPERIMENTAL
-  const int nb16 = (n_valid + 15) / 16;
-  const int ring = (ctx->out_tile != 2 && ctx->out_tile != 3) || K % 32 != 0 || nb16 < 13 || nb16 > 15 ? 0
-                   : ctx->out_tile == 3 ? (nb16 <= 14 ? 3 : 0) : 2;
-  if (ring) {
-    const int bn = ring == 3 ? 224 : 16 * nb16;
-    AMX_CHECK_ARG(strideW2 >= 2LL * K * bn || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
-    int nwg = 0, ksplit = 0;
-    const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K);
-    if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
-        ctx->split_floats >= (long long)tiles * ksplit * 128 * bn) {
-      a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
-    }
-    if (ring == 3) return launch_ring<TileRing<4, 2, 2, 7>>(a, s);
-    switch (nb16) {
-      case 13: return launch_ring<TileRing<8, 1, 1, 13>>(a, s);
-      case 14: return launch_ring<TileRing<8, 1, 1, 14>>(a, s);
-      default: return launch_ring<TileRing<8, 1, 1, 15>>(a, s);
-    }
-  }
-#endif
   // weight rows padded to round_up(S, 128) (amx_layout n_out_pad); S <= 224 runs one 224-wide tile
   const int n32 = amx::round_up(n_valid, 32);
   // one wave of row-block tiles RB x (N/2) when rows = RB * n_cus / (2 groups), RB in {128..224}
@@ -2119,17 +1798,6 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     a.N = 224;
     AMX_CHECK_ARG(strideW2 >= 2LL * K * 224 || groups == 1, "amx_gemm_out_unnorm_h3: strideW2=%lld", strideW2);
     if (K % 32 != 0) return launch_h3<EPI_UNNORM, H128x224k16>(a, s);
-#if AMX_EXPERIMENTAL
-    if (ctx->out_tile == 4) {  // 256 x 224 tiles, stream-K over the CUs
-      int nwg = 0, ksplit = 0;
-      const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K, 256);
-      if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
-          ctx->split_floats >= (long long)tiles * ksplit * 256 * 224) {
-        a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
-        return launch_h3<EPI_UNNORM, H256x224>(a, s);
-      }
-    }
-#endif
 #if OUT80
     if (rows % 80 == 0 && (long long)groups * (rows / 80) == ctx->n_cus) return launch_h3<EPI_UNNORM, H80x224>(a, s);
 #endif
@@ -2197,9 +1865,6 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
 #if RFF_OCC3
     if ((long long)(rows / 128) * (F / 128) > 2LL * ctx->n_cus) return launch_h3<EPI_RFF, H128rff3>(a, (hipStream_t)stream);
 #endif
-#if AMX_EXPERIMENTAL && RFF_TILE == 1
-    if (F % 256 == 0 && (rows / 128) * (F / 256) >= ctx->n_cus) return launch_h3<EPI_RFF, H128x256>(a, (hipStream_t)stream);
-#endif
     return launch_h3<EPI_RFF, H128k32>(a, (hipStream_t)stream);
   }
   return launch_h3<EPI_RFF, H128>(a, (hipStream_t)stream);
@@ -2208,17 +1873,6 @@ extern "C" int amx_rff_features_h3(amx_ctx* ctx, int rows, int n_valid, int F, i
 extern "C" int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf) {
   AMX_CHECK_ARG(ctx, "amx_set_gemm_timer: null ctx");
   ctx->gemm_timer = buf;
-  return AMX_OK;
-}
-
-extern "C" int amx_set_out_tile(amx_ctx* ctx, int tile) {
-  AMX_CHECK_ARG(ctx, "amx_set_out_tile: null ctx");
-#if AMX_EXPERIMENTAL
-  AMX_CHECK_ARG(tile >= 0 && tile <= 4, "amx_set_out_tile: tile=%d not in 0..4", tile);
-#else
-  AMX_CHECK_ARG(tile >= 0 && tile <= 1, "amx_set_out_tile: tile=%d (2-4 need an AMX_EXPERIMENTAL=1 build)", tile);
-#endif
-  ctx->out_tile = tile;
   return AMX_OK;
 }
 
@@ -2242,21 +1896,8 @@ extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, 
                           ? streamk_hidden(ctx, groups, rows, ctx->H, ctx->k0_pad + (ctx->L - 1) * ctx->H, &nwg_h,
                                            &ksplit_h)
                           : 0;
-  int nwg2 = 0, ksplit2 = 0, tiles2 = 0, nc_lb = 0;
-  long long f_lb = 0;
-#if AMX_EXPERIMENTAL
-  // the 256-row output tiles (amx_set_out_tile 4)
-  tiles2 = streamk_tiles(ctx, groups, rows, &nwg2, &ksplit2, ctx->k0_pad + ctx->L * ctx->H, 256);
-  // the limb-format forward's stream-K shapes (experimental/amx_gemm_lb.hip)
-  f_lb = amx::lb_split_floats(ctx, groups, rows, &nc_lb);
-#endif
-  int nc = tiles > tiles_h ? tiles : tiles_h;
-  nc = nc > tiles2 ? nc : tiles2;
-  nc = nc > nc_lb ? nc : nc_lb;
+  const int nc = tiles > tiles_h ? tiles : tiles_h;
   if (n_counters) *n_counters = nc;
   const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
-  const long long f2 = (long long)tiles2 * ksplit2 * 256 * 224;
-  long long f = fo > fh ? fo : fh;
-  f = f > f2 ? f : f2;
-  return f > f_lb ? f : f_lb;
+  return fo > fh ? fo : fh;
 }

@@ -46,10 +46,6 @@ struct GemmArgs {
   uint32_t* split_cnt;     //   arrivals per tile (zero between launches: the last arriver resets it)
   uint64_t* timer;         // amx_set_gemm_timer buffer (null: off)
   int timer_role;          //   1: first layer of a forward (block 0 stamps the start), 2: output layer
-  // limb-format activations (amx_gemm_lb.hip): A is stored as scaled fp16 limb pairs, one
-  // exponent per row and chunk (x0, then 128-column chunks of the hidden slices)
-  int lb_k0;               // columns of chunk 0 (the x0 slice)
-  long long rexp_ld;       // elements between two exponent slots of one group (the padded rows)
 };
 
 // Linear block id -> (group, tile_m, tile_n).  Workgroups are dispatched round-robin over

@@ -12,8 +12,6 @@ inert), so any BasicMLP config runs on the same 128x128 MFMA tiles.
 """
 from __future__ import annotations
 
-import math
-import os
 
 import numpy as np
 import torch
@@ -74,11 +72,6 @@ class AmxContext:
         N.check(self.lib.amx_set_gemm_timer(self.h, self._timer.data_ptr()), "amx_set_gemm_timer")
         return self._timer
 
-    def set_out_tile(self, tile: int) -> None:
-        """Output-layer tile of the f16x3 forward (amx_set_out_tile): 0 default (= 1, the
-        register-staged tiles), 2 LDS-DMA ring with 16-row waves, 3 ring with 32 x 112 waves."""
-        N.check(self.lib.amx_set_out_tile(self.h, int(tile)), "amx_set_out_tile")
-
     @property
     def stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -108,24 +101,36 @@ class AmxContext:
                 "amx_gemm_bias_act")
 
 
-def split_bf16x3(ctx: AmxContext, W: torch.Tensor) -> torch.Tensor:
+def split_bf16x3(ctx: AmxContext, W: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """3-limb bf16 image [G][rows][K/16][3][16] (int16 bits) of a [G][rows][K] fp32 device
-    weight (amx_split_bf16x3), the operand of the amx_*_x6 GEMMs."""
+    weight (amx_split_bf16x3), the operand of the amx_*_x6 GEMMs; `out` rewrites an image in place."""
     G, rows, K = W.shape
     W = W.contiguous()
-    W3 = torch.empty(G, rows, 3 * K, dtype=torch.int16, device=ctx.device)
+    W3 = torch.empty(G, rows, 3 * K, dtype=torch.int16, device=ctx.device) if out is None else out
+    _check_dev(W3, torch.int16, "out", ctx.device)
+    if tuple(W3.shape) != (G, rows, 3 * K):
+        raise ValueError(f"out: expected shape {(G, rows, 3 * K)}, got {tuple(W3.shape)}")
     N.check(ctx.lib.amx_split_bf16x3(ctx.h, G, rows, K, W.data_ptr(), K, rows * K, W3.data_ptr(), rows * 3 * K,
                                      ctx.stream), "amx_split_bf16x3")
     return W3
 
 
-def split_f16x2(ctx: AmxContext, W: torch.Tensor):
+def split_f16x2(ctx: AmxContext, W: torch.Tensor, out=None):
     """Scaled 2-limb fp16 image [G][rows][K/16][2][16] (int16 bits) + row exponents [G][rows]
-    of a [G][rows][K] fp32 device weight (amx_split_f16x2), the operand of the amx_*_h3 GEMMs."""
+    of a [G][rows][K] fp32 device weight (amx_split_f16x2), the operand of the amx_*_h3 GEMMs;
+    `out` = (image, exponents) rewrites an existing pair in place."""
     G, rows, K = W.shape
     W = W.contiguous()
-    W2 = torch.empty(G, rows, 2 * K, dtype=torch.int16, device=ctx.device)
-    wexp = torch.empty(G, rows, dtype=torch.int32, device=ctx.device)
+    if out is None:
+        W2 = torch.empty(G, rows, 2 * K, dtype=torch.int16, device=ctx.device)
+        wexp = torch.empty(G, rows, dtype=torch.int32, device=ctx.device)
+    else:
+        W2, wexp = out
+        _check_dev(W2, torch.int16, "out[0]", ctx.device)
+        _check_dev(wexp, torch.int32, "out[1]", ctx.device)
+        if tuple(W2.shape) != (G, rows, 2 * K) or tuple(wexp.shape) != (G, rows):
+            raise ValueError(f"out: expected shapes {(G, rows, 2 * K)} and {(G, rows)}, got "
+                             f"{tuple(W2.shape)} and {tuple(wexp.shape)}")
     N.check(ctx.lib.amx_split_f16x2(ctx.h, G, rows, K, W.data_ptr(), K, rows * K, W2.data_ptr(), rows * 2 * K,
                                     wexp.data_ptr(), rows, ctx.stream), "amx_split_f16x2")
     return W2, wexp
@@ -147,94 +152,26 @@ class DeviceEnsemble:
 
     GEMM_PRECISIONS = ("f16x3", "bf16x6", "f32")
 
-    ACT_FORMATS = ("f32", "limbs")
-
-    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "f16x3",
-                 act_format: str = "f32"):
+    def __init__(self, ctx: AmxContext, weights, norms, threshold: float = 0.0, gemm: str = "f16x3"):
         """gemm: "bf16x6" (fp32 operands split into 3 bf16 limbs, 6 limb products on the bf16
         MFMA pipe: fp32-level error, amx_gemm_*_x6), "f16x3" (power-of-two scaled operands
-        split into 2 fp16 limbs, 3 products) or "f32" (v_mfma_f32_32x32x2_f32).
-        act_format (f16x3): "f32" (default) -- fp32 activation rows, split into limbs by every
-        consumer (amx_gemm_*_h3); "limbs" -- rows stored as scaled fp16 limb pairs with one
-        exponent per row and 128-column chunk, each value split once by its producer
-        (amx_assemble_input_limbs, amx_gemm_*_lb; hidden width a multiple of 256).  The limb form
-        is exact to the same tolerance and measured slower (the K loop's time per K-tile is the
-        same without the split, the limb epilogue costs more)."""
+        split into 2 fp16 limbs, 3 products; the default) or "f32" (v_mfma_f32_32x32x2_f32)."""
         if gemm not in self.GEMM_PRECISIONS:
             raise ValueError(f"gemm must be one of {self.GEMM_PRECISIONS}, got {gemm!r}")
-        if act_format not in self.ACT_FORMATS:
-            raise ValueError(f"act_format must be one of {self.ACT_FORMATS}, got {act_format!r}")
         self.gemm = gemm
-        lb_ok = (gemm == "f16x3" and ctx.Hp % 256 == 0 and ctx.k0_pad <= 1024
-                 and 1 + ctx.L * ctx.Hp // 128 <= 24)
-        if act_format == "limbs" and not lb_ok:
-            raise ValueError("act_format='limbs' needs gemm='f16x3', a hidden width that is a multiple of 256, "
-                             "S + A <= 1024 and at most 23 hidden chunks of 128 columns")
-        if act_format == "limbs" and not N.has_experimental(ctx.lib):
-            raise N.AmxNativeError("act_format='limbs' is an experimental A/B path: rebuild the library with "
-                                   "AMX_EXPERIMENTAL=1 python -m amp_extensions_amd._build")
-        self.limbs = act_format == "limbs"
-        # exponent slots per row: f32 format x0, h0 .. h_{L-1}; limbs x0 + one per 128 hidden columns
-        self.n_slots = 1 + ctx.L * ctx.Hp // 128 if self.limbs else ctx.L + 1
+        # exponent slots per row (f16x3): x0, h0 .. h_{L-1}
+        self.n_slots = ctx.L + 1
         self.shared_x0 = True  # f16x3: x0 assembled once, read by every member (k_shared)
         self.ctx = ctx
-        S, A, M, Hp, L = ctx.S, ctx.A, ctx.M, ctx.Hp, ctx.L
+        M, Hp, L = ctx.M, ctx.Hp, ctx.L
         if len(weights) != M:
             raise ValueError(f"expected {M} ensemble members, got {len(weights)}")
         hidden = weights[0][0][0].shape[0]
         self.hidden = hidden
         if round_up(hidden, 128) != Hp or len(weights[0]) != L + 1:
             raise ValueError("weights do not match the context's (hidden, n_hidden)")
-        dev, k0 = ctx.device, ctx.k0_pad
-        # original input column -> padded activation column
-        colmap = np.concatenate([np.arange(S + A)] + [k0 + i * Hp + np.arange(hidden) for i in range(L)])
-        self.W, self.b = [], []
-        for i in range(L + 1):
-            last = i == L
-            n_rows = ctx.n_out_pad if last else Hp
-            Kp = ctx.ldk if last else k0 + i * Hp
-            Wp = torch.zeros(M, n_rows, Kp, dtype=torch.float32)
-            bp = torch.zeros(M, n_rows, dtype=torch.float32)
-            for m in range(M):
-                W_m, b_m = weights[m][i]
-                W_m = torch.as_tensor(W_m).float().cpu()
-                out_dim, in_dim = W_m.shape
-                exp_in = S + A + i * hidden
-                if in_dim != exp_in or out_dim != (S if last else hidden):
-                    raise ValueError(f"layer {i} of member {m}: shape {tuple(W_m.shape)}, expected "
-                                     f"({S if last else hidden}, {exp_in})")
-                Wp[m, :out_dim][:, torch.from_numpy(colmap[:in_dim])] = W_m
-                bp[m, :out_dim] = torch.as_tensor(b_m).float().cpu()
-            self.W.append(Wp.to(dev).contiguous())
-            self.b.append(bp.to(dev).contiguous())
-        self.W3 = self.W2 = self.wexp = None
-        if gemm == "bf16x6":
-            self.W3 = [split_bf16x3(ctx, W) for W in self.W]
-        elif gemm == "f16x3":
-            sp = [split_f16x2(ctx, W) for W in self.W]
-            self.W2, self.wexp = [x[0] for x in sp], [x[1] for x in sp]
-        # f16x3 forward: "layers" (default) -- one launch per layer; "fused" -- the whole forward in
-        # one launch (amx_forward_h3, an AMX_EXPERIMENTAL=1 build) at the lane counts whose row
-        # blocks fill the CUs in one round, the per-layer launches elsewhere.  Same bits (whole-K
-        # output tiles); measured equal at the N = 8 share (DESIGN §6 round 5).  Env AMX_FORWARD.
-        self.forward_mode = os.environ.get("AMX_FORWARD", "layers")
-        if self.forward_mode not in ("fused", "layers"):
-            raise ValueError(f"AMX_FORWARD must be 'fused' or 'layers', got {self.forward_mode!r}")
-        self._fw_ptrs = None
-        self._fw_rows = {}
-        self.W2f = None
-        if self.W2 is not None and Hp == 512 and 1 <= L <= 8 and hasattr(ctx.lib, "amx_fwd_weight_image"):
-            # the one-launch forward reads its weights in fragment order (amx_fwd_weight_image)
-            self.W2f = []
-            for i, w in enumerate(self.W2):
-                rows, K2 = w.shape[1], w.shape[2]
-                wf = torch.empty_like(w)
-                N.check(ctx.lib.amx_fwd_weight_image(ctx.h, M, rows, K2 // 2, w.data_ptr(), wf.data_ptr(),
-                                                     ctx.stream), "amx_fwd_weight_image")
-                self.W2f.append(wf)
-            vp = N.C.c_void_p * (L + 1)
-            self._fw_ptrs = (vp(*[w.data_ptr() for w in self.W2f]), vp(*[w.data_ptr() for w in self.wexp]),
-                             vp(*[b.data_ptr() for b in self.b]))
+        self.W = self.b = self.W3 = self.W2 = self.wexp = None
+        self.set_weights(weights)
         ctx.set_normalizers(norms)
         self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
         self.threshold = float(threshold)
@@ -243,6 +180,57 @@ class DeviceEnsemble:
         # torch.cuda.Events recorded on the launch stream around the L+1 GEMM launches (inside
         # captured graphs use the context's in-kernel timer instead: AmxContext.gemm_timer)
         self.gemm_events = None
+
+    def set_weights(self, weights) -> None:
+        """(Re)load the members' nn.Linear weights, re-indexed into the dense-concat column
+        layout and split into the GEMM path's limb image.  After the first call the device
+        buffers are updated in place, so engines and captured graphs that hold their pointers
+        see the new weights (DynamicsEnsemble.load_ensemble, dynamics.py:118-131)."""
+        ctx = self.ctx
+        S, A, M, Hp, L = ctx.S, ctx.A, ctx.M, ctx.Hp, ctx.L
+        if len(weights) != M:
+            raise ValueError(f"expected {M} ensemble members, got {len(weights)}")
+        hidden = self.hidden
+        dev, k0 = ctx.device, ctx.k0_pad
+        # original input column -> padded activation column
+        colmap = np.concatenate([np.arange(S + A)] + [k0 + i * Hp + np.arange(hidden) for i in range(L)])
+        Ws, bs = [], []
+        for i in range(L + 1):
+            last = i == L
+            n_rows = ctx.n_out_pad if last else Hp
+            Kp = ctx.ldk if last else k0 + i * Hp
+            Wp = torch.zeros(M, n_rows, Kp, dtype=torch.float32)
+            bp = torch.zeros(M, n_rows, dtype=torch.float32)
+            for m in range(M):
+                if len(weights[m]) != L + 1:
+                    raise ValueError(f"member {m}: {len(weights[m])} layers, expected {L + 1}")
+                W_m, b_m = weights[m][i]
+                W_m = torch.as_tensor(W_m).detach().float().cpu()
+                out_dim, in_dim = W_m.shape
+                exp_in = S + A + i * hidden
+                if in_dim != exp_in or out_dim != (S if last else hidden):
+                    raise ValueError(f"layer {i} of member {m}: shape {tuple(W_m.shape)}, expected "
+                                     f"({S if last else hidden}, {exp_in})")
+                Wp[m, :out_dim][:, torch.from_numpy(colmap[:in_dim])] = W_m
+                bp[m, :out_dim] = torch.as_tensor(b_m).detach().float().cpu()
+            Ws.append(Wp)
+            bs.append(bp)
+        if self.W is None:
+            self.W = [w.to(dev).contiguous() for w in Ws]
+            self.b = [b.to(dev).contiguous() for b in bs]
+            if self.gemm == "bf16x6":
+                self.W3 = [split_bf16x3(ctx, W) for W in self.W]
+            elif self.gemm == "f16x3":
+                sp = [split_f16x2(ctx, W) for W in self.W]
+                self.W2, self.wexp = [x[0] for x in sp], [x[1] for x in sp]
+            return
+        for i in range(L + 1):
+            self.W[i].copy_(Ws[i])
+            self.b[i].copy_(bs[i])
+            if self.W3 is not None:
+                split_bf16x3(ctx, self.W[i], out=self.W3[i])
+            if self.W2 is not None:
+                split_f16x2(ctx, self.W[i], out=(self.W2[i], self.wexp[i]))
 
     @property
     def num_models(self) -> int:
@@ -256,8 +244,7 @@ class DeviceEnsemble:
             c = self.ctx
             ws = dict(Bp=Bp, act=torch.zeros(c.M, Bp, c.ldk, dtype=torch.float32, device=c.device),
                       preds=torch.zeros(c.M, Bp, c.S, dtype=torch.float32, device=c.device),
-                      # f16x3: row exponents [M][slots][Bp] (f32 format: x0, h0..h_{L-1}; limbs: x0, then
-                      # one slot per 128 hidden columns)
+                      # f16x3: row exponents [M][slots][Bp] (x0, h0..h_{L-1})
                       rexp=torch.zeros(c.M, self.n_slots, Bp, dtype=torch.int32, device=c.device))
             if self.W2 is not None:
                 self._ensure_split_workspace(Bp)
@@ -304,15 +291,6 @@ class DeviceEnsemble:
         s = c.stream
         rexp = ws["rexp"]
         k_shared = 0
-        if self.limbs:
-            if x0_ready or assembled:
-                raise ValueError("x0_ready / assembled need act_format='f32' (the fused assemblies write fp32 x0)")
-            k_shared = c.k0_pad if self.shared_x0 else 0
-            N.check(c.lib.amx_assemble_input_limbs(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(),
-                                                   0 if k_shared else Bp * c.ldk, c.ldk, B, rexp.data_ptr(),
-                                                   self.n_slots * Bp, s), "amx_assemble_input_limbs")
-            self._mlp(buf, preds, Bp, s, rexp, row_exponents=False, k_shared=k_shared)
-            return preds
         if x0_ready:
             if self.W2 is None:
                 raise ValueError("x0_ready needs the f16x3 GEMM (shared x0 slice + row exponents)")
@@ -330,28 +308,9 @@ class DeviceEnsemble:
         self._mlp(buf, preds, Bp, s, rexp, row_exponents=assembled, k_shared=k_shared)
         return preds
 
-    def fused_rows(self, Bp: int) -> int:
-        """Rows per workgroup of the one-launch forward at Bp padded lanes (0: per-layer launches)."""
-        r = self._fw_rows.get(Bp)
-        if r is None:
-            c = self.ctx
-            ok = (self._fw_ptrs is not None and c.Hp == 512 and 1 <= c.L <= 8 and c.k0_pad % 64 == 0
-                  and c.n_out_pad in (128, 256))
-            r = int(c.lib.amx_forward_h3_rows(c.h, c.M, Bp)) if ok else 0
-            self._fw_rows[Bp] = r
-        return r
-
     def _mlp_h3(self, buf, preds, Bp, s, rexp, k_shared=0):
         c = self.ctx
         sA, sR, L = Bp * c.ldk, (c.L + 1) * Bp, c.L
-        if self.forward_mode == "fused" and self._fw_ptrs is None:
-            raise N.AmxNativeError("forward_mode='fused' is an experimental A/B path: rebuild the library with "
-                                   "AMX_EXPERIMENTAL=1 python -m amp_extensions_amd._build")
-        if self.forward_mode == "fused" and self.fused_rows(Bp):
-            N.check(c.lib.amx_forward_h3(c.h, c.M, Bp, c.k0_pad, c.Hp, L, buf.data_ptr(), c.ldk, sA, *self._fw_ptrs,
-                                         c.n_out_pad, preds.data_ptr(), c.S, Bp * c.S, rexp.data_ptr(), sR, k_shared,
-                                         s), "amx_forward_h3")
-            return
         for i in range(L):
             K = c.k0_pad + i * c.Hp
             N.check(c.lib.amx_gemm_bias_act_h3(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),
@@ -364,24 +323,6 @@ class DeviceEnsemble:
                                              Bp * c.S, rexp.data_ptr(), sR, L + 1, k_shared, s),
                 "amx_gemm_out_unnorm_h3")
 
-    def _mlp_lb(self, buf, preds, Bp, s, rexp, k_shared=0):
-        """The limb-format forward: L hidden layers (each writes its slice's limbs and chunk
-        exponents) and the output layer, amx_gemm_*_lb."""
-        c = self.ctx
-        sA, sR, L, per = Bp * c.ldk, self.n_slots * Bp, c.L, c.Hp // 128
-        for i in range(L):
-            K = c.k0_pad + i * c.Hp
-            N.check(c.lib.amx_gemm_bias_act_lb(c.h, c.M, Bp, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),
-                                               c.Hp * 2 * K, self.wexp[i].data_ptr(), c.Hp, self.b[i].data_ptr(), c.Hp,
-                                               buf.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, rexp.data_ptr(), sR, Bp,
-                                               rexp[0, 1 + i * per].data_ptr(), c.k0_pad, k_shared, s),
-                    "amx_gemm_bias_act_lb")
-        N.check(c.lib.amx_gemm_out_unnorm_lb(c.h, c.M, Bp, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
-                                             self.W2[L].data_ptr(), c.n_out_pad * 2 * c.ldk, self.wexp[L].data_ptr(),
-                                             c.n_out_pad, self.b[L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
-                                             Bp * c.S, rexp.data_ptr(), sR, Bp, c.k0_pad, k_shared, s),
-                "amx_gemm_out_unnorm_lb")
-
     def _mlp(self, buf, preds, Bp, s, rexp, row_exponents=True, k_shared=0):
         c = self.ctx
         sA = Bp * c.ldk
@@ -393,7 +334,7 @@ class DeviceEnsemble:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
         if self.W2 is not None:
-            (self._mlp_lb if self.limbs else self._mlp_h3)(buf, preds, Bp, s, rexp, k_shared)
+            self._mlp_h3(buf, preds, Bp, s, rexp, k_shared)
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1, Bp))

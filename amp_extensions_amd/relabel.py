@@ -11,7 +11,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .costs import GAILCost, RBFLinearCost, cost_input
+from .costs import GAILCost, RBFLinearCost, cost_input, device_discrepancy
 from .dist import feature_mean
 
 
@@ -61,7 +61,7 @@ def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", all
             phi = phi_fit
         else:
             phi = reward_func.get_rep(cost_input(reward_func.input_type, obs, act, nxt, reward_func.motion))
-        disc = ensemble.get_action_discrepancy(obs, act)
+        disc = device_discrepancy(ensemble, obs, act)
         reward, ipm, wb = reward_func._values(phi, disc, ensemble.threshold)
         bonus_v, ipm_v = wb.cpu().numpy(), ipm.cpu().numpy()
     elif isinstance(reward_func, GAILCost):

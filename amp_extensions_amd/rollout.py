@@ -232,7 +232,7 @@ class RolloutEngine:
         """amx_step_reset_act applies: policy-driven steps, the fused table reset, the f16x3 GEMM's
         shared x0 slice (the kernel writes x0 once, into model 0's rows), S <= 256."""
         return (self.fuse_step_act and self.policy is not None and self.auto_reset and self.motion is None
-                and self.fuse_reset and self.ens.W2 is not None and not self.ens.limbs and self.ens.shared_x0
+                and self.fuse_reset and self.ens.W2 is not None and self.ens.shared_x0
                 and self.ctx.S <= 256
                 and self.t + 1 < self.K)
 
@@ -267,7 +267,7 @@ class RolloutEngine:
                 self._graph_ahead = False
             # f16x3 with the shared x0 slice: the policy launch also writes x0 (once, model 0's
             # rows) and its row exponents, as amx_assemble_input_rexp (one launch fewer per step)
-            fuse_x0 = self.fuse_assembly and self.ens.W2 is not None and not self.ens.limbs and self.ens.shared_x0
+            fuse_x0 = self.fuse_assembly and self.ens.W2 is not None and self.ens.shared_x0
             ws = self.ens.workspace(B) if fuse_x0 else None
             self.policy.act(ob, B, act, t if self._capturing else self.step_counter, noise=noise,
                             eval_mode=self.eval_mode, mean_out=None if self.means is None else self.means[t],

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from .engine import AmxContext
+from .ensemble import as_device_ensemble
 from .humanoid import BODY_DEFS, FALL_BODIES, HORIZON, TerminationConfig
 from .rollout import RolloutEngine
 
@@ -166,7 +167,7 @@ class SimEnv(_EnvBase):
         device, check_reset_args; a reset-state table with noise raises NotImplementedError)."""
         self.reset_args = check_reset_args(reset_args)
         self.dynamic_ensemble = dynamic_ensemble
-        dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
+        dev_ens = as_device_ensemble(dynamic_ensemble)
         self.device = device
         self.enable_velocity_check = enable_velocity_check
         self.horizon = horizon
@@ -274,7 +275,7 @@ class BatchedSimEnv:
         SimEnv's (custom_time / time_max bound the lanes' Philox reset times, or the table rows
         drawn; the noise options perturb every motion reset, check_reset_args)."""
         self.reset_args = check_reset_args(reset_args)
-        dev_ens = getattr(dynamic_ensemble, "device", dynamic_ensemble)
+        dev_ens = as_device_ensemble(dynamic_ensemble)
         self.term = termination_from_args(deepmimic_args, horizon, enable_velocity_check)
         if reset_table is None:
             if not deepmimic_args:

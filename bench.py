@@ -80,16 +80,6 @@ def parse():
     p.add_argument("--gemm", choices=["f16x3", "bf16x6", "f32"], default="f16x3",
                    help="ensemble GEMM: scaled 2-limb fp16 split (3 products) or 3-limb bf16 split (6 products) on "
                         "the 16-bit MFMA pipe (both fp32-level error), or f32 MFMA")
-    p.add_argument("--act-format", choices=["f32", "limbs"], default="f32",
-                   help="f16x3 activation rows: f32 (split by every consumer, amx_gemm_*_h3; default) or limbs "
-                        "(split once by the producer, amx_gemm_*_lb; measured slower, DESIGN §6 round 4; needs a "
-                        "library built with AMX_EXPERIMENTAL=1)")
-    p.add_argument("--forward", choices=["fused", "layers"], default="layers",
-                   help="f16x3 forward: one launch per layer (default), or the whole forward in one launch "
-                        "(amx_forward_h3) at the lane counts whose row blocks fill the CUs in one round (A/B, "
-                        "measured equal at the N = 8 share; needs a library built with AMX_EXPERIMENTAL=1)")
-    p.add_argument("--lb-stage", type=int, choices=[0, 1], default=0,
-                   help="limb forward's K-loop staging: 0 registers, 1 LDS-DMA (A/B; AMX_EXPERIMENTAL=1 build)")
     p.add_argument("--expert-rows", type=int, default=50000)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-workers", type=int, default=0)
@@ -423,10 +413,7 @@ def main():
     from amp_extensions_amd.ensemble import init_ensemble_weights
     ens_w = init_ensemble_weights(S, A, hidden, M, base_seed=100)
     ctx = amx.AmxContext(S, A, n_models=M, hidden=512, n_hidden=4, feat_dim=512, device=dev)
-    ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm, act_format=args.act_format)
-    ens.forward_mode = args.forward
-    if args.lb_stage:
-        ctx.lib.amx_set_lb_stage(ctx.h, args.lb_stage)
+    ens = amx.DeviceEnsemble(ctx, ens_w, norms, gemm=args.gemm)
     thr = ens.compute_threshold(st.to(dev), at.to(dev))
     reset_source = syn.reset_table(65536, S, 1)
     if args.cost == "amp":
@@ -601,8 +588,7 @@ def main():
         ctx.gemm_timer(False)
     shard_note = (f"; expert cost over {args.expert_rows}/{world} expert rows per rank, its fp64 sum all-reduced "
                   f"off the critical path" if shard else "")
-    fused = ens.forward_mode == "fused" and ens.W2 is not None and not ens.limbs and ens.fused_rows((B + 127) // 128 * 128) > 0
-    per_fwd = 1 if fused else ctx.L + 1  # GEMM launches per forward
+    per_fwd = ctx.L + 1  # GEMM launches per forward
     launches = n_fwd * per_fwd
     flops_per_fwd = ens.mlp_flops_per_sample() * B
     if args.mode == "paths":

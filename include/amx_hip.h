@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define AMX_ABI_VERSION 1
+#define AMX_ABI_VERSION 2
 #define AMX_ROW_TILE 128
 #define AMX_K_TILE 32
 #define AMX_MAX_MODELS 8
@@ -468,8 +468,7 @@ int amx_set_gemm_timer(amx_ctx* ctx, uint64_t* buf);
  * each tile's 1-3 K segments stored raw and summed in K order by the last arriver
  * (deterministic); the hidden layers' 128 x 256 tiles split the same way below 2048 lanes.
  * amx_split_workspace_floats: floats of scratch (up to 6 partial tiles per tile, the largest
- * of the shapes above and amx_set_out_tile 4's)
- * and *n_counters uint32 counters a forward of `rows` padded lanes needs, 0 when that shape
+ * of the shapes above) and *n_counters uint32 counters a forward of `rows` padded lanes needs, 0 when that shape
  * does not use it.  amx_set_split_workspace registers caller-owned device memory with the
  * context (counters zeroed by the caller once; each launch leaves them zero); without it the
  * layer runs on row-block tiles.  One launch at a time per context. */
@@ -477,19 +476,6 @@ long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, i
 
 int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long floats, uint32_t* counters,
                             int n_counters);
-
-/* Output-layer tile of the f16x3 forward (amx_gemm_out_unnorm_h3), for A/B measurement:
- * 0 = default = 1, the register-staged 128 x 224 / row-block / 128 x 256 tiles; 2 = the
- * LDS-DMA ring tile (both operands by global_load_lds into a 3-slot ring, two K-tiles ahead)
- * with 8 waves of 16 x 16*ceil(S/16) (S in 193..240), 3 = the ring tile with 8 waves of
- * 32 x 112 (S in 193..224); other S fall back to 1.  Identical bits: the ring issues the same
- * limb products per 16 x 16 block in the same K order over the same stream-K segments.
- * 4 = 256 x 224 tiles, stream-K over the CUs at every lane count whose 256-row tiles are fewer
- * than the CUs (S in 129..224, needs the split workspace, which amx_split_workspace_floats also
- * sizes for it): different K segments, so equal to 1 to fp32 rounding, not bit for bit.
- * Tiles 2-4 are measured slower and exist only in an AMX_EXPERIMENTAL=1 build
- * (amx_hip_experimental.h); the default library accepts 0 and 1 and refuses 2-4. */
-int amx_set_out_tile(amx_ctx* ctx, int tile);
 
 /* Floats to allocate for the packed policy weight image for hidden widths H1, H2 (host query;
  * -1 on a bad argument): the image rounded up to whole 1-KiB pieces, which

@@ -104,6 +104,20 @@ def ensemble_preds(ens_weights, norms, state: torch.Tensor, action: torch.Tensor
         return torch.stack([dynamics_forward(w, norms, state, action) for w in ens_weights], dim=0)
 
 
+def load_ensemble_weights(path) -> list:
+    """DynamicsEnsemble.load_ensemble (dynamics.py:118-126) reduced to what the forward needs:
+    the list of {'model', 'optim'} dicts save_ensemble writes (dynamics.py:110-116), each
+    member's BasicMLP state dict ('fc_layers.{i}.weight/bias') as [(W, b), ...].  Read with the
+    weights-only unpickler."""
+    sds = torch.load(path, map_location="cpu", weights_only=True)
+    out = []
+    for sd in sds:
+        m = sd["model"]
+        n = 1 + max(int(k.split(".")[1]) for k in m if k.startswith("fc_layers."))
+        out.append([(m[f"fc_layers.{i}.weight"], m[f"fc_layers.{i}.bias"]) for i in range(n)])
+    return out
+
+
 def compute_threshold(ens_weights, norms, states: torch.Tensor, actions: torch.Tensor, batch_size: int = 256) -> float:
     """compute_threshold (dynamics.py:145-152): max discrepancy over the offline set.
     The reference iterates a shuffled DataLoader; the max is order-independent."""

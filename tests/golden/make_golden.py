@@ -12,7 +12,8 @@ Stubs are installed ONLY for imports the path does not use or that are absent he
   DeepMimicEnv/ArgParser (imported by sim_env.py:2,8; SimEnv is built with object.__new__ and
   reset() is served by a stub core that returns reset-table row floor(t)).
 
-Usage:  python tests/golden/make_golden.py        (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py            (writes tests/golden/*.npz, *.pt)
+        python tests/golden/make_golden.py --only g13  (one fixture set)
 """
 from __future__ import annotations
 
@@ -153,12 +154,16 @@ def make_simenv(SimEnv, ensemble, table, horizon=300, seed=1):
     return env
 
 
-def main():
+def main(argv=()):
     if not os.path.isdir(os.path.join(REF, "milo")):
         print(f"[make_golden] {REF} not present: nothing to do")
         return 0
     install_stubs()
     torch.set_num_threads(1)
+    if len(argv) == 2 and argv[0] == "--only":
+        globals()[f"make_{argv[1]}"]()
+        print("[make_golden] wrote", argv[1], "to", OUT)
+        return 0
     from milo.datasets import AmpDataset
     from milo.dynamics import DynamicsEnsemble
     from milo.linear_cost import RBFLinearCost
@@ -288,6 +293,7 @@ def main():
     make_g10()
     make_g11()
     make_g12()
+    make_g13()
     print("[make_golden] wrote fixtures to", OUT)
     return 0
 
@@ -473,5 +479,53 @@ def make_g12():
                         record_all_world=bool(ctrl.get("RecordAllWorld", False)))
 
 
+G13_HIDDEN = [32, 32]
+# run.py's dynamics optimizer defaults (milo/milo/arguments.py:56-59: --dynamic_optim adam,
+# --dynamic_lr 1e-3, --dynamic_eps 1e-8)
+G13_OPTIM = {"optim": "adam", "lr": 1e-3, "eps": 1e-8}
+
+
+def make_g13():
+    """G13: the ensemble checkpoint run.py loads (run.py:63-78, 105, 108).  A reference
+    DynamicsEnsemble (S/A 226/28, dense [32, 32] -- run.py's default depth -- Adam at run.py's
+    defaults, base_seed 100) takes one optimizer step per member on the G7 offline set (so the
+    weights are no longer the seed's and 'optim' holds Adam state), is written by the
+    reference's own save_ensemble (a list of {'model', 'optim'}, dynamics.py:110-116) to
+    g13_ensemble.pt, then loaded back into a fresh reference ensemble exactly as run.py:72-78
+    does, followed by compute_threshold() (run.py:108).  Recorded: the threshold, every
+    member's forward (un-normalised and normalised) and the disagreement on seeded query rows."""
+    from milo.datasets import AmpDataset
+    from milo.dynamics import DynamicsEnsemble
+
+    s, a, s2 = synthetic_offline(2048, seed=0)
+    ds = AmpDataset(torch.from_numpy(s).float(), torch.from_numpy(a).float(), torch.from_numpy(s2).float())
+    kw = dict(num_models=4, batch_size=256, hidden_sizes=G13_HIDDEN, transform=True, dense_connect=True,
+              optim_args=G13_OPTIM, base_seed=100, device=torch.device("cpu"))
+    ens = DynamicsEnsemble(S, A, ds, None, **kw)
+    for m in ens.models:  # as DynamicsModel.train sets them (dynamics.py:311-313)
+        m.state_mean, m.state_scale, m.action_mean, m.action_scale, m.diff_mean, m.diff_scale = ens.transformations
+    rs = np.random.RandomState(13)
+    idx = rs.permutation(2048)[:256]
+    for m in ens.models:
+        m.train_step(0, ds.states[idx], ds.actions[idx], ds.next_states[idx])
+    path = os.path.join(OUT, "g13_ensemble.pt")
+    ens.save_ensemble(path)
+    # run.py:72-78 + 108 as written
+    loaded = DynamicsEnsemble(S, A, ds, None, **kw)
+    loaded.load_ensemble(path)
+    loaded.compute_threshold()
+    qs = torch.from_numpy(rs.randn(48, S) * 0.5).float()
+    qs[:, 0] = torch.from_numpy(rs.uniform(0.8, 0.95, 48)).float()
+    qa = torch.from_numpy(rs.randn(48, A)).float()
+    with torch.no_grad():
+        preds = torch.stack([m.forward(qs, qa) for m in loaded.models]).numpy()
+        preds_norm = torch.stack([m.forward(qs, qa, unnormalize_out=False) for m in loaded.models]).numpy()
+    disc = loaded.get_action_discrepancy(qs, qa).numpy()
+    np.savez_compressed(os.path.join(OUT, "g13_ensemble_ckpt.npz"), hidden=np.array(G13_HIDDEN), base_seed=100,
+                        offline_seed=0, n_offline=2048, optim="adam", lr=1e-3, eps=1e-8, query_s=qs.numpy(),
+                        query_a=qa.numpy(), preds=preds, preds_norm=preds_norm, disc=disc,
+                        threshold=np.float64(loaded.threshold))
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(main(sys.argv[1:]))

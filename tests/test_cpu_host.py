@@ -25,13 +25,8 @@ def test_library_exports_every_header_symbol(lib):
     raw = ctypes.CDLL(_build.LIB_PATH)
     for s in syms:
         assert hasattr(raw, s), s
-    # the Python binding declares exactly the header's functions, plus the experimental
-    # header's (bound only when the library was built with AMX_EXPERIMENTAL=1)
-    exp = _native.header_symbols(os.path.join(_build.INCLUDE, "amx_hip_experimental.h"))
-    assert sorted(exp) == sorted(_native.EXPERIMENTAL) and not set(exp) & set(syms)
-    assert sorted(_native.SIGNATURES) == sorted(syms + exp)
-    # the shipped library is the default build: the experimental entry points are not exported
-    assert not any(hasattr(raw, s) for s in exp) or _build.EXPERIMENTAL
+    # the Python binding declares exactly the header's functions
+    assert sorted(_native.SIGNATURES) == sorted(syms)
 
 
 def test_library_is_gfx950_code_object():
@@ -40,7 +35,7 @@ def test_library_is_gfx950_code_object():
 
 
 def test_abi_version_and_errors(lib):
-    assert lib.amx_abi_version() == 1
+    assert lib.amx_abi_version() == _native.ABI_VERSION == 2
     # bad dims are refused without touching the GPU
     assert not lib.amx_create(0, 226, 28, 9, 512, 4, 512)   # > AMX_MAX_MODELS
     assert b"bad dims" in lib.amx_last_error()
@@ -307,3 +302,28 @@ def test_host_policy_noise_many_lanes(lib):
             for k in range(K):
                 rss[lane].uniform()
                 rss[lane].randn(A)
+
+
+def test_reference_checkpoint_loads_into_host_members(golden, golden_path):
+    """G13's ensemble.pt (written by the reference's save_ensemble, dynamics.py:110-116) loads
+    with the weights-only unpickler into the drop-in members' host containers (the reference's
+    state-dict keys) and into run.py's default optimizer (Adam) with its state; the seeded init
+    of the containers draws what DynamicsModel.__init__ draws (oracle restatement)."""
+    from oracle import milo_ref as R
+    from amp_extensions_amd.ensemble import BasicMLPWeights, _make_optimizer, init_model_weights
+    g = golden("g13_ensemble_ckpt.npz")
+    hidden = [int(x) for x in g["hidden"]]
+    S, A = 226, 28
+    sds = torch.load(golden_path("g13_ensemble.pt"), map_location="cpu", weights_only=True)
+    assert isinstance(sds, list) and len(sds) == 4 and all(set(d) == {"model", "optim"} for d in sds)
+    for k, d in enumerate(sds):
+        m = BasicMLPWeights(S + A, S, hidden)
+        m.load_state_dict(d["model"])
+        opt = _make_optimizer(m.parameters(), {"optim": str(g["optim"]), "lr": float(g["lr"]), "eps": float(g["eps"])})
+        opt.load_state_dict(d["optim"])
+        st = opt.state_dict()["state"]
+        assert len(st) == 2 * (len(hidden) + 1) and all("exp_avg" in v for v in st.values())
+        for (W, b), (W2, b2) in zip(m.layers(), weights_from_state_dict(d["model"])):
+            assert torch.equal(W, W2) and torch.equal(b, b2)
+        for (W, b), (Wr, br) in zip(init_model_weights(S, A, hidden, 100 + k), R.init_model_weights(S, A, hidden, 100 + k)):
+            assert torch.equal(W, Wr) and torch.equal(b, br)

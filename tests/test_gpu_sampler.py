@@ -35,7 +35,7 @@ def setup():
     ens = DynamicsEnsemble.random_init(S, A, norms, hidden_sizes=(64, 64, 64, 64), num_models=4, base_seed=100)
     ens_w = R.init_ensemble_weights(S, A, [64] * 4, 4, 100)
     pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100, init_log_std=-0.25)
-    pol = amx.DevicePolicy(ens.device.ctx, pw, log_std)
+    pol = amx.DevicePolicy(ens.ctx, pw, log_std)
     return amx, ens, ens_w, norms, pw, log_std, pol
 
 
@@ -257,7 +257,7 @@ def test_sample_points_takes_mjrl_policy(setup):
     b = amx.sample_points(env, mj, num_to_collect=200, base_seed=9, num_workers=2)
     assert mj.__dict__["_amx_device_policy"][1] is dp  # re-synced in place, not rebuilt
     layers = [(l.weight.data, l.bias.data) for l in mj.model.fc_layers]
-    fresh = amx.DevicePolicy(ens.device.ctx, layers, mj.log_std.data)
+    fresh = amx.DevicePolicy(ens.ctx, layers, mj.log_std.data)
     a = amx.sample_points(env, fresh, num_to_collect=200, base_seed=9, num_workers=2)
     assert len(a) == len(b)
     for pa, pb in zip(a, b):
@@ -294,7 +294,7 @@ def test_sample_points_sees_in_place_mjrl_updates(setup, update):
     # the mean from the updated model, the noise from log_std_val as mjrl's get_action (its
     # float64 copy is refreshed by set_param_values only, gaussian_mlp.py:53, 91, 102)
     layers = [(l.weight.data, l.bias.data) for l in mj.model.fc_layers]
-    fresh = amx.DevicePolicy(ens.device.ctx, layers, torch.from_numpy(mj.log_std_val))
+    fresh = amx.DevicePolicy(ens.ctx, layers, torch.from_numpy(mj.log_std_val))
     a = amx.sample_points(env, fresh, num_to_collect=200, base_seed=9, num_workers=2)
     assert len(a) == len(b)
     for pa, pb in zip(a, b):

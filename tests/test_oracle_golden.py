@@ -66,6 +66,27 @@ def test_ensemble_forward_disc_threshold(golden, norms, tag):
     close(thr, float(g["threshold"]))
 
 
+def test_ensemble_checkpoint(golden, golden_path, norms):
+    """G13: the reference's save_ensemble file (run.py's ensemble.pt) read back by the oracle's
+    load_ensemble_weights reproduces the reference's run.py:72-78 + 108 outputs."""
+    g = golden("g13_ensemble_ckpt.npz")
+    ens = R.load_ensemble_weights(golden_path("g13_ensemble.pt"))
+    hidden = [int(x) for x in g["hidden"]]
+    assert len(ens) == 4 and [W.shape[0] for W, _ in ens[0][:-1]] == hidden
+    # one Adam step moved every member off its seeded init
+    init = R.init_ensemble_weights(S, A, hidden, 4, int(g["base_seed"]))
+    assert all(not torch.equal(w[0][0], i[0][0]) for w, i in zip(ens, init))
+    qs, qa = torch.from_numpy(g["query_s"]), torch.from_numpy(g["query_a"])
+    close(R.ensemble_preds(ens, norms, qs, qa).numpy(), g["preds"])
+    with torch.no_grad():
+        pn = torch.stack([R.dynamics_forward(w, norms, qs, qa, unnormalize_out=False) for w in ens])
+    close(pn.numpy(), g["preds_norm"])
+    close(R.compute_discrepancy(ens, norms, qs, qa).numpy(), g["disc"])
+    s, a, _ = synthetic_offline(2048, 0)
+    close(R.compute_threshold(ens, norms, torch.from_numpy(s).float(), torch.from_numpy(a).float()),
+          float(g["threshold"]))
+
+
 def test_simenv_trace(golden, norms):
     g = golden("g2_simenv_trace.npz")
     ens = R.init_ensemble_weights(S, A, [64] * 4, 4, 100)

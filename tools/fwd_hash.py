@@ -1,6 +1,6 @@
 """Hash of the f16x3 ensemble forward (every lane-count regime: 256x256, row-block, stream-K
 and small-tile shapes) and of an RFF pass, for bit-identity checks between library builds
-(tools/lib_ab.sh).  usage: python tools/fwd_hash.py"""
+(tools/so_ab.sh).  usage: python tools/fwd_hash.py"""
 import hashlib
 import sys
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build amp_extensions_amd/libamx_hip_<tag>.so with one csrc source compiled with extra defines,
-# linked with the in-tree objects of the others (A/B experiments; tools/ab_bench.sh, tools/lib_ab.sh).
+# linked with the in-tree objects of the others (A/B experiments; tools/so_ab.sh).
 # usage: tools/src_variant.sh <source.hip> <tag> -DNAME=VALUE ...
 set -e
 src=$1; tag=$2; shift 2
