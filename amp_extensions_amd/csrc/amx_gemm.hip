@@ -92,6 +92,11 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef H3_EXP
 #define H3_EXP 0
 #endif
+// H3_ORDERED_LOADS (A/B builds: 0 = the scheduler's order): the f16x3 K loop's prologue issues
+// its staging loads in the loop's piece order (h3_tile's `load`)
+#ifndef H3_ORDERED_LOADS
+#define H3_ORDERED_LOADS 1
+#endif
 // OUT80 (A/B builds): 1 = the 80 x 224 output tile where it makes exactly one tile per CU
 #ifndef OUT80
 #define OUT80 1
@@ -959,9 +964,23 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     for (int j = 0; j < VW; ++j)
       if (w_ok[j]) rw[j] = gW(j, kt);
   };
+  // the prologue's loads in the K loop's piece order (A chunks, then W chunks; each pinned by a
+  // sched_barrier).  The compiler's waits at the loop head merge the prologue's pending-load
+  // order with the back edge's: left to the scheduler, the prologue issued them in reverse (A
+  // chunk 0 youngest), and the first publish of EVERY K-tile then waited vmcnt(0) -- for all
+  // of the previous tile's loads, the W chunks issued just before the barrier included.
   auto load = [&](int kt) {
-    load_a(std::integral_constant<int, 0>{}, kt);
-    load_w(kt);
+    kt = kt < nk ? kt : nk - 1;
+#pragma unroll
+    for (int j = 0; j < VA; ++j) {
+      if (a_ok[j]) ra[0][j] = gA(j, kt);
+      if constexpr (H3_ORDERED_LOADS) __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < VW; ++j) {
+      if (w_ok[j]) rw[j] = gW(j, kt);
+      if constexpr (H3_ORDERED_LOADS) __builtin_amdgcn_sched_barrier(0);
+    }
   };
   auto publish = [&](int base) {  // A from set 0
 #pragma unroll

@@ -173,7 +173,7 @@ class DeviceEnsemble:
         self.W = self.b = self.W3 = self.W2 = self.wexp = None
         self.set_weights(weights)
         ctx.set_normalizers(norms)
-        self.norms = tuple(torch.as_tensor(x).float().to(dev) for x in norms)
+        self.norms = tuple(torch.as_tensor(x).float().to(ctx.device) for x in norms)
         self.threshold = float(threshold)
         self._ws = {}
         # optional timing hook: when a list, every forward appends a (start, end) pair of
