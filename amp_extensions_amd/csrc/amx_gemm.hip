@@ -97,6 +97,18 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef H3_ORDERED_LOADS
 #define H3_ORDERED_LOADS 1
 #endif
+// H3_AFFINE (A/B builds: 0 = per-chunk offset registers): the 16x16x32 tiles' staging chunks j
+// sit NT / CPR rows apart, so a chunk's global offset is chunk 0's plus a wave-uniform step
+// (the buffer load's SGPR offset) and its LDS offset chunk 0's plus an immediate -- one
+// address register per operand instead of one per chunk
+#ifndef H3_AFFINE
+#define H3_AFFINE 1
+#endif
+// H3_W4 (A/B builds): the hidden layers' 256 x 256 tile on 4 waves of 128 x 128 (one wave per
+// SIMD, 256 accumulator registers each) instead of 8 waves of 128 x 64
+#ifndef H3_W4
+#define H3_W4 0
+#endif
 // OUT80 (A/B builds): 1 = the 80 x 224 output tile where it makes exactly one tile per CU
 #ifndef OUT80
 #define OUT80 1
@@ -925,13 +937,24 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Ag), 0, 0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsA0 = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Ag0), 0, 0x7ffffff0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsW = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(Wg), 0, 0x7ffffff0, 0x00020000);
+  // AFF: chunk j = chunk 0 + j * RSTEP rows (the plain map of the 16x16x32 tiles)
+  constexpr bool AFF = H3_AFFINE && TL::M16 && !TL::AMAP && TL::NA % NT == 0 && TL::NW % NT == 0;
+  constexpr int RSTEP = NT / CPR;
   auto gA = [&](int j, int kt) -> f32x4 {
+    if constexpr (AFF)
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           kt < nks ? rsA0 : rsA, a_src[0] * 4, (kt * BK + j * RSTEP * a.lda) * 4, 0));
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(kt < nks ? rsA0 : rsA, a_src[j] * 4,
                                                                           kt * BK * 4, 0));
   };
   auto gW = [&](int j, int kt) -> u32x4 {
+    if constexpr (AFF)
+      return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rsW, w_off_b[0], kt * 2 * BK * 2 + (int)(j * RSTEP * ldw2 * 2), 0));
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, w_off_b[j], kt * 2 * BK * 2, 0));
   };
+  auto adst = [&](int j) { return AFF ? a_dst[0] + j * RSTEP * LD : a_dst[j]; };
+  auto wdst = [&](int j) { return AFF ? w_dst[0] + j * RSTEP * LD : w_dst[j]; };
   f32x4 ra[TL::DEEPA ? 2 : 1][VA];  // A stage registers (DEEPA: the sets of tiles t+1 and t+2)
   u32x4 rw[VW];
   constexpr int MB = TL::MB, NB = TL::NB;  // 16x16 blocks of the M16 form
@@ -969,16 +992,21 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
   // order with the back edge's: left to the scheduler, the prologue issued them in reverse (A
   // chunk 0 youngest), and the first publish of EVERY K-tile then waited vmcnt(0) -- for all
   // of the previous tile's loads, the W chunks issued just before the barrier included.
+  // staging piece q: an A chunk or a W chunk (SPREAD with VA == VW alternates them, so every
+  // m-block carries one A split; otherwise the A chunks first)
+  constexpr bool ALT = TL::SPREAD && VA == VW;
+  auto piece_a = [](int q) { return ALT ? (q & 1) == 0 : q < VA; };
+  auto piece_j = [](int q) { return ALT ? q >> 1 : (q < VA ? q : q - VA); };
   auto load = [&](int kt) {
     kt = kt < nk ? kt : nk - 1;
 #pragma unroll
-    for (int j = 0; j < VA; ++j) {
-      if (a_ok[j]) ra[0][j] = gA(j, kt);
-      if constexpr (H3_ORDERED_LOADS) __builtin_amdgcn_sched_barrier(0);
-    }
-#pragma unroll
-    for (int j = 0; j < VW; ++j) {
-      if (w_ok[j]) rw[j] = gW(j, kt);
+    for (int q = 0; q < VA + VW; ++q) {
+      const int j = piece_j(q);
+      if (piece_a(q)) {
+        if (a_ok[j]) ra[0][j] = gA(j, kt);
+      } else {
+        if (w_ok[j]) rw[j] = gW(j, kt);
+      }
       if constexpr (H3_ORDERED_LOADS) __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -996,12 +1024,12 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
         u32x2 l0, l1;
         split2(x, l0, l1);
 #endif
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+        *reinterpret_cast<u32x2*>(sm + base + adst(j)) = l0;
+        *reinterpret_cast<u32x2*>(sm + base + adst(j) + 16) = l1;
       }
 #pragma unroll
     for (int j = 0; j < VW; ++j)
-      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+      if (w_ok[j]) *reinterpret_cast<u32x4*>(sm + base + wdst(j)) = rw[j];
   };
   // one staging piece (SPLIT): publish A/W chunk j of the registered tile, then reload chunk j
   // of tile kt (clamped as load()); DEEPA: A chunk j of register set `set`, reloaded with tile
@@ -1010,8 +1038,9 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
     constexpr int SA = decltype(set)::value;
     const int kta = TL::DEEPA ? (kt + 1 < nk ? kt + 1 : nk - 1) : (kt < nk ? kt : nk - 1);
     kt = kt < nk ? kt : nk - 1;
-    if (q < VA) {
-      const int j = q;
+    if (q >= VA + VW) return;
+    if (piece_a(q)) {
+      const int j = piece_j(q);
       if (a_ok[j]) {
         f32x4 x = ra[SA][j];
 #if H3_EXP & 2
@@ -1023,16 +1052,16 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
         u32x2 l0, l1;
         split2(x, l0, l1);
 #endif
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j]) = l0;
-        *reinterpret_cast<u32x2*>(sm + base + a_dst[j] + 16) = l1;
+        *reinterpret_cast<u32x2*>(sm + base + adst(j)) = l0;
+        *reinterpret_cast<u32x2*>(sm + base + adst(j) + 16) = l1;
 #if !(H3_EXP & 1)
         ra[SA][j] = gA(j, kta);
 #endif
       }
-    } else if (q < VA + VW) {
-      const int j = q - VA;
+    } else {
+      const int j = piece_j(q);
       if (w_ok[j]) {
-        *reinterpret_cast<u32x4*>(sm + base + w_dst[j]) = rw[j];
+        *reinterpret_cast<u32x4*>(sm + base + wdst(j)) = rw[j];
 #if !(H3_EXP & 1)
         rw[j] = gW(j, kt);
 #endif
@@ -1074,15 +1103,40 @@ __device__ __forceinline__ void h3_tile(const GemmArgs& a, int tile, int kb, int
         for (int l = 0; l < 2; ++l)
           ga[(m + 1) & 1][l] = *reinterpret_cast<const f16x8*>(As + (m + 1) * 16 * LD + l * 16);
       }
-      if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (TL::PIN && !TL::SPREAD) __builtin_amdgcn_sched_barrier(0);
       constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};  // small terms first
 #pragma unroll
       for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int n = 0; n < NB; ++n)
           acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ga[m & 1][PA[p]], gb[n][PB[p]], acc[m][n], 0, 0, 0);
-      if constexpr (TL::PIN) __builtin_amdgcn_sched_barrier(0);
-      if constexpr (TL::SPLIT) {
+      if constexpr (TL::PIN && !TL::SPREAD) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (TL::SPREAD) {
+        // one wave per SIMD: no partner wave covers the staging work, so it is interleaved into
+        // the block's MFMA stream (sched_group_barrier: MFMA / DS read / VALU / DS write / VMEM)
+        constexpr int PPB = (VA + VW + MB - 1) / MB;
+#pragma unroll
+        for (int q = m * PPB; q < (m + 1) * PPB; ++q) piece(q, split_base, split_kt, set);
+        constexpr int NMF = 3 * NB;
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < PPB; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NMF - 14 - 2 * PPB, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (TL::SPLIT) {
         piece(m, split_base, split_kt, set);
         if (m == MB - 1) {
 #pragma unroll
@@ -1347,6 +1401,9 @@ __global__ __launch_bounds__(256) void k_row_exp(const float* __restrict__ A, in
 //   output layer S <= 224: 128x224, 14 waves of 64x32 on 16x16x32 (same schedule);
 //     S in (224, 256]: 128x256, 8 waves of 64x64
 using H256 = TileH3<2, 4, 4, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
+// 4 waves of 128 x 128, one per SIMD (H3_W4 A/B): 192 MFMAs and 32 fragment reads per wave and
+// K-tile, the 16 staging pieces two behind each m-block
+using H256w4 = TileH3<2, 2, 4, 4, 1, 2, true, true, true, 0, 0, true, true, true, false, true>;
 // row-block tiles for the strong-scaling lane counts (rows = 32 RB, 4 members: a 256-workgroup
 // grid for every RB): hidden RB x 256 (8 waves of RB/2 x 64), output RB x 112 / RB x 128
 // (RB/32 waves of 32 x 112 or 32 x 128), same schedule as H256
@@ -1722,7 +1779,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
   const hipStream_t s = (hipStream_t)stream;
   if (rows % 256 == 0 && N % 256 == 0 && K % 32 == 0 &&
       (long long)(rows / 256) * (N / 256) * groups >= resident_wgs(ctx, H256::LDS, H256::NT, 2))
-    return launch_h3<EPI_BIAS_ACT, H256>(a, s);
+    return H3_W4 ? launch_h3<EPI_BIAS_ACT, H256w4>(a, s) : launch_h3<EPI_BIAS_ACT, H256>(a, s);
   // one wave of row-block tiles: rows = RB * n_cus / (groups * N/256), RB in {128..224}
   if (N % 256 == 0 && K % 32 == 0) {
     const long long per = (long long)groups * (N / 256);

@@ -112,7 +112,7 @@ __device__ __forceinline__ int exp_of_bits(uint32_t absbits) {
 // distinct 4-bank slots)
 template <int WM_, int WN_, int TM_, int TN_, int OCC_ = 2, int NSUB_ = 1, bool LATE_ = false, bool AMAP_ = true,
           bool M16_ = false, int MB16_ = 0, int NB16_ = 0, bool PIN_ = false, bool EARLY_ = false,
-          bool SPLIT_ = false, bool DEEPA_ = false>
+          bool SPLIT_ = false, bool DEEPA_ = false, bool SPREAD_ = false>
 struct TileH3 {
   static constexpr bool EARLY = EARLY_ && M16_ && LATE_;  // first fragment reads before the publish
   // SPLIT: the publish of tile t+1 and the loads of t+2 are cut into one piece per m-block and
@@ -122,6 +122,9 @@ struct TileH3 {
   // register sets; the loop unrolled by two): the output layer's A panel is streamed from HBM
   // once (N = 224 columns per A row), so its K loop waits on load latency, not on the MFMAs
   static constexpr bool DEEPA = DEEPA_ && SPLIT;
+  // SPREAD (SPLIT): the staging pieces dealt evenly over the m-blocks (ceil(pieces / MB) behind
+  // each) instead of one per block with the rest behind the last
+  static constexpr bool SPREAD = SPREAD_ && SPLIT;
   // PIN: sched_barriers keep each block's fragment reads one MFMA group ahead of their use
   static constexpr bool PIN = PIN_;
   static constexpr int WM = WM_, WN = WN_, TM = TM_, TN = TN_, OCC = OCC_, NSUB = NSUB_, BK = 16 * NSUB_;

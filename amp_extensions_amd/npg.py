@@ -248,7 +248,7 @@ class DeviceNPG:
         obs, act, adv = self._inputs(observations, actions, advantages)
         c = self.ctx
         n = obs.shape[0]
-        if whiten:  # (adv - mean) / (std + 1e-6), population std, in one launch (amx_adv_whiten)
+        if whiten:  # (adv - mean) / (std + 1e-6), population std: amx_adv_whiten (per-block parts, then combine + apply)
             w = torch.empty_like(adv)
             stats = torch.empty(2, dtype=torch.float64, device=c.device)
             N.check(c.lib.amx_adv_whiten(c.h, 1, n, None, None, n, adv.data_ptr(), 1e-6, w.data_ptr(),

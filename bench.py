@@ -635,7 +635,11 @@ def main():
     else:
         step_flops = ens.mlp_flops_per_sample() + 2 * (cost.input_dim * 1024 + 1024 * 512 + 512)
     value = total_samples / elapsed
-    traffic, traffic_note = gemm_traffic(args.gemm, S, B)
+    if args.mode == "paths":
+        # the sampler's forwards run at its own (chunk-dependent) lane counts, which no PMC record covers
+        traffic, traffic_note = None, "paths mode: the sampler's forwards run at other lane counts than the PMC record's"
+    else:
+        traffic, traffic_note = gemm_traffic(args.gemm, S, B)
 
     gi = GEMM_INFO[args.gemm]
     peak = gi["peak"]

@@ -626,7 +626,10 @@ int amx_gae(amx_ctx* ctx, int T, int L, const int32_t* len, const int64_t* base,
 
 /* Advantage whitening of BatchREINFORCE.process_paths (mjrl/mjrl/algos/batch_reinforce.py:
  * 280-285): over the grid's rows, out = (adv - mean) / (std + eps) (population std);
- * stats[0..1] = mean, std (fp64, fixed reduction order).  out may alias adv. */
+ * stats[0..1] = mean, std (fp64, fixed reduction order).  out may alias adv.  Two launches over
+ * the chip (per-block count / sum / M2, then the combine in block order and the apply); the
+ * per-block partials live in the context (graph-capturable), so a context runs one whitening
+ * at a time: do not issue two on different streams, or a captured one beside an eager one. */
 int amx_adv_whiten(amx_ctx* ctx, int T, int L, const int32_t* len, const int64_t* base,
                    long long stride, const double* adv, double eps, double* out, double* stats,
                    void* stream);
