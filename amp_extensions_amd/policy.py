@@ -53,12 +53,18 @@ class DevicePolicy:
         # log_std_val = float64(log_std); noise scale = np.exp(log_std_val) (gaussian_mlp.py:53,102)
         ls = np.float64(torch.as_tensor(log_std).detach().cpu().numpy().ravel())
         self.log_std_val = ls
-        self.noise_scale = torch.from_numpy(np.exp(ls)).to(dev)
+        scale = torch.from_numpy(np.exp(ls)).to(dev)
         c = self.ctx
         n = int(c.lib.amx_policy_blob_floats(c.h, self.H1, self.H2))
         if n <= 0:
             raise ValueError("amx_policy_blob_floats failed")
-        self.blob = torch.zeros(n, dtype=torch.float32, device=dev)  # (the tail past the image: LDS-DMA padding)
+        # a re-sync of the same shapes rewrites the device buffers in place: HIP graphs captured
+        # around this policy (sample_points' chunk graphs) keep reading the current parameters
+        if getattr(self, "blob", None) is not None and self.blob.numel() == n and self.noise_scale.shape == scale.shape:
+            self.noise_scale.copy_(scale)
+        else:
+            self.noise_scale = scale
+            self.blob = torch.zeros(n, dtype=torch.float32, device=dev)  # (the tail past the image: LDS-DMA padding)
         N.check(c.lib.amx_policy_pack(c.h, self.W[0].data_ptr(), self.b[0].data_ptr(), self.H1, self.W[1].data_ptr(),
                                       self.b[1].data_ptr(), self.H2, self.W[2].data_ptr(), self.b[2].data_ptr(),
                                       self.blob.data_ptr(), c.stream), "amx_policy_pack")

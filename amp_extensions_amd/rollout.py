@@ -148,6 +148,10 @@ class RolloutEngine:
         if self._fbuf is not None:  # feature_sum()'s output is the message's first F slots
             self.phi_sum = self._fbuf[:cost.feature_dim]  # (the global sums once all-reduced)
         self.mb_mmd = None
+        # rollout(): score each step's cost rows on a side stream under the next step's policy
+        # (bit-identical; see rollout)
+        self.score_overlap = False
+        self._side = None
 
     # ------------------------------------------------------------------------------------
     def reset_all(self, rows: torch.Tensor | None = None) -> None:
@@ -374,15 +378,30 @@ class RolloutEngine:
         N.check(c.lib.amx_cost_rows(c.h, *args, B, self.cost_in[t].data_ptr(), self.kc, c.stream), "amx_cost_rows")
 
     def rollout(self, K: int | None = None) -> int:
-        """K synchronous steps (default: the buffer depth), then the batched reward pass.
-        Returns K*B transitions."""
+        """K synchronous steps (default: the buffer depth), then the reward pass.  With
+        `score_overlap` (K > 1) each step's cost rows are scored on a side stream right after
+        its step kernel, under the next step's latency-bound policy and assembly launches;
+        otherwise in one batched launch at the end.  Same rows, same per-row work and the same
+        32-row fp64 partials: the results are bit-identical either way.  Returns K*B transitions."""
         K = self.K if K is None else K
         self._rollout_begin()
         self._act_ready = -1
+        side = self._score_stream() if (self.score_overlap and K > 1 and self.cost is not None) else None
         for t in range(K):
             self.step(act_next=t + 1 < K)
+            if side is not None and t + 1 < K:
+                side.wait_stream(torch.cuda.current_stream(self.ctx.device))
+                with torch.cuda.stream(side):
+                    self.score()
+        if side is not None:
+            torch.cuda.current_stream(self.ctx.device).wait_stream(side)
         self.score()
         return K * self.B
+
+    def _score_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.ctx.device)
+        return self._side
 
     def score(self) -> None:
         """Features (MMD) or discriminator rewards (GAIL) of the steps recorded since the last

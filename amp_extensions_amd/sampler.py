@@ -259,6 +259,36 @@ class _ChunkGraph:
         self.eng._graph_ahead = True
 
 
+def _chunk_graph(eng: RolloutEngine, K: int, noise_dev, eval_mode: bool) -> _ChunkGraph:
+    """The chunk's captured graph, cached on the engine across sample_points calls: it bakes in
+    the engine's and the policy's device buffers (persistent; DevicePolicy.sync_from rewrites
+    them in place), the noise buffer, eval_mode and, for device-drawn noise, the policy seed."""
+    pol = eng.policy
+    key = (K, 0 if noise_dev is None else noise_dev.data_ptr(), bool(eval_mode), id(pol), pol.blob.data_ptr(),
+           pol.noise_scale.data_ptr(), pol.H1, pol.H2, pol.seed if noise_dev is None else 0)
+    cache = eng.__dict__.setdefault("_chunk_graphs", {})
+    g = cache.get(key)
+    if g is None:
+        if len(cache) >= 4:  # (re-created policies: keep the newest few)
+            cache.pop(next(iter(cache)))
+        eng.begin_rollout()
+        g = cache[key] = _ChunkGraph(eng, K, noise_dev)
+    else:
+        eng.begin_rollout()
+        if eng._graph_ahead:
+            eng.step_counter = int(eng.dev_step.item())
+    return g
+
+
+def _noise_buffer(eng: RolloutEngine, K: int, L: int, A: int) -> torch.Tensor:
+    """The [K, L, A] device buffer of the uploaded reference noise (persistent per engine: the
+    cached chunk graphs read it)."""
+    buf = eng.__dict__.get("_noise_dev")
+    if buf is None or tuple(buf.shape) != (K, L, A):
+        buf = eng.__dict__["_noise_dev"] = torch.zeros(K, L, A, dtype=torch.float64, device=eng.ctx.device)
+    return buf
+
+
 def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, rng: str, eval_mode: bool,
              time_max: float, speculate: bool = True, graph: bool = True):
     """Run the W workers' trajectory sequences on the engine's lanes (see the module notes).
@@ -287,7 +317,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     eng.eval_mode = eval_mode
     ref_noise = rng == "reference" and not eval_mode
     hn = _HostNoise(c.lib, L, K, A) if ref_noise else None
-    noise_dev = torch.zeros(K, L, A, dtype=torch.float64, device=dev) if ref_noise else None
+    noise_dev = _noise_buffer(eng, K, L, A) if ref_noise else None
     pin = torch.cuda.is_available()
     # per-chunk reset inputs: staged in pinned memory, uploaded without a host wait
     mask_h = torch.zeros(L, dtype=torch.uint8, pin_memory=pin)
@@ -386,9 +416,9 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
             buf = hn.bufs[hn.cur]
             hn.draw(new_lanes if pre_drawn else active, buf)  # (the continuing lanes' noise is drawn)
             noise_dev.copy_(buf, non_blocking=True)
-        if graph and chunk_graph is None and chunks >= 2:  # (the first chunk allocates the workspaces)
-            eng.begin_rollout()
-            chunk_graph = _ChunkGraph(eng, K, noise_dev)
+        # (the first chunk of a new shape allocates the workspaces: captured from the second on)
+        if graph and chunk_graph is None and (chunks >= 2 or "_chunk_graphs" in eng.__dict__):
+            chunk_graph = _chunk_graph(eng, K, noise_dev, eval_mode)
         if chunk_graph is not None:
             chunk_graph.replay()
         else:
@@ -481,7 +511,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
     eng.eval_mode = eval_mode
     ref_noise = rng == "reference" and not eval_mode
     hn = _HostNoise(c.lib, L, K, A) if ref_noise else None
-    noise_dev = torch.zeros(K, L, A, dtype=torch.float64, device=dev) if ref_noise else None
+    noise_dev = _noise_buffer(eng, K, L, A) if ref_noise else None
     pin = torch.cuda.is_available()
     # two sets of pinned staging: set i % 2 is rewritten only after chunk i - 2 has completed
     stage = []
@@ -615,9 +645,9 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
             buf = hn.bufs[si]
             hn.draw(active, buf)  # the next K draws of every lane in flight (finished ones idle)
             noise_dev.copy_(buf, non_blocking=True)
-        if graph and chunk_graph is None and chunks >= 2:  # (the first chunk allocates the workspaces)
-            eng.begin_rollout()
-            chunk_graph = _ChunkGraph(eng, K, noise_dev)
+        # (the first chunk of a new shape allocates the workspaces: captured from the second on)
+        if graph and chunk_graph is None and (chunks >= 2 or "_chunk_graphs" in eng.__dict__):
+            chunk_graph = _chunk_graph(eng, K, noise_dev, eval_mode)
         if chunk_graph is not None:
             chunk_graph.replay()
         else:

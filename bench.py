@@ -93,6 +93,9 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the whole rollout as captured HIP graph(s); auto = off: eager launches measured "
                         "faster at every per-rank share on ROCm 7 (profiles/r05z_graph_vs_eager.txt)")
+    p.add_argument("--score-overlap", choices=["on", "off"], default="on",
+                   help="score each step's cost rows on a side stream under the next step's policy "
+                        "(RolloutEngine.score_overlap; bit-identical to the batched pass at the rollout's end)")
     p.add_argument("--fuse-assembly", choices=["on", "off"], default="off",
                    help="f16x3: the policy launch also writes the ensemble's x0 slice (RolloutEngine.fuse_assembly)")
     p.add_argument("--overlap", choices=["on", "off"], default="off",
@@ -441,6 +444,7 @@ def main():
     eng = amx.RolloutEngine(ens, reset_source, lanes=B, policy=pol, cost=cost,
                             seed=(7 << 32) + rank, max_steps=T)
     eng.fuse_assembly = args.fuse_assembly == "on"
+    eng.score_overlap = args.score_overlap == "on"
     eng.reset_all()
     # steady-state phase: a long-running lane fleet has its trajectories at uniformly spread
     # positions, so horizon resets (1/300 per step) happen inside the timed region as they do

@@ -64,6 +64,29 @@ def test_fused_step_reset_matches_step_then_reset(cost_kind):
     assert (ref.reset_rows[done[:, :ref.B]] >= 0).all()
 
 
+@pytest.mark.parametrize("cost_kind", ["mmd", "gail"])
+def test_score_overlap_bit_identical(cost_kind):
+    """RolloutEngine.score_overlap (each step's cost rows scored on a side stream under the next
+    step's policy) against the batched pass at the rollout's end: every feature, fp64 partial,
+    disagreement, reward and relabel output bit-identical over rollouts with resets."""
+    engs = _engines(cost_kind, flag="score_overlap")
+    outs = []
+    for eng in engs:
+        eng.reset_all()
+        for _ in range(3):
+            eng.rollout()
+            outs.append(eng.relabel() if cost_kind == "mmd" else None)
+    torch.cuda.synchronize()
+    ref, got = engs
+    names = ["cost_in", "cost_rexp", "disc", "rewards"] + (["phi", "partials", "ipm", "wbonus", "_fbuf"]
+                                                          if cost_kind == "mmd" else [])
+    for n in names:
+        assert torch.equal(getattr(ref, n), getattr(got, n)), n
+    if cost_kind == "mmd":
+        assert [float(o["mb_mmd"]) for o in outs[:3]] == [float(o["mb_mmd"]) for o in outs[3:]]
+    assert got._side is not None and ref._side is None
+
+
 @pytest.mark.parametrize("hidden", [(32, 32), (64, 48)])
 def test_policy_fused_assembly_bit_identical(hidden):
     """k_policy writing the ensemble's x0 rows itself (fused assembly) gives the same actions and
