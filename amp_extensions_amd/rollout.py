@@ -379,14 +379,16 @@ class RolloutEngine:
 
     def rollout(self, K: int | None = None) -> int:
         """K synchronous steps (default: the buffer depth), then the reward pass.  With
-        `score_overlap` (K > 1) each step's cost rows are scored on a side stream right after
+        `score_overlap` (K > 1, MMD cost) each step's cost rows are scored on a side stream right after
         its step kernel, under the next step's latency-bound policy and assembly launches;
         otherwise in one batched launch at the end.  Same rows, same per-row work and the same
         32-row fp64 partials: the results are bit-identical either way.  Returns K*B transitions."""
         K = self.K if K is None else K
         self._rollout_begin()
         self._act_ready = -1
-        side = self._score_stream() if (self.score_overlap and K > 1 and self.cost is not None) else None
+        # (the MMD features only: the GAIL discriminator's GEMMs split K differently at one step's
+        # row count than over the whole rollout, which changes their fp32 rounding)
+        side = self._score_stream() if (self.score_overlap and K > 1 and isinstance(self.cost, RBFLinearCost)) else None
         for t in range(K):
             self.step(act_next=t + 1 < K)
             if side is not None and t + 1 < K:

@@ -33,8 +33,10 @@ and copied to the host ONCE at the end; each path's arrays are views of that cop
 """
 from __future__ import annotations
 
+import gc
 import math
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -228,7 +230,9 @@ class _ChunkGraph:
 
     def __init__(self, eng: RolloutEngine, K: int, noise_dev):
         c = eng.ctx
-        self.eng, self.K = eng, K
+        # (a weak reference: the graph is cached on the engine, engine -> graph -> engine would be
+        # a reference cycle that only the garbage collector frees)
+        self.eng, self.K = weakref.proxy(eng), K
         self.g = torch.cuda.CUDAGraph()
         if eng._graph_ahead:
             eng.step_counter = int(eng.dev_step.item())
@@ -236,10 +240,16 @@ class _ChunkGraph:
         side = torch.cuda.Stream(c.device)
         side.wait_stream(torch.cuda.current_stream(c.device))
         t0 = eng.t
+        # no garbage collection during the capture: a collected cycle holding another graph or
+        # device memory would be torn down in the middle of it (a HIP error / abort).  One
+        # collection up front (torch.cuda.graph does the same), then the collector is off until
+        # capture_end.  (capture_begin/end directly: torch.cuda.graph's context manager also
+        # synchronises and empties the allocator cache, 13 ms per capture)
+        gc.collect()
+        gc_was_on = gc.isenabled()
+        gc.disable()
         with torch.cuda.stream(side):
             eng._capturing = True
-            # capture_begin/end directly: torch.cuda.graph's context manager also synchronises,
-            # garbage-collects and empties the allocator cache (13 ms per sample_points call)
             self.g.capture_begin(capture_error_mode="thread_local")
             try:
                 for k in range(K):
@@ -248,6 +258,8 @@ class _ChunkGraph:
             finally:
                 self.g.capture_end()
                 eng._capturing = False
+                if gc_was_on:
+                    gc.enable()
         torch.cuda.current_stream(c.device).wait_stream(side)
         eng.t, eng.step_counter = t0, eng.step_counter - K  # the captured steps did not run
         eng._graph_ahead = True

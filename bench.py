@@ -93,9 +93,10 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="replay the whole rollout as captured HIP graph(s); auto = off: eager launches measured "
                         "faster at every per-rank share on ROCm 7 (profiles/r05z_graph_vs_eager.txt)")
-    p.add_argument("--score-overlap", choices=["on", "off"], default="on",
+    p.add_argument("--score-overlap", choices=["on", "off"], default="off",
                    help="score each step's cost rows on a side stream under the next step's policy "
-                        "(RolloutEngine.score_overlap; bit-identical to the batched pass at the rollout's end)")
+                        "(RolloutEngine.score_overlap; bit-identical to the batched pass at the rollout's end; measured "
+                        "1.6 %% slower at 8192 x 5, profiles/r06h_score_overlap_ab.txt)")
     p.add_argument("--fuse-assembly", choices=["on", "off"], default="off",
                    help="f16x3: the policy launch also writes the ensemble's x0 slice (RolloutEngine.fuse_assembly)")
     p.add_argument("--overlap", choices=["on", "off"], default="off",
