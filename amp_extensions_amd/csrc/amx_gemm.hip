@@ -109,13 +109,6 @@ __device__ __forceinline__ uint64_t row_valid_mask(const GemmArgs& a, int row0, 
 #ifndef H3_W4
 #define H3_W4 0
 #endif
-// H3_STORE_WT (A/B builds: 0 = plain stores): the f16x3 epilogues (the 16x16x32 tiles: hidden
-// slices and the output layer's deltas) store write-through (sc1: the line leaves the XCD's L2
-// at once instead of sitting dirty there until the kernel's end-of-launch writeback, which the
-// next dependent launch waits for: MI355X_MICROARCH.md, price list row 'boundary')
-#ifndef H3_STORE_WT
-#define H3_STORE_WT 0
-#endif
 // OUT80 (A/B builds): 1 = the 80 x 224 output tile where it makes exactly one tile per CU
 #ifndef OUT80
 #define OUT80 1
@@ -707,14 +700,6 @@ __device__ __forceinline__ void epilogue_h3_impl(const GemmArgs& a, f32x16 (&acc
   }
 }
 
-__device__ __forceinline__ void store_wt(float* p, float v) {
-  if constexpr (H3_STORE_WT) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    *p = v;
-  }
-}
-
 // epilogue of the 16x16x32 form: block (m, n) of the wave holds, per lane, column n*16 + (l&15)
 // and rows m*16 + 4(l>>4) + j (j = reg); the row-exponent reduction is a reduce-scatter over
 // the 16 column lanes of the lane's MB*4 rows
@@ -813,7 +798,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
           const int row = row0 + m * 16 + 4 * lq + j;
           float v = __builtin_amdgcn_ldexpf(acc[m][n][j], er[j] + ec[n]) + bv[n];
           if (a.act == AMX_ACT_RELU) v = (v < 0.f) ? 0.f : v;  // keeps NaN, as torch.relu
-          store_wt(Cg + (long long)row * a.ldc + a.col_off + col, v);
+          Cg[(long long)row * a.ldc + a.col_off + col] = v;
           const uint32_t b = __float_as_uint(v) & 0x7fffffffu;
           mx[m * 4 + j] = mx[m * 4 + j] > b ? mx[m * 4 + j] : b;
         }
@@ -868,7 +853,7 @@ __device__ __forceinline__ void epilogue_h3_m16(const GemmArgs& a, f32x4 (&acc)[
             const int row = row0 + m * 16 + 4 * lq + j;
             const float y = __builtin_amdgcn_ldexpf(acc[m][n][j], er[j] + ec) + bv;
             const float prod = y * sc;    // two roundings, as torch's (y*scale)+mean
-            store_wt(Cg + (long long)row * a.ldc + col, prod + sh);
+            Cg[(long long)row * a.ldc + col] = prod + sh;
           }
         }
       }

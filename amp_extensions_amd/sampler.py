@@ -271,6 +271,20 @@ class _ChunkGraph:
         self.eng._graph_ahead = True
 
 
+def _to_host_path_order(perm: torch.Tensor, arrays) -> list:
+    """The store's rows gathered into path order on the device, then ONE copy each into pinned
+    host memory (2-4x the pageable .cpu() rate; torch's pinned-block cache reuses the blocks of
+    paths the caller has dropped).  The returned numpy arrays keep their pinned tensors alive."""
+    sel = [x.index_select(0, perm) for x in arrays]
+    pin = torch.cuda.is_available()
+    host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=pin) for t in sel]
+    for h, t in zip(host, sel):
+        h.copy_(t, non_blocking=pin)
+    if pin:
+        torch.cuda.current_stream(sel[0].device).synchronize()
+    return [h.numpy() for h in host]
+
+
 def _chunk_graph(eng: RolloutEngine, K: int, noise_dev, eval_mode: bool) -> _ChunkGraph:
     """The chunk's captured graph, cached on the engine across sample_points calls: it bakes in
     the engine's and the policy's device buffers (persistent; DevicePolicy.sync_from rewrites
@@ -465,7 +479,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
         return [], 0
     perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
     pd = torch.from_numpy(perm).to(dev)
-    host = [x.index_select(0, pd).cpu().numpy() for x in (store.obs, store.nxt, store.act, store.mean)]
+    host = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean))
     log_std = np.float64(eng.policy.log_std_val)
     paths, off = [], 0
     for tr in trajs:
@@ -678,7 +692,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         return [], 0
     perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
     pd = torch.from_numpy(perm).to(dev)
-    host = [x.index_select(0, pd).cpu().numpy() for x in (store.obs, store.nxt, store.act, store.mean)]
+    host = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean))
     log_std = np.float64(eng.policy.log_std_val)
     paths, off = [], 0
     for tr in trajs:
