@@ -1434,6 +1434,12 @@ using H80x224 = TileH3<1, 7, 1, 1, 1, 2, true, true, true, 5, 2, true, true, tru
 
 using H128x224k16 = TileH3<2, 7, 2, 1, 4>;  // K not a multiple of 32
 using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, true>;
+// small-row tiles (the reference-semantics sampler: a few hundred lanes, or 128 per member when
+// each lane runs its own member only): 128 x 64 hidden tiles (4 waves of 64 x 32) and 128 x 32
+// output tiles (4 waves of 32 x 32), stream-K over up to one workgroup per CU (small_plan) --
+// the weight panels read once per K range, 8-32 KB partial tiles per segment
+using HS64 = TileH3<2, 2, 1, 1, 2, 2, true, true, true, 4, 2, true, true, true>;
+using HS32 = TileH3<4, 1, 1, 1, 2, 2, true, true, true, 2, 2, true, true, true>;
 
 using X128 = TileX6<2, 2, 2, 2>;        // 128x128, 4 waves of 64x64 (57 KB): 2 WGs / CU
 using X256 = TileX6<2, 4, 4, 2>;        // 256x256, 8 waves of 128x64 (115 KB): 1 WG / CU
@@ -1732,22 +1738,38 @@ extern "C" int amx_row_exponents(amx_ctx* ctx, int groups, int rows, int K, cons
   return AMX_OK;
 }
 
-// Hidden-layer tiles of a stream-K launch (128 x 256, HRow<4>) when 128 x 256 tiles would fill
-// less than half the CUs (rows < 2048 at 4 members, N = 512): SPLIT = min(CUs / tiles, 6)
-// workgroups per tile over contiguous K ranges of at least 4 K-tiles, combined in K order by the
-// last arriver before the bias / ReLU / row-exponent epilogue.  0: not used.  (At the sampler's
-// 640 lanes the 128 x 128 grid put 80 workgroups on the CUs: 37 us per layer.)
-static int streamk_hidden(const amx_ctx* ctx, int groups, int rows, int N, int K, int* nwg, int* ksplit) {
-  if (N % 256 != 0 || K % 32 != 0 || rows % 128 != 0) return 0;
-  const int tiles = rows / 128 * (N / 256) * groups;
-  if (tiles < 1 || 2 * tiles >= ctx->n_cus) return 0;
-  int split = ctx->n_cus / tiles;
-  split = split > 6 ? 6 : split;
-  while (split > 1 && (K / 32) / split < 4) --split;
-  if (split < 2) return 0;
-  *nwg = tiles * split;
-  *ksplit = split;
+// Few rows (128 x 256 hidden tiles would fill less than half the CUs: rows x groups < 8192 at
+// N = 512; the reference-semantics sampler's 128-640 rows per member): bm x bn tiles (HS64 /
+// HS32), each tile's K range cut into ks = clamp(round(K/32 / 7), 1, 8) contiguous segments of
+// about seven K-tiles, one workgroup per segment (k_gemm_h3's stream-K with G = tiles x ks
+// workgroups: workgroup v runs units [v U / G, (v + 1) U / G) = segment v % ks of tile v / ks),
+// the segments combined in K order by the tile's last arriver (split_combine).  ks depends on K
+// alone, so a row's result does not depend on how many rows the launch has (a rank's lanes
+// equal the same lanes of one process, bit for bit).  Returns the tile count (0: shape not
+// covered), *nwg = G and *ksplit = ks.  (Rounds 3-6 used 128 x 256 tiles split at most 6 ways
+// here: 33.7 us per hidden layer at the sampler's 640 lanes, profiles/r06q_paths_trace_summary.txt
+// -- each workgroup ran a 10-K-tile chain and wrote a 128 KB partial tile.)
+#ifndef SMALL_KT
+#define SMALL_KT 7     // K-tiles per segment (target)
+#endif
+#ifndef SMALL_KSMAX
+#define SMALL_KSMAX 8  // segments per tile at most
+#endif
+static int small_plan(const amx_ctx* ctx, int groups, int rows, int N, int K, int bn, int* nwg, int* ksplit) {
+  (void)ctx;
+  if (rows <= 0 || rows % 128 != 0 || N % bn != 0 || K % 32 != 0 || groups < 1) return 0;
+  const int tiles = rows / 128 * (N / bn) * groups;
+  const int nk = K / 32;
+  int ks = (nk + SMALL_KT / 2) / SMALL_KT;
+  ks = ks < 1 ? 1 : (ks > SMALL_KSMAX ? SMALL_KSMAX : ks);
+  if (nwg) *nwg = tiles * ks;
+  if (ksplit) *ksplit = ks;
   return tiles;
+}
+
+// the hidden layers' shapes that take the small-row tiles
+static bool small_hidden(const amx_ctx* ctx, int groups, int rows, int N) {
+  return N % 256 == 0 && rows % 128 == 0 && 2LL * (rows / 128) * (N / 256) * groups < ctx->n_cus;
 }
 
 extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, int K, const float* A, int lda,
@@ -1793,13 +1815,13 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
       }
     }
   }
-  {  // few tiles (the sampler's few hundred lanes): 128 x 256 tiles split over K (stream-K)
+  if (small_hidden(ctx, groups, rows, N)) {  // few rows (the sampler's lanes): HS64 tiles, stream-K
     int nwg = 0, ksplit = 0;
-    const int tiles = streamk_hidden(ctx, groups, rows, N, K, &nwg, &ksplit);
+    const int tiles = small_plan(ctx, groups, rows, N, K, HS64::BN, &nwg, &ksplit);
     if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
-        ctx->split_floats >= (long long)tiles * ksplit * 128 * 256) {
+        ctx->split_floats >= (long long)tiles * ksplit * HS64::BM * HS64::BN) {
       a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
-      return launch_h3<EPI_BIAS_ACT, HRow<4>>(a, s);
+      return launch_h3<EPI_BIAS_ACT, HS64>(a, s);
     }
   }
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
@@ -1807,16 +1829,13 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
 }
 
 // Output-layer tiles (128 x 224, S <= 224) of a stream-K launch for `rows` padded lanes x
-// `groups` members, 0 when the shape does not use it; *nwg workgroups, *ksplit slots per tile.
-//  * fewer tiles than CUs but at least half as many (4096-7168 lanes x 4 members): one workgroup
-//    per CU, the tiles' K-tiles dealt out evenly, so a tile's K range spans at most 3 workgroups;
-//  * fewer than half (the reference-semantics sampler's few hundred lanes: 20 tiles at 640):
-//    SPLIT = min(CUs / tiles, 6) workgroups per tile, each a contiguous K range (nwg = tiles x
-//    SPLIT, so every tile is exactly SPLIT segments); a one-wave tile grid left most CUs idle
-//    and ran the whole K = 2304 chain per tile (71 us at 640 lanes).  The last arriver reads
-//    SPLIT - 1 partial tiles, so SPLIT stays small.
+// `groups` members when the tiles are fewer than the CUs but at least half as many (4096-7168
+// lanes x 4 members: 128-224 tiles): one workgroup per CU, the tiles' K-tiles dealt out evenly,
+// so a tile's K range spans at most 3 workgroups (*nwg workgroups, *ksplit slots per tile);
+// 0 when the shape does not use it.  Fewer tiles than that take the small-row HS32 tiles
+// (small_out).
 static int streamk_tiles(const amx_ctx* ctx, int groups, int rows, int* nwg = nullptr, int* ksplit = nullptr,
-                         int K = 0, int bm = 128) {
+                         int bm = 128) {
   const int n32 = amx::round_up(ctx->S, 32);
   if (n32 <= 128 || n32 > 224 || rows % bm != 0) return 0;
   const int tiles = rows / bm * groups;
@@ -1825,19 +1844,15 @@ static int streamk_tiles(const amx_ctx* ctx, int groups, int rows, int* nwg = nu
     if (ksplit) *ksplit = 3;
     return tiles;
   }
-  if (tiles >= 1 && 2 * tiles < ctx->n_cus) {
-    int split = ctx->n_cus / tiles;
-    split = split > 6 ? 6 : split;
-    if (K > 0) {  // at least 4 K-tiles (of 32) per segment
-      const int nk = K / 32;
-      while (split > 1 && nk / split < 4) --split;
-    }
-    if (split < 2) return 0;
-    if (nwg) *nwg = tiles * split;
-    if (ksplit) *ksplit = split;
-    return tiles;
-  }
   return 0;
+}
+
+// the output layer's shapes (S <= 224) that take the small-row tiles: fewer 128 x 224 tiles than
+// half the CUs (the sampler's lanes; a one-wave 128 x 224 grid ran the whole K = 2304 chain per
+// tile, 71 us at 640 lanes in round 3, then 35 us split at most 6 ways)
+static bool small_out(const amx_ctx* ctx, int groups, int rows) {
+  const int n32 = amx::round_up(ctx->S, 32);
+  return n32 > 128 && n32 <= 224 && rows % 128 == 0 && 2LL * (rows / 128) * groups < ctx->n_cus;
 }
 
 extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_valid, int K, const float* A,
@@ -1881,7 +1896,15 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
     // members: 128-224 tiles): stream-K over one workgroup per CU (each tile's K range in <= 3
     // segments), instead of the row-block tiles' 4-7 waves per workgroup
     int nwg = 0, ksplit = 0;
-    const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, K);
+    if (small_out(ctx, groups, rows)) {  // few rows (the sampler's lanes): HS32 tiles, stream-K
+      const int tiles = small_plan(ctx, groups, rows, 224, K, HS32::BN, &nwg, &ksplit);
+      if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
+          ctx->split_floats >= (long long)tiles * ksplit * HS32::BM * HS32::BN) {
+        a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
+        return launch_h3<EPI_UNNORM, HS32>(a, s);
+      }
+    }
+    const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit);
     if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
         ctx->split_floats >= (long long)tiles * ksplit * 128 * 224) {
       a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
@@ -1965,15 +1988,28 @@ extern "C" int amx_set_split_workspace(amx_ctx* ctx, float* scratch, long long f
 
 extern "C" long long amx_split_workspace_floats(const amx_ctx* ctx, int groups, int rows, int* n_counters) {
   if (!ctx || groups < 1 || rows <= 0) return -1;
-  int nwg = 0, ksplit = 0, nwg_h = 0, ksplit_h = 0;
-  const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit, ctx->k0_pad + ctx->L * ctx->H);
-  // the hidden layers' split at their largest K (every smaller K splits no wider)
-  const int tiles_h = ctx->H % 256 == 0 && ctx->L > 1
-                          ? streamk_hidden(ctx, groups, rows, ctx->H, ctx->k0_pad + (ctx->L - 1) * ctx->H, &nwg_h,
-                                           &ksplit_h)
-                          : 0;
-  const int nc = tiles > tiles_h ? tiles : tiles_h;
+  long long floats = 0;
+  int nc = 0;
+  auto need = [&](int tiles, int ksplit, int bm, int bn) {
+    if (tiles <= 0) return;
+    const long long f = (long long)tiles * ksplit * bm * bn;
+    floats = f > floats ? f : floats;
+    nc = tiles > nc ? tiles : nc;
+  };
+  int nwg = 0, ksplit = 0;
+  const int ldk = ctx->k0_pad + ctx->L * ctx->H;
+  const int to = streamk_tiles(ctx, groups, rows, &nwg, &ksplit);
+  need(to, ksplit, 128, 224);
+  if (small_out(ctx, groups, rows)) {
+    const int t = small_plan(ctx, groups, rows, 224, ldk, HS32::BN, &nwg, &ksplit);
+    need(t, ksplit, HS32::BM, HS32::BN);
+  }
+  if (small_hidden(ctx, groups, rows, ctx->H)) {
+    for (int i = 0; i < ctx->L; ++i) {  // every hidden layer's K (segments per tile depend on it)
+      const int t = small_plan(ctx, groups, rows, ctx->H, ctx->k0_pad + i * ctx->H, HS64::BN, &nwg, &ksplit);
+      need(t, ksplit, HS64::BM, HS64::BN);
+    }
+  }
   if (n_counters) *n_counters = nc;
-  const long long fo = (long long)tiles * ksplit * 128 * 224, fh = (long long)tiles_h * ksplit_h * 128 * 256;
-  return fo > fh ? fo : fh;
+  return floats;
 }

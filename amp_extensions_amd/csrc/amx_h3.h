@@ -244,6 +244,45 @@ __device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL
   }
   __syncthreads();
   if (!*flag) return false;
+  if constexpr (TL::NT == 256 && MB * NB <= 8) {
+    // the small-row tiles (HS64 / HS32: up to 8 segments): the loads of four segments in flight
+    // per round trip (each a write-through partial in memory, ~1-2 us away), then the sums in K
+    // order -- v = P0, v += P1, ... exactly as below
+    f32x4 v[MB][NB];
+    for (int s0 = 0; s0 < nseg; s0 += 4) {
+      f32x4 p[4][MB][NB];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = s0 + q;
+        if (s < nseg && s != seg) {
+#pragma unroll
+          for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int n = 0; n < NB; ++n)
+              p[q][m][n] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                         rs, (int)(((s * MB + m) * NB + n) * NT + t) * 16, 0, 16));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int s = s0 + q;
+        if (s < nseg) {
+#pragma unroll
+          for (int m = 0; m < MB; ++m)
+#pragma unroll
+            for (int n = 0; n < NB; ++n) {
+              const f32x4 x = s == seg ? acc[m][n] : p[q][m][n];
+              v[m][n] = s == 0 ? x : v[m][n] + x;
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < MB; ++m)
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[m][n] = v[m][n];
+    return true;
+  }
   // per block: v = P0, v += P1, ... (own segment from the accumulators) -- the segments' sum in
   // K order without a second copy of the accumulators (which spilled the 128-accumulator tiles).
   // (Round 4: reading this segment's slot back with the others so every segment's loads are in

@@ -251,6 +251,61 @@ class DeviceEnsemble:
             self._ws[Bp] = ws
         return ws
 
+    def workspace_blocked(self, Bq: int):
+        """Buffers of the member-blocked forward (forward_blocked): M blocks of Bq lanes, lane
+        b = g * Bq + r runs member g only.  act [M * Bq][ldk] (one x0 per lane), preds
+        [M * Bq][S] (lane b's delta at row b), row exponents [M][slots][Bq]."""
+        if Bq <= 0 or Bq % 128:
+            raise ValueError(f"member blocks of {Bq} lanes: must be a positive multiple of 128")
+        key = ("blocked", Bq)
+        ws = self._ws.get(key)
+        if ws is None:
+            c = self.ctx
+            ws = dict(Bq=Bq, act=torch.zeros(c.M * Bq, c.ldk, dtype=torch.float32, device=c.device),
+                      preds=torch.zeros(c.M * Bq, c.S, dtype=torch.float32, device=c.device),
+                      rexp=torch.zeros(c.M, self.n_slots, Bq, dtype=torch.int32, device=c.device))
+            self._ensure_split_workspace(Bq)
+            self._ws[key] = ws
+        return ws
+
+    def forward_blocked(self, ob: torch.Tensor, act: torch.Tensor, Bq: int) -> torch.Tensor:
+        """One member per lane: lanes [g * Bq, (g + 1) * Bq) through member g alone (SimEnv.step
+        runs the lane's current member only, sim_env.py:154-157, with reset_counter % M choosing
+        it at reset, :282-283).  A quarter of forward_preds' rows for the reference-semantics
+        sampler, whose lanes are placed in the block of their trajectory's member.  Returns
+        preds [M * Bq][S] (view of the workspace).  f16x3 only."""
+        if self.W2 is None:
+            raise ValueError("forward_blocked needs the f16x3 GEMM")
+        c = self.ctx
+        B = c.M * Bq
+        if ob.dtype != act.dtype or ob.dtype not in (torch.float64, torch.float32):
+            raise ValueError("ob and act must both be float64 or both float32")
+        _check_dev(ob, ob.dtype, "ob", c.device)
+        _check_dev(act, act.dtype, "act", c.device)
+        if ob.shape[-1] != c.S or act.shape[-1] != c.A or ob.shape[0] < B or act.shape[0] < B:
+            raise ValueError(f"ob {tuple(ob.shape)} / act {tuple(act.shape)} do not match S={c.S}, A={c.A}, "
+                             f"{c.M} blocks of {Bq} lanes")
+        ws = self.workspace_blocked(Bq)
+        buf, preds, rexp = ws["act"], ws["preds"], ws["rexp"]
+        s = c.stream
+        dt = N.AMX_IN_F64 if ob.dtype == torch.float64 else N.AMX_IN_F32
+        N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), 0, c.ldk, B, s),
+                "amx_assemble_input")
+        sA, sR, L = Bq * c.ldk, self.n_slots * Bq, c.L
+        N.check(c.lib.amx_row_exponents(c.h, c.M, Bq, c.k0_pad, buf.data_ptr(), c.ldk, sA, rexp.data_ptr(), sR,
+                                        self.n_slots, s), "amx_row_exponents")
+        for i in range(L):
+            K = c.k0_pad + i * c.Hp
+            N.check(c.lib.amx_gemm_bias_act_h3(c.h, c.M, Bq, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),
+                                               c.Hp * 2 * K, self.wexp[i].data_ptr(), c.Hp, self.b[i].data_ptr(), c.Hp,
+                                               buf.data_ptr(), c.ldk, sA, K, N.AMX_ACT_RELU, rexp.data_ptr(), sR,
+                                               i + 1, rexp[0, i + 1].data_ptr(), 0, s), "amx_gemm_bias_act_h3")
+        N.check(c.lib.amx_gemm_out_unnorm_h3(c.h, c.M, Bq, c.S, c.ldk, buf.data_ptr(), c.ldk, sA,
+                                             self.W2[L].data_ptr(), c.n_out_pad * 2 * c.ldk, self.wexp[L].data_ptr(),
+                                             c.n_out_pad, self.b[L].data_ptr(), c.n_out_pad, preds.data_ptr(), c.S,
+                                             Bq * c.S, rexp.data_ptr(), sR, L + 1, 0, s), "amx_gemm_out_unnorm_h3")
+        return preds
+
     def _ensure_split_workspace(self, Bp: int) -> None:
         """Register the output layer's split-K scratch with the context when Bp lanes split
         (amx_split_workspace_floats > 0); the buffer only grows.  A replaced buffer stays

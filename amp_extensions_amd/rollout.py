@@ -152,6 +152,10 @@ class RolloutEngine:
         # (bit-identical; see rollout)
         self.score_overlap = False
         self._side = None
+        # member-blocked stepping (the reference-semantics sampler): Bq > 0 = the lanes are M
+        # blocks of Bq and lane b steps through member b // Bq only (DeviceEnsemble.forward_blocked;
+        # its trajectory was reset onto that member), without the per-step disagreement
+        self.member_blocks = 0
 
     # ------------------------------------------------------------------------------------
     def reset_all(self, rows: torch.Tensor | None = None) -> None:
@@ -279,6 +283,10 @@ class RolloutEngine:
                             x0=None if ws is None else ws["act"], row_exp=None if ws is None else ws["rexp"],
                             shared_x0=fuse_x0)
             x0_ready = fuse_x0
+        if self.member_blocks:
+            if x0_ready or self.B != self.ctx.M * self.member_blocks:
+                raise ValueError("member-blocked stepping needs M * member_blocks lanes and no fused x0")
+            return t, src, self.ens.forward_blocked(ob, act, self.member_blocks)
         preds = self.ens.forward_preds(ob, act, B, x0_ready=x0_ready)
         return t, src, preds
 
@@ -289,14 +297,18 @@ class RolloutEngine:
         t, src, preds = front
         fused = self.auto_reset and self.motion is None and self.fuse_reset
         ob, ob_next = self.obs[src], self.next_obs[t]
+        # member stride of preds (0: member-blocked, lane b's own member at row b) and the
+        # disagreement output (not formed per step when member-blocked)
+        sP = 0 if self.member_blocks else preds.shape[1] * c.S
+        disc = self.disc[t].data_ptr() if c.M >= 2 and not self.member_blocks else None
         if fused and act_next:  # step t + policy(t+1) + x0(t+1) in one launch
             ss = self.cost_type == "ss"
             pol, ws = self.policy, self.ens.workspace(B)
             rx = ws["rexp"]
             N.check(c.lib.amx_step_reset_act(
-                c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(), ob.data_ptr(),
+                c.h, preds.data_ptr(), c.S, sP, self.model_idx.data_ptr(), ob.data_ptr(),
                 ob_next.data_ptr(), self.num_steps.data_ptr(), self.done[t].data_ptr(),
-                self.disc[t].data_ptr() if c.M >= 2 else None, self.cost_in[t].data_ptr() if ss else None, self.kc,
+                disc, self.cost_in[t].data_ptr() if ss else None, self.kc,
                 self.cost_rexp[t].data_ptr() if ss and self.cost_rexp is not None else None,
                 self.nonfinite[t].data_ptr(), self.table.data_ptr(), self.table.shape[0], None, self.seed,
                 self.obs[t + 1].data_ptr(), self.reset_count.data_ptr(), self.reset_rows[t].data_ptr(),
@@ -314,9 +326,9 @@ class RolloutEngine:
             # (amx_counter_add folded into the step kernel: one graph node fewer)
             last = self._capturing and self._ctr_delta and t == self._ctr_delta - 1
             ctr, ctr_delta = (self.dev_step, self._ctr_delta) if last else (None, 0)
-            N.check(c.lib.amx_step_reset(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+            N.check(c.lib.amx_step_reset(c.h, preds.data_ptr(), c.S, sP, self.model_idx.data_ptr(),
                                          ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
-                                         self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                                         self.done[t].data_ptr(), disc,
                                          self.cost_in[t].data_ptr() if ss else None, self.kc,
                                          self.cost_rexp[t].data_ptr() if ss and self.cost_rexp is not None else None,
                                          self.nonfinite[t].data_ptr(), self.table.data_ptr(), self.table.shape[0],
@@ -328,15 +340,15 @@ class RolloutEngine:
                     "amx_step_reset")
             self._ctr_folded = ctr is not None
         elif self.cost_type == "ss" and self.cost_rexp is not None:
-            N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+            N.check(c.lib.amx_step_rexp(c.h, preds.data_ptr(), c.S, sP, self.model_idx.data_ptr(),
                                         ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
-                                        self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                                        self.done[t].data_ptr(), disc,
                                         self.cost_in[t].data_ptr(), self.kc, self.cost_rexp[t].data_ptr(),
                                         self.nonfinite[t].data_ptr(), B, s), "amx_step_rexp")
         else:
-            N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, preds.shape[1] * c.S, self.model_idx.data_ptr(),
+            N.check(c.lib.amx_step(c.h, preds.data_ptr(), c.S, sP, self.model_idx.data_ptr(),
                                    ob.data_ptr(), ob_next.data_ptr(), self.num_steps.data_ptr(),
-                                   self.done[t].data_ptr(), self.disc[t].data_ptr() if c.M >= 2 else None,
+                                   self.done[t].data_ptr(), disc,
                                    self.cost_in[t].data_ptr() if self.cost_type == "ss" else None, self.kc,
                                    self.nonfinite[t].data_ptr(), B, s), "amx_step")
         if self.cost is not None and self.cost_type != "ss":

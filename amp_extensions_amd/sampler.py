@@ -106,6 +106,30 @@ class _Store:
         return base
 
 
+class _FreeLanes:
+    """The idle lanes.  Member-blocked engines (RolloutEngine.member_blocks = Bq: lane b runs
+    member b // Bq only) keep one list per member: trajectory j resets to member j mod M
+    (sim_env.py:282-283 with the counter at j - 1), so it takes a lane of that block."""
+
+    def __init__(self, L: int, M: int, Bq: int):
+        self.M, self.Bq = M, Bq
+        if Bq:
+            self.lists = [list(range((g + 1) * Bq - 1, g * Bq - 1, -1)) for g in range(M)]
+        else:
+            self.lists = [list(range(L - 1, -1, -1))]
+
+    def __bool__(self) -> bool:
+        return any(self.lists)
+
+    def take(self, j: int) -> int:
+        """A lane for trajectory j (-1: none of its member's block is free)."""
+        lst = self.lists[j % self.M if self.Bq else 0]
+        return lst.pop() if lst else -1
+
+    def put(self, lane: int) -> None:
+        self.lists[lane // self.Bq if self.Bq else 0].append(lane)
+
+
 def _reset_time_max(env) -> float:
     """The reset-time window [0, time_max) every trajectory's env.reset() draws from
     (sim_env.py:76-77, 276): reset_args['time_max'] when custom_time is on, else the clip length
@@ -120,12 +144,14 @@ def _reset_time_max(env) -> float:
     return src.motion.get_motion_length() if src.motion is not None else float(src.table.shape[0])
 
 
-def _sampler_engine(env, lanes: int, K: int, policy, time_max: float) -> RolloutEngine:
+def _sampler_engine(env, lanes: int, K: int, policy, time_max: float, member_blocks: int = 0) -> RolloutEngine:
     """A lanes-sized engine on the env's ensemble, reset source and termination (cached per
-    lane count, chunk and reset window); its device-drawn motion resets use the env's window."""
+    lane count, chunk, reset window and member blocking); its device-drawn motion resets use the
+    env's window.  member_blocks = Bq > 0: lanes = M * Bq, lane b steps through member b // Bq
+    only (RolloutEngine.member_blocks)."""
     src = env.engine if isinstance(env, BatchedSimEnv) else env
     cache = src.__dict__.setdefault("_sampler_engines", {})
-    key = (lanes, K, float(time_max))
+    key = (lanes, K, float(time_max), int(member_blocks))
     eng = cache.get(key)
     if eng is None:
         reset_source = src.motion if src.motion is not None else src.table
@@ -134,6 +160,7 @@ def _sampler_engine(env, lanes: int, K: int, policy, time_max: float) -> Rollout
         # (0 = the whole clip; a table source is already cut to the window's rows)
         if src.motion is not None and time_max != src.motion.get_motion_length():
             eng.reset_time_max = float(time_max)
+        eng.member_blocks = int(member_blocks)
         cache[key] = eng
     # the env's reset_args noise (AddNoise) as it is NOW: a later set_reset_noise on the env
     # reaches the cached engine.  The noise draws come from Philox(engine seed; lane, reset#),
@@ -338,7 +365,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     next_j = [1] * W
     done_w = [False] * W
     lane_tr: list[_Traj | None] = [None] * L
-    free = list(range(L - 1, -1, -1))
+    free = _FreeLanes(L, c.M, eng.member_blocks)
     store = _Store(dev, S, A, W * (quota + R) if mode == "samples" else W * quota * 64)
     eng.eval_mode = eval_mode
     ref_noise = rng == "reference" and not eval_mode
@@ -361,7 +388,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     def drop(tr: _Traj) -> None:
         if tr.lane >= 0:
             lane_tr[tr.lane] = None
-            free.append(tr.lane)
+            free.put(tr.lane)
             tr.lane = -1
 
     while True:
@@ -403,9 +430,12 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
                     ok = len(trs) < quota
                 if ok:
                     j = next_j[w]
+                    lane = free.take(j)
+                    if lane < 0:  # (member-blocked: j waits for a lane of its member's block)
+                        continue
                     next_j[w] += 1
                     tr = _Traj(w, j, 12345 + base_seed * w + j)
-                    tr.lane = free.pop()
+                    tr.lane = lane
                     lane_tr[tr.lane] = tr
                     trs.append(tr)
                     new.append(tr)
@@ -531,7 +561,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
     next_j = [1] * W
     done_w = [False] * W
     lane_tr: list[_Traj | None] = [None] * L
-    free = list(range(L - 1, -1, -1))
+    free = _FreeLanes(L, c.M, eng.member_blocks)
     store = _Store(dev, S, A, W * (quota + R) if mode == "samples" else W * quota * 64)
     ring = _ChunkRing(eng, K)
     eng.eval_mode = eval_mode
@@ -559,7 +589,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
     def drop(tr: _Traj) -> None:
         if tr.lane >= 0:
             lane_tr[tr.lane] = None
-            free.append(tr.lane)
+            free.put(tr.lane)
             tr.lane = -1
 
     def process(p) -> None:
@@ -628,9 +658,12 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
                     ok = len(trs) < quota
                 if ok:
                     j = next_j[w]
+                    lane = free.take(j)
+                    if lane < 0:  # (member-blocked: j waits for a lane of its member's block)
+                        continue
                     next_j[w] += 1
                     tr = _Traj(w, j, 12345 + base_seed * w + j)
-                    tr.lane = free.pop()
+                    tr.lane = lane
                     lane_tr[tr.lane] = tr
                     trs.append(tr)
                     new.append(tr)
@@ -708,7 +741,8 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
 
 def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_workers: int = 4, mode: str = "samples",
                   eval_mode: bool = False, verbose: bool = False, deepmimic: bool = False, rng: str = "reference",
-                  chunk: int = 16, speculate: bool = True, graph: bool = True, pipeline: bool = True):
+                  chunk: int = 16, speculate: bool = True, graph: bool = True, pipeline: bool = True,
+                  member_blocked: bool = True):
     """milo.sampler.sample_points on the GPU.  `env` is a BatchedSimEnv (or a RolloutEngine):
     its ensemble, reset source, reset-time window (reset_args custom_time / time_max) and
     termination are used, and its lane count caps the concurrency; `policy` a DevicePolicy or
@@ -719,7 +753,10 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
     `speculate`: admit beyond the worst-case reservation from the observed trajectory lengths
     (same result, see _collect); `graph`: replay each chunk's steps as a captured HIP graph;
     `pipeline`: queue chunk i before reading chunk i-1's done flags (same result,
-    _collect_pipelined)."""
+    _collect_pipelined); `member_blocked` (f16x3 ensembles with M >= 2): every lane steps through
+    its trajectory's member only, as SimEnv.step does (the engine's lanes in M blocks of a
+    multiple of 128; a quarter of the ensemble rows per step at M = 4), instead of all M members
+    on every lane (same paths up to the GEMM's fp32 rounding)."""
     assert mode == "samples" or mode == "trajectories"
     if rng not in ("reference", "device"):
         raise ValueError("rng must be 'reference' or 'device'")
@@ -731,10 +768,17 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
     if speculate and mode == "samples":
         need *= 4  # room for trajectories shorter than the horizon (lengths ~R/4) to run at once
     lanes = max(1, min(need, src.B))
+    M = src.ctx.M
+    Bq = 0
+    if member_blocked and M >= 2 and src.ens.W2 is not None:
+        Bq = math.ceil(math.ceil(need / M) / 128) * 128  # member blocks of a multiple of 128 lanes
+        while Bq > 128 and M * Bq > max(src.B, M * 128):
+            Bq -= 128
+        lanes = M * Bq
     K = max(1, min(int(chunk), R))
     time_max = _reset_time_max(env)
     policy = device_policy(env, policy)
-    eng = _sampler_engine(env, lanes, K, policy, time_max)
+    eng = _sampler_engine(env, lanes, K, policy, time_max, Bq)
     if rng == "device":
         policy.seed = (12345 + int(base_seed)) & 0xFFFFFFFFFFFFFFFF
     t0 = time.time()

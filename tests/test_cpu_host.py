@@ -327,3 +327,20 @@ def test_reference_checkpoint_loads_into_host_members(golden, golden_path):
             assert torch.equal(W, W2) and torch.equal(b, b2)
         for (W, b), (Wr, br) in zip(init_model_weights(S, A, hidden, 100 + k), R.init_model_weights(S, A, hidden, 100 + k)):
             assert torch.equal(W, Wr) and torch.equal(b, br)
+
+
+def test_sampler_free_lanes_member_blocks():
+    """The sampler's idle-lane pool: one list without member blocks; with blocks of Bq lanes
+    trajectory j takes a lane of block j mod M (the member its reset selects), -1 when that
+    block is full, and a freed lane returns to its own block."""
+    from amp_extensions_amd.sampler import _FreeLanes
+    f = _FreeLanes(5, 4, 0)
+    assert [f.take(j) for j in range(1, 6)] == [0, 1, 2, 3, 4] and not f and f.take(1) == -1
+    f.put(3)
+    assert f and f.take(7) == 3
+    g = _FreeLanes(8, 4, 2)
+    got = [g.take(j) for j in (1, 2, 3, 4, 5, 9)]
+    assert got == [2, 4, 6, 0, 3, -1]
+    assert g.take(8) == 1 and g.take(4) == -1
+    g.put(3)
+    assert g.take(13) == 3

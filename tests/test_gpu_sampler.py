@@ -150,6 +150,49 @@ def test_sample_points_eval_mode_and_member_rotation(setup):
         _state_close(p["next_observations"][0], want, f"trajectory {j}")
 
 
+def test_forward_blocked_matches_member_rows(setup):
+    """DeviceEnsemble.forward_blocked (lanes [g*Bq, (g+1)*Bq) through member g alone) equals
+    member g's rows of the all-member forward."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    dev = ens.engine
+    rs = np.random.RandomState(5)
+    for Bq in (128, 256):
+        B = 4 * Bq
+        ob = torch.from_numpy(0.5 * rs.randn(B, S)).to(DEV)
+        ac = torch.from_numpy(rs.randn(B, A)).to(DEV)
+        full = dev.forward_preds(ob, ac, B).clone()
+        blk = dev.forward_blocked(ob, ac, Bq).clone()
+        assert tuple(blk.shape) == (B, S)
+        for g in range(4):
+            np.testing.assert_allclose(blk[g * Bq:(g + 1) * Bq].cpu().numpy(),
+                                       full[g, g * Bq:(g + 1) * Bq].cpu().numpy(), rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError):
+        dev.forward_blocked(ob, ac, 100)
+
+
+def test_sample_points_member_blocked_matches_all_member_lanes(setup):
+    """member_blocked=True (the default: each lane steps through its trajectory's member only,
+    the lanes in M blocks of a multiple of 128) against every member on every lane: the same
+    trajectories (lengths, terminations, reset poses exact), states / actions / means within the
+    ensemble's fp32 tolerance; both against the oracle."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    from amp_extensions_amd.synthetic import reset_table
+    table = reset_table(256, S, 3)
+    table[::6, 2] = -2.0
+    table[1::4, 2] = -0.3
+    env = amx.BatchedSimEnv(ens, table, lanes=512, horizon=40, record_means=True)
+    W, N = 3, 700
+    a = amx.sample_points(env, pol, num_to_collect=N, base_seed=5, num_workers=W, member_blocked=False)
+    b = amx.sample_points(env, pol, num_to_collect=N, base_seed=5, num_workers=W, member_blocked=True)
+    _compare_paths(b, a)
+    ref = []
+    for i in range(W):
+        envr = R.SimEnvRef(ens_w, norms, horizon=40)
+        p, _ = R.get_samples(envr, pw, log_std, math.ceil(N / W), 12345 + 5 * i, table)
+        ref.extend(p)
+    _compare_paths(b, ref)
+
+
 def test_sample_points_pipelined_bit_identical(setup):
     """The pipelined chunk loop (chunk i queued before chunk i-1's done flags are read; lanes
     re-admitted one chunk later) returns the serial loop's paths bit for bit: the same

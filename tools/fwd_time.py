@@ -1,5 +1,9 @@
-"""Median HIP-event time of one f16x3 ensemble forward (assembly + 5 GEMM launches) at the given
-lane counts, plus the output layer alone (rocprof gives per-kernel times; this is the quick A/B).
+"""Time one f16x3 ensemble forward (assembly + 5 GEMM launches) at the given lane counts:
+every member on every lane (forward_preds) and, for lane counts that are multiples of 4 x 128,
+one member per lane (forward_blocked, the reference-semantics sampler's form).  Each form is
+timed eagerly (HIP events, median of 40) and as 20 forwards replayed back to back from one
+captured HIP graph (the sampler's chunk graphs), and the blocked preds are checked against the
+matching member's rows of forward_preds.
 usage: python tools/fwd_time.py [B ...]"""
 import os
 import sys
@@ -18,18 +22,60 @@ s, a, s2 = syn.offline(20000, S, A, 0)
 norms = get_transformations(*(torch.from_numpy(x).float() for x in (s, a, s2)))
 ctx = amx.AmxContext(S, A, n_models=4, hidden=512, n_hidden=4, feat_dim=512, device="cuda")
 ens = amx.DeviceEnsemble(ctx, init_ensemble_weights(S, A, [512] * 4, 4, base_seed=100), norms)
-for B in [int(x) for x in sys.argv[1:]] or [8192, 5120]:
-    rs = np.random.RandomState(1)
-    ob = torch.from_numpy(0.5 * rs.randn(B, S)).cuda()
-    ac = torch.from_numpy(rs.randn(B, A)).cuda()
+
+
+def eager(fn):
     for _ in range(10):
-        ens.forward_preds(ob, ac, B)
+        fn()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(40)]
     for e0, e1 in ev:
         e0.record()
-        ens.forward_preds(ob, ac, B)
+        fn()
         e1.record()
     torch.cuda.synchronize()
-    t = np.median([e0.elapsed_time(e1) * 1e3 for e0, e1 in ev])
-    print(f"lanes {B}: forward {t:.1f} us", flush=True)
+    return float(np.median([e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]))
+
+
+def graphed(fn, n=20):
+    fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        g.capture_begin()
+        for _ in range(n):
+            fn()
+        g.capture_end()
+    torch.cuda.current_stream().wait_stream(st)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(10):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3 / n)
+    return float(np.median(ts))
+
+
+M = ctx.M
+for B in [int(x) for x in sys.argv[1:]] or [512, 640, 1024, 2048]:
+    rs = np.random.RandomState(1)
+    ob = torch.from_numpy(0.5 * rs.randn(B, S)).cuda()
+    ac = torch.from_numpy(rs.randn(B, A)).cuda()
+    full = lambda: ens.forward_preds(ob, ac, B)
+    line = f"lanes {B:5d}: all members {eager(full):7.1f} us eager, {graphed(full):7.1f} us graphed"
+    if B % (M * 128) == 0:
+        Bq = B // M
+        blk = lambda: ens.forward_blocked(ob, ac, Bq)
+        ref = ens.forward_preds(ob, ac, B).clone()
+        got = ens.forward_blocked(ob, ac, Bq).clone()
+        want = torch.cat([ref[g, g * Bq:(g + 1) * Bq] for g in range(M)])
+        err = float(((got - want).abs().max() / want.abs().max()).item())
+        line += f" | one member {eager(blk):7.1f} us eager, {graphed(blk):7.1f} us graphed (max rel diff {err:.1e})"
+    print(line, flush=True)

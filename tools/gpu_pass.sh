@@ -13,9 +13,10 @@
 #   shares         the N = 8 / 4 per-rank share lines (5000 / 10000 samples)
 #   train          bench --mode train
 #   paths          bench --mode paths (the drop-in sample_points + relabel_paths)
+#   pathsprof      rocprofv3 --kernel-trace --stats of bench --mode paths (per-kernel totals vs the wall)
 #   configs        the other BASELINE configs (tools/gpu_configs.sh)
 #   timeline       per-launch timeline of the N = 8 share (tools/trace_timeline.py)
-#   py:SCRIPT[:ARGS]  python tools/SCRIPT ARGS (an A/B or timing tool), output to TAG_SCRIPT.txt
+#   py:SCRIPT[:ARGS]  python tools/SCRIPT ARGS (comma-separated; an A/B or timing tool), output to TAG_SCRIPT.txt
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd "$R" && mkdir -p gpurun_out
@@ -58,6 +59,13 @@ for step in "$@"; do
       timeout -k 10 300 python bench.py --mode paths --no-cpu-baseline > "${O}_bench_paths.json" 2>"${O}_paths.err" \
         || { echo "paths bench failed"; tail -5 "${O}_paths.err"; exit 1; }
       cut -c1-200 "${O}_bench_paths.json" ;;
+    pathsprof)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/${O}_pprof" -o run \
+          --output-format csv -- python "$R/bench.py" --mode paths --no-cpu-baseline > "$R/${O}_pprof.log" 2>&1 ) \
+        || { echo "rocprof (paths) failed"; tail -5 "${O}_pprof.log"; exit 1; }
+      cp "${O}_pprof/run_kernel_stats.csv" "${O}_paths_kernel_stats.csv" 2>/dev/null
+      python tools/trace_summary.py "${O}_pprof/run_kernel_trace.csv" > "${O}_paths_trace_summary.txt" 2>&1
+      head -24 "${O}_paths_trace_summary.txt" ;;
     configs)
       timeout -k 10 900 bash tools/gpu_configs.sh "${TAG}" > "${O}_configs.log" 2>&1 || { tail -20 "${O}_configs.log"; exit 1; }
       tail -8 "${O}_configs.log" ;;
@@ -68,7 +76,7 @@ for step in "$@"; do
       python tools/trace_timeline.py "${O}_tl/run_kernel_trace.csv" > "${O}_timeline_share.txt" 2>&1
       head -20 "${O}_timeline_share.txt" ;;
     py:*)
-      spec=${step#py:}; script=${spec%%:*}; rest=""; [[ "$spec" == *:* ]] && rest=${spec#*:}
+      spec=${step#py:}; script=${spec%%:*}; rest=""; [[ "$spec" == *:* ]] && rest=${spec#*:}; rest=${rest//,/ }
       timeout -k 10 600 python -u "tools/$script" $rest > "${O}_${script%.py}.txt" 2>&1 \
         || { tail -20 "${O}_${script%.py}.txt"; exit 1; }
       tail -15 "${O}_${script%.py}.txt" ;;
