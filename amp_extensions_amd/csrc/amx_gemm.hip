@@ -1438,8 +1438,13 @@ using H128x256 = TileH3<2, 4, 2, 2, 2, 2, true, true, true, 0, 0, true, true, tr
 // each lane runs its own member only): 128 x 64 hidden tiles (4 waves of 64 x 32) and 128 x 32
 // output tiles (4 waves of 32 x 32), stream-K over up to one workgroup per CU (small_plan) --
 // the weight panels read once per K range, 8-32 KB partial tiles per segment
+// 8 waves (two per SIMD: one wave's staging overlaps the other's MFMAs) when a member has one
+// 128-row tile (the member-blocked sampler's 512 lanes: forward 75 -> 68 us), else 4 waves
+// (256+ rows: 85 vs 90 us at 1024 lanes; profiles/r06y_small_tile_waves_ab.txt)
 using HS64 = TileH3<2, 2, 1, 1, 2, 2, true, true, true, 4, 2, true, true, true>;
+using HS64w8 = TileH3<4, 2, 1, 1, 2, 2, true, true, true, 2, 2, true, true, true>;
 using HS32 = TileH3<4, 1, 1, 1, 2, 2, true, true, true, 2, 2, true, true, true>;
+using HS32w8 = TileH3<8, 1, 1, 1, 2, 2, true, true, true, 1, 2, true, true, true>;
 
 using X128 = TileX6<2, 2, 2, 2>;        // 128x128, 4 waves of 64x64 (57 KB): 2 WGs / CU
 using X256 = TileX6<2, 4, 4, 2>;        // 256x256, 8 waves of 128x64 (115 KB): 1 WG / CU
@@ -1821,7 +1826,7 @@ extern "C" int amx_gemm_bias_act_h3(amx_ctx* ctx, int groups, int rows, int N, i
     if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
         ctx->split_floats >= (long long)tiles * ksplit * HS64::BM * HS64::BN) {
       a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
-      return launch_h3<EPI_BIAS_ACT, HS64>(a, s);
+      return rows == 128 ? launch_h3<EPI_BIAS_ACT, HS64w8>(a, s) : launch_h3<EPI_BIAS_ACT, HS64>(a, s);
     }
   }
   if (K % 32 == 0) return launch_h3<EPI_BIAS_ACT, H128k32>(a, s);
@@ -1901,7 +1906,7 @@ extern "C" int amx_gemm_out_unnorm_h3(amx_ctx* ctx, int groups, int rows, int n_
       if (tiles > 0 && ctx->split_scratch && ctx->split_cnt && ctx->split_ncnt >= tiles &&
           ctx->split_floats >= (long long)tiles * ksplit * HS32::BM * HS32::BN) {
         a.ksplit = ksplit; a.streamk = nwg; a.split_scratch = ctx->split_scratch; a.split_cnt = ctx->split_cnt;
-        return launch_h3<EPI_UNNORM, HS32>(a, s);
+        return rows == 128 ? launch_h3<EPI_UNNORM, HS32w8>(a, s) : launch_h3<EPI_UNNORM, HS32>(a, s);
       }
     }
     const int tiles = streamk_tiles(ctx, groups, rows, &nwg, &ksplit);

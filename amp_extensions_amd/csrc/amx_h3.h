@@ -244,8 +244,8 @@ __device__ __forceinline__ bool split_combine(const GemmArgs& a, f32x4 (&acc)[TL
   }
   __syncthreads();
   if (!*flag) return false;
-  if constexpr (TL::NT == 256 && MB * NB <= 8) {
-    // the small-row tiles (HS64 / HS32: up to 8 segments): the loads of four segments in flight
+  if constexpr (TL::NT <= 512 && MB * NB * TL::NT <= 2048) {
+    // the small-row tiles (HS64 / HS32, 4 or 8 waves): the loads of four segments in flight
     // per round trip (each a write-through partial in memory, ~1-2 us away), then the sums in K
     // order -- v = P0, v += P1, ... exactly as below
     f32x4 v[MB][NB];

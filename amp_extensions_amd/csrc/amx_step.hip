@@ -88,7 +88,12 @@ __global__ __launch_bounds__(256) void k_assemble(const T* __restrict__ ob, cons
     int e = (int)(mx >> 23) - 126;  // max|x0| < 2^e, clamped as the GEMM's exponents
     e = e < -100 ? -100 : (e > 100 ? 100 : e);
     const int v = lane == 0 ? e : -100;
-    for (int m = 0; m < M; ++m) row_exp[m * stride_rexp + lane * slot_stride + b] = v;
+    if (slot_stride < B) {  // member-blocked layout: row b % Bq of member block b / Bq, once
+      const int Bq = (int)slot_stride, g = b / Bq;
+      row_exp[g * stride_rexp + lane * slot_stride + (b - g * Bq)] = v;
+    } else {
+      for (int m = 0; m < M; ++m) row_exp[m * stride_rexp + lane * slot_stride + b] = v;
+    }
   }
 }
 
@@ -717,7 +722,12 @@ __device__ __forceinline__ void policy_core(const PolicyArgs& p, float* psm, int
   e = e < -100 ? -100 : (e > 100 ? 100 : e);
   for (int sl = c0; sl < p.n_slots; sl += 16) {
     const int v = sl == 0 ? e : -100;
-    for (int mm = 0; mm < p.M; ++mm) p.row_exp[mm * p.stride_rexp + sl * p.slot_stride + bb] = v;
+    if (p.slot_stride < p.B) {  // member-blocked layout (as k_assemble)
+      const int Bq = (int)p.slot_stride, g = bb / Bq;
+      p.row_exp[g * p.stride_rexp + sl * p.slot_stride + (bb - g * Bq)] = v;
+    } else {
+      for (int mm = 0; mm < p.M; ++mm) p.row_exp[mm * p.stride_rexp + sl * p.slot_stride + bb] = v;
+    }
   }
 }
 
@@ -825,6 +835,14 @@ inline dim3 lanes_grid(int B) { return dim3((unsigned)((B + 3) / 4)); }  // 4 la
 
 }  // namespace
 
+// the member-blocked row-exponent layout (slot_stride = Bq < B): B = M' x Bq lanes, M' <= M member
+// blocks, x0 written once (stride_m 0), member block g's slots at g * stride_rexp
+static bool blocked_rexp_ok(const amx_ctx* ctx, int B, long long stride_m, long long stride_rexp, long long slot_stride,
+                            int n_slots) {
+  return ctx && stride_m == 0 && slot_stride > 0 && B % slot_stride == 0 && B / slot_stride <= ctx->M &&
+         stride_rexp >= (long long)n_slots * slot_stride;
+}
+
 static int assemble(const char* fn, amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
                     long long stride_m, int ldk, int B, int* row_exp, long long stride_rexp, long long slot_stride,
                     int n_slots, void* stream) {
@@ -859,8 +877,9 @@ extern "C" int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act,
 extern "C" int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
                                        long long stride_m, int ldk, int B, int* row_exp, long long strideRexp,
                                        long long slot_stride, int n_slots, void* stream) {
-  AMX_CHECK_ARG(row_exp && n_slots >= 1 && n_slots <= 64 && slot_stride >= B &&
-                    (ctx == nullptr || ctx->M == 1 || strideRexp >= (long long)n_slots * slot_stride),
+  AMX_CHECK_ARG(row_exp && n_slots >= 1 && n_slots <= 64 &&
+                    (slot_stride >= B ? (ctx == nullptr || ctx->M == 1 || strideRexp >= (long long)n_slots * slot_stride)
+                                      : blocked_rexp_ok(ctx, B, stride_m, strideRexp, slot_stride, n_slots)),
                 "amx_assemble_input_rexp: row_exp=%p n_slots=%d slot_stride=%lld strideRexp=%lld B=%d", (void*)row_exp,
                 n_slots, slot_stride, strideRexp, B);
   return assemble("amx_assemble_input_rexp", ctx, ob, act, in_dtype, act_buf, stride_m, ldk, B, row_exp, strideRexp,
@@ -885,9 +904,11 @@ static int make_policy_args(const char* fn, amx_ctx* ctx, const double* ob, int 
   AMX_CHECK_ARG(!x0_buf || (ctx->have_norm && ldk >= ctx->k0_pad &&
                             (ctx->M == 1 || stride_m == 0 || stride_m >= (long long)ldk * B)),
                 "%s: fused assembly needs normalizers and ldk >= k0_pad, stride_m >= ldk*B", fn);
-  AMX_CHECK_ARG(!row_exp || (x0_buf && n_slots >= 1 && n_slots <= 64 && slot_stride >= B &&
-                             (ctx->M == 1 || stride_rexp >= (long long)n_slots * slot_stride)),
-                "%s: row_exp needs x0_buf, 1 <= n_slots <= 64, slot_stride >= B, stride_rexp", fn);
+  AMX_CHECK_ARG(!row_exp || (x0_buf && n_slots >= 1 && n_slots <= 64 &&
+                             (slot_stride >= B ? (ctx->M == 1 || stride_rexp >= (long long)n_slots * slot_stride)
+                                               : blocked_rexp_ok(ctx, B, stride_m, stride_rexp, slot_stride, n_slots))),
+                "%s: row_exp needs x0_buf, 1 <= n_slots <= 64, slot_stride >= B (or the member-blocked layout), "
+                "stride_rexp", fn);
   const size_t lds = pol_lds_bytes(ctx->S, H1, H2, ctx->A);
   AMX_CHECK_ARG(lds <= 160 * 1024, "%s: S/H too large for LDS staging (%zu B)", fn, lds);
   p.ob = ob; p.blob = blob; p.H1 = H1; p.H2 = H2;

@@ -253,27 +253,30 @@ class DeviceEnsemble:
 
     def workspace_blocked(self, Bq: int):
         """Buffers of the member-blocked forward (forward_blocked): M blocks of Bq lanes, lane
-        b = g * Bq + r runs member g only.  act [M * Bq][ldk] (one x0 per lane), preds
-        [M * Bq][S] (lane b's delta at row b), row exponents [M][slots][Bq]."""
+        b = g * Bq + r runs member g only.  act [1][M * Bq][ldk] (one x0 per lane), preds
+        [M * Bq][S] (lane b's delta at row b), row exponents [M][slots][Bq] (the member-blocked
+        exponent layout of amx_assemble_input_rexp / amx_policy_act: slot stride Bq)."""
         if Bq <= 0 or Bq % 128:
             raise ValueError(f"member blocks of {Bq} lanes: must be a positive multiple of 128")
         key = ("blocked", Bq)
         ws = self._ws.get(key)
         if ws is None:
             c = self.ctx
-            ws = dict(Bq=Bq, act=torch.zeros(c.M * Bq, c.ldk, dtype=torch.float32, device=c.device),
+            ws = dict(Bq=Bq, act=torch.zeros(1, c.M * Bq, c.ldk, dtype=torch.float32, device=c.device),
                       preds=torch.zeros(c.M * Bq, c.S, dtype=torch.float32, device=c.device),
                       rexp=torch.zeros(c.M, self.n_slots, Bq, dtype=torch.int32, device=c.device))
             self._ensure_split_workspace(Bq)
             self._ws[key] = ws
         return ws
 
-    def forward_blocked(self, ob: torch.Tensor, act: torch.Tensor, Bq: int) -> torch.Tensor:
+    def forward_blocked(self, ob: torch.Tensor, act: torch.Tensor, Bq: int, x0_ready: bool = False) -> torch.Tensor:
         """One member per lane: lanes [g * Bq, (g + 1) * Bq) through member g alone (SimEnv.step
         runs the lane's current member only, sim_env.py:154-157, with reset_counter % M choosing
         it at reset, :282-283).  A quarter of forward_preds' rows for the reference-semantics
         sampler, whose lanes are placed in the block of their trajectory's member.  Returns
-        preds [M * Bq][S] (view of the workspace).  f16x3 only."""
+        preds [M * Bq][S] (view of the workspace).  f16x3 only.  `x0_ready`: the policy launch
+        already wrote x0 and its exponents into workspace_blocked(Bq) (amx_policy_act's fused
+        assembly in the member-blocked layout)."""
         if self.W2 is None:
             raise ValueError("forward_blocked needs the f16x3 GEMM")
         c = self.ctx
@@ -289,11 +292,10 @@ class DeviceEnsemble:
         buf, preds, rexp = ws["act"], ws["preds"], ws["rexp"]
         s = c.stream
         dt = N.AMX_IN_F64 if ob.dtype == torch.float64 else N.AMX_IN_F32
-        N.check(c.lib.amx_assemble_input(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), 0, c.ldk, B, s),
-                "amx_assemble_input")
         sA, sR, L = Bq * c.ldk, self.n_slots * Bq, c.L
-        N.check(c.lib.amx_row_exponents(c.h, c.M, Bq, c.k0_pad, buf.data_ptr(), c.ldk, sA, rexp.data_ptr(), sR,
-                                        self.n_slots, s), "amx_row_exponents")
+        if not x0_ready:  # x0 once per lane + slot 0 of its member block's exponents (slot stride Bq)
+            N.check(c.lib.amx_assemble_input_rexp(c.h, ob.data_ptr(), act.data_ptr(), dt, buf.data_ptr(), 0, c.ldk, B,
+                                                  rexp.data_ptr(), sR, Bq, self.n_slots, s), "amx_assemble_input_rexp")
         for i in range(L):
             K = c.k0_pad + i * c.Hp
             N.check(c.lib.amx_gemm_bias_act_h3(c.h, c.M, Bq, c.Hp, K, buf.data_ptr(), c.ldk, sA, self.W2[i].data_ptr(),

@@ -276,7 +276,12 @@ class RolloutEngine:
             # f16x3 with the shared x0 slice: the policy launch also writes x0 (once, model 0's
             # rows) and its row exponents, as amx_assemble_input_rexp (one launch fewer per step)
             fuse_x0 = self.fuse_assembly and self.ens.W2 is not None and self.ens.shared_x0
-            ws = self.ens.workspace(B) if fuse_x0 else None
+            if not fuse_x0:
+                ws = None
+            elif self.member_blocks:  # (x0 + exponents in the member-blocked layout)
+                ws = self.ens.workspace_blocked(self.member_blocks)
+            else:
+                ws = self.ens.workspace(B)
             self.policy.act(ob, B, act, t if self._capturing else self.step_counter, noise=noise,
                             eval_mode=self.eval_mode, mean_out=None if self.means is None else self.means[t],
                             counter_dev=self.dev_step if self._capturing else None,
@@ -284,9 +289,9 @@ class RolloutEngine:
                             shared_x0=fuse_x0)
             x0_ready = fuse_x0
         if self.member_blocks:
-            if x0_ready or self.B != self.ctx.M * self.member_blocks:
-                raise ValueError("member-blocked stepping needs M * member_blocks lanes and no fused x0")
-            return t, src, self.ens.forward_blocked(ob, act, self.member_blocks)
+            if self.B != self.ctx.M * self.member_blocks:
+                raise ValueError("member-blocked stepping needs M * member_blocks lanes")
+            return t, src, self.ens.forward_blocked(ob, act, self.member_blocks, x0_ready=x0_ready)
         preds = self.ens.forward_preds(ob, act, B, x0_ready=x0_ready)
         return t, src, preds
 

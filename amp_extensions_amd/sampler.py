@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import gc
 import math
+import threading
 import time
 import weakref
 
@@ -231,6 +232,8 @@ class _HostNoise:
         pin = torch.cuda.is_available()
         self.bufs = [torch.zeros(K, L, A, dtype=torch.float64, pin_memory=pin) for _ in range(2)]
         self.cur = 0
+        self.ahead = -1  # buffer already holding the continuing lanes' next draws (draw_async)
+        self._thread, self._err = None, None
 
     def seed(self, lanes: np.ndarray, seeds: np.ndarray) -> None:
         sl = np.ascontiguousarray(lanes, np.int32)
@@ -248,6 +251,30 @@ class _HostNoise:
                                              self.A, buf.data_ptr(), self.L * self.A, self.A),
                 "amx_mt_policy_noise")
         return buf
+
+    # background draws (the pipelined collector): the next chunk's noise of the lanes in flight,
+    # drawn on a host thread (the ctypes call releases the GIL) while the main thread reads the
+    # previous chunk and admits; join() before any seed or draw touches the generator states
+    def draw_async(self, lanes: np.ndarray, which: int) -> None:
+        self.join()
+        self._err = None
+
+        def run():
+            try:
+                self.draw(lanes, self.bufs[which])
+            except BaseException as e:  # re-raised by join()
+                self._err = e
+        self._thread = threading.Thread(target=run, daemon=True)
+        self._thread.start()
+        self.ahead = which
+
+    def join(self) -> None:
+        th = getattr(self, "_thread", None)
+        if th is not None:
+            th.join()
+            self._thread = None
+            if self._err is not None:
+                raise self._err
 
 
 class _ChunkGraph:
@@ -318,7 +345,7 @@ def _chunk_graph(eng: RolloutEngine, K: int, noise_dev, eval_mode: bool) -> _Chu
     them in place), the noise buffer, eval_mode and, for device-drawn noise, the policy seed."""
     pol = eng.policy
     key = (K, 0 if noise_dev is None else noise_dev.data_ptr(), bool(eval_mode), id(pol), pol.blob.data_ptr(),
-           pol.noise_scale.data_ptr(), pol.H1, pol.H2, pol.seed if noise_dev is None else 0)
+           pol.noise_scale.data_ptr(), pol.H1, pol.H2, pol.seed if noise_dev is None else 0, bool(eng.fuse_assembly))
     cache = eng.__dict__.setdefault("_chunk_graphs", {})
     g = cache.get(key)
     if g is None:
@@ -415,6 +442,14 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
             elif len(trs) == quota and all(tr.ended for tr in trs):
                 done_w[w] = True
         new = []
+        # per worker: the lower bound (lengths so far) and the estimate, summed once per chunk
+        # and extended as trajectories are admitted (a new one adds 0 and lhat)
+        lbs, ests = [0] * W, [0.0] * W
+        if mode == "samples":
+            for w in range(W):
+                if not done_w[w]:
+                    lbs[w] = sum(tr.length for tr in adm[w])
+                    ests[w] = sum(tr.length if tr.ended else max(tr.length, lhat) for tr in adm[w])
         progress = True
         while free and progress:
             progress = False
@@ -422,12 +457,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
                 if not free or done_w[w]:
                     continue
                 trs = adm[w]
-                if mode == "samples":
-                    lb = sum(tr.length for tr in trs)
-                    est = sum(tr.length if tr.ended else max(tr.length, lhat) for tr in trs)
-                    ok = lb < quota and est < quota
-                else:
-                    ok = len(trs) < quota
+                ok = (lbs[w] < quota and ests[w] < quota) if mode == "samples" else len(trs) < quota
                 if ok:
                     j = next_j[w]
                     lane = free.take(j)
@@ -439,6 +469,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
                     lane_tr[tr.lane] = tr
                     trs.append(tr)
                     new.append(tr)
+                    ests[w] += max(0, lhat)
                     progress = True
         active = np.array([b for b in range(L) if lane_tr[b] is not None], np.int64)
         if active.size == 0:
@@ -577,7 +608,8 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         rh = torch.zeros(L, dtype=torch.float64 if motion is not None else torch.int32, pin_memory=pin)
         dh = torch.zeros(K, L, dtype=torch.uint8, pin_memory=pin)
         fh = torch.zeros(K * L, dtype=torch.int64, pin_memory=pin)  # compaction indices (async upload)
-        stage.append((mh, ch, rh, dh, torch.cuda.Event() if pin else None, fh))
+        stage.append((mh, ch, rh, dh, torch.cuda.Event() if pin else None, fh,
+                      torch.empty(K * L, dtype=torch.int64, device=dev)))
     mask_dev = torch.empty(L, dtype=torch.uint8, device=dev)
     counts_dev = torch.empty(L, dtype=torch.int32, device=dev)
     rows_dev = torch.empty(L, dtype=stage[0][2].dtype, device=dev)
@@ -610,9 +642,10 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         step_of = np.arange(int(n.sum())) - np.repeat(starts, n)
         flat = step_of * L + np.repeat(lanes, n)
         # pinned + non_blocking: a pageable upload would wait for the chunk queued behind this one
-        fh = stage[si][5]
+        fh, fd = stage[si][5], stage[si][6]
         fh.numpy()[:flat.size] = flat
-        base = store.append_from(ring.slots[si], fh[:flat.size].to(dev, non_blocking=True))
+        fd[:flat.size].copy_(fh[:flat.size], non_blocking=True)
+        base = store.append_from(ring.slots[si], fd[:flat.size])
         for i, (b, tr) in enumerate(live):
             tr.segs.append((base + int(starts[i]), int(n[i])))
             tr.length += int(n[i])
@@ -643,6 +676,14 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
             elif len(trs) == quota and all(tr.ended for tr in trs):
                 done_w[w] = True
         new = []
+        # per worker: the lower bound (lengths so far) and the estimate, summed once per chunk
+        # and extended as trajectories are admitted (a new one adds 0 and lhat)
+        lbs, ests = [0] * W, [0.0] * W
+        if mode == "samples":
+            for w in range(W):
+                if not done_w[w]:
+                    lbs[w] = sum(tr.length for tr in adm[w])
+                    ests[w] = sum(tr.length if tr.ended else max(tr.length, lhat) for tr in adm[w])
         progress = True
         while free and progress:
             progress = False
@@ -650,12 +691,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
                 if not free or done_w[w]:
                     continue
                 trs = adm[w]
-                if mode == "samples":
-                    lb = sum(tr.length for tr in trs)
-                    est = sum(tr.length if tr.ended else max(tr.length, lhat) for tr in trs)
-                    ok = lb < quota and est < quota
-                else:
-                    ok = len(trs) < quota
+                ok = (lbs[w] < quota and ests[w] < quota) if mode == "samples" else len(trs) < quota
                 if ok:
                     j = next_j[w]
                     lane = free.take(j)
@@ -667,6 +703,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
                     lane_tr[tr.lane] = tr
                     trs.append(tr)
                     new.append(tr)
+                    ests[w] += max(0, lhat)
                     progress = True
         active = np.array([b for b in range(L) if lane_tr[b] is not None], np.int64)
         if active.size == 0:
@@ -679,7 +716,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         if chunks > budget:
             raise RuntimeError("sample_points: step budget exhausted (trajectories longer than the horizon?)")
         si = chunks & 1
-        mask_h, counts_h, rows_h, done_h, ev, _ = stage[si]
+        mask_h, counts_h, rows_h, done_h, ev = stage[si][:5]
         mask_np, counts_np, rows_np = mask_h.numpy(), counts_h.numpy(), rows_h.numpy()
         eng.begin_rollout()
         mask_np.fill(1)
@@ -699,10 +736,18 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
             rows_dev.copy_(rows_h, non_blocking=True)
         eng.reset_lanes(mask_dev, rows_dev if rng == "reference" else None)
         if hn is not None:
-            if new:
-                hn.seed(new_lanes, np.array([tr.seed for tr in new]))  # np.random.seed (sampler.py:39)
             buf = hn.bufs[si]
-            hn.draw(active, buf)  # the next K draws of every lane in flight (finished ones idle)
+            if hn.ahead == si:  # the lanes of the previous chunk were drawn in the background
+                hn.join()
+                hn.ahead = -1
+                if new:
+                    hn.seed(new_lanes, np.array([tr.seed for tr in new]))  # np.random.seed (sampler.py:39)
+                    hn.draw(new_lanes, buf)
+            else:
+                hn.join()
+                if new:
+                    hn.seed(new_lanes, np.array([tr.seed for tr in new]))
+                hn.draw(active, buf)  # the next K draws of every lane in flight (finished ones idle)
             noise_dev.copy_(buf, non_blocking=True)
         # (the first chunk of a new shape allocates the workspaces: captured from the second on)
         if graph and chunk_graph is None and (chunks >= 2 or "_chunk_graphs" in eng.__dict__):
@@ -720,6 +765,13 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         if pending is not None:
             process(pending)
         pending = (si, launched)
+        if hn is not None:
+            # the next chunk's draws of this chunk's lanes (buffer si ^ 1: chunk i - 1's upload
+            # is complete, process() waited for it); a lane that ends or is dropped is re-seeded
+            # and re-drawn if admitted again, so its surplus draws are never used
+            hn.draw_async(active, si ^ 1)
+    if hn is not None:
+        hn.join()
     trajs = [tr for w in range(W) for tr in adm[w]]
     if not trajs:
         return [], 0
@@ -771,7 +823,10 @@ def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_work
     M = src.ctx.M
     Bq = 0
     if member_blocked and M >= 2 and src.ens.W2 is not None:
-        Bq = math.ceil(math.ceil(need / M) / 128) * 128  # member blocks of a multiple of 128 lanes
+        # member blocks of a multiple of 128 lanes, rounded down: the lanes in flight at once stay
+        # well below the speculative estimate (~125 of 544 at 40 000 samples), and a member's
+        # single 128-row tile runs the 8-wave small-row GEMM (68 vs 85 us per forward at 256)
+        Bq = max(128, math.ceil(need / M) // 128 * 128)
         while Bq > 128 and M * Bq > max(src.B, M * 128):
             Bq -= 128
         lanes = M * Bq

@@ -104,7 +104,10 @@ int amx_assemble_input(amx_ctx* ctx, const void* ob, const void* act, int in_dty
  * (row_exp[m][slot][b], slot stride slot_stride >= B, model stride strideRexp; the layout of
  * amx_row_exponents) from max |x0| and resets slots 1..n_slots-1, for rows b < B.
  * stride_m = 0: x0 is written once (model 0's rows) and the f16x3 GEMMs read it for every
- * model (their k_shared); the exponent slots are still written for every model. */
+ * model (their k_shared); the exponent slots are still written for every model.
+ * Member-blocked layout (slot_stride = Bq < B, stride_m = 0, B = M' x Bq with M' <= M): lane b
+ * belongs to member block g = b / Bq (the sampler's one-member-per-lane forward), its x0 is row b
+ * and its exponents go to row b % Bq of block g's slots only (g * strideRexp + slot * Bq). */
 int amx_assemble_input_rexp(amx_ctx* ctx, const void* ob, const void* act, int in_dtype, float* act_buf,
                             long long stride_m, int ldk, int B, int* row_exp, long long strideRexp,
                             long long slot_stride, int n_slots, void* stream);
@@ -436,7 +439,8 @@ int amx_reset_lanes(amx_ctx* ctx, const uint8_t* mask, const double* table, int 
  * AMX_IN_F64) for the same lanes: x0 = [(float(ob)-mu_s)/sd_s, (float(act)-mu_a)/sd_a, 0]
  * written to every model's activation row (stride_m, ldk as in amx_assemble_input; stride_m
  * 0: once, model 0's rows, the f16x3 GEMMs' shared x0 slice); row_exp (nullable, needs x0_buf)
- * additionally writes the f16x3 row-exponent slots exactly as amx_assemble_input_rexp. */
+ * additionally writes the f16x3 row-exponent slots exactly as amx_assemble_input_rexp (including
+ * its member-blocked layout, slot_stride < B). */
 int amx_policy_act(amx_ctx* ctx, const double* ob, int B, const float* blob, int H1, int H2,
                    const double* noise_scale, const double* noise, uint64_t seed, uint64_t counter,
                    int eval_mode, double* act, float* mean, float* x0_buf, long long stride_m, int ldk,

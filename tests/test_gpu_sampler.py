@@ -193,6 +193,35 @@ def test_sample_points_member_blocked_matches_all_member_lanes(setup):
     _compare_paths(b, ref)
 
 
+def test_sample_points_member_blocked_fused_assembly_bit_identical(setup):
+    """Member-blocked lanes with the policy launch writing x0 and its exponents in the blocked
+    layout (amx_policy_act's fused assembly, slot stride Bq) against the separate assembly
+    launch: the same paths bit for bit."""
+    amx, ens, ens_w, norms, pw, log_std, pol = setup
+    from amp_extensions_amd.synthetic import reset_table
+    table = reset_table(256, S, 4)
+    table[::5, 2] = -2.0
+    table[1::4, 2] = -0.3
+    env = amx.BatchedSimEnv(ens, table, lanes=512, horizon=30, record_means=True)
+    kw = dict(num_to_collect=600, base_seed=4, num_workers=3)
+    a = amx.sample_points(env, pol, **kw)
+    engines = list(env.engine.__dict__["_sampler_engines"].values())
+    assert any(e.member_blocks for e in engines)
+    before = {id(e): e.fuse_assembly for e in engines}
+    for e in engines:
+        e.fuse_assembly = not e.fuse_assembly
+    try:
+        b = amx.sample_points(env, pol, **kw)
+    finally:
+        for e in engines:
+            e.fuse_assembly = before[id(e)]
+    assert len(a) == len(b)
+    for pa, pb in zip(a, b):
+        for k in ("observations", "next_observations", "actions"):
+            np.testing.assert_array_equal(pa[k], pb[k])
+        np.testing.assert_array_equal(pa["agent_infos"]["mean"], pb["agent_infos"]["mean"])
+
+
 def test_sample_points_pipelined_bit_identical(setup):
     """The pipelined chunk loop (chunk i queued before chunk i-1's done flags are read; lanes
     re-admitted one chunk later) returns the serial loop's paths bit for bit: the same

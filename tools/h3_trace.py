@@ -19,7 +19,8 @@ from amp_extensions_amd.datasets import get_transformations  # noqa: E402
 from amp_extensions_amd.ensemble import init_ensemble_weights  # noqa: E402
 
 S, A = 197, 36
-lanes = [int(x) for x in sys.argv[1:]] or [5120, 8192]
+# "b512": 512 lanes through the member-blocked forward (forward_blocked, 128 rows per member)
+lanes = [x for x in sys.argv[1:]] or ["5120", "8192"]
 s, a, s2 = syn.offline(20000, S, A, 0)
 norms = get_transformations(*(torch.from_numpy(x).float() for x in (s, a, s2)))
 ctx = amx.AmxContext(S, A, n_models=4, hidden=512, n_hidden=4, feat_dim=512, device="cuda")
@@ -30,16 +31,21 @@ if not hasattr(lib, "amx_h3_trace_read"):
 lib.amx_h3_trace_read.argtypes = [ctypes.c_void_p]
 buf = np.zeros((5, 1024, 8), np.uint64)
 names = ["L0", "L1", "L2", "L3", "out"]
-for B in lanes:
+for spec in lanes:
+    blocked = spec.startswith("b")
+    B = int(spec.lstrip("b"))
     rs = np.random.RandomState(B)
     ob = torch.from_numpy(0.5 * rs.randn(B, S)).cuda()
     ac = torch.from_numpy(rs.randn(B, A)).cuda()
     for rep in range(6):
         buf[:] = 0
-        ens.forward_preds(ob, ac, B)
+        if blocked:
+            ens.forward_blocked(ob, ac, B // 4)
+        else:
+            ens.forward_preds(ob, ac, B)
         torch.cuda.synchronize()
         assert lib.amx_h3_trace_read(buf.ctypes.data) == 0
-    print(f"lanes {B}: medians over workgroups, us (100 MHz stamps; last of 6 forwards)")
+    print(f"lanes {spec}: medians over workgroups, us (100 MHz stamps; last of 6 forwards)")
     print(f"  {'layer':5s} {'wgs':>4s} {'start':>7s} {'rexp':>6s} {'prolog':>6s} {'kloop':>7s} {'epi':>6s} "
           f"{'drain':>6s} | {'span':>7s} {'entry spread':>12s} {'gap->next':>9s}")
     t0 = None

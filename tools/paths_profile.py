@@ -1,5 +1,7 @@
 """cProfile of the reference-semantics path (bench.py --mode paths): one warm sample_points +
-relabel_paths at the bench shape, then a profiled one.  usage: python tools/paths_profile.py [W] [chunk]"""
+relabel_paths at the bench shape, then a profiled one.
+usage: python tools/paths_profile.py [W] [chunk] [fuse|nofuse]  (fuse: the sampler engine's policy
+launch writes the ensemble input, RolloutEngine.fuse_assembly)"""
 import cProfile
 import io
 import os
@@ -49,6 +51,11 @@ def once(i):
 
 
 once(1)
+if len(sys.argv) > 3:
+    for e in eng.__dict__.get("_sampler_engines", {}).values():
+        e.fuse_assembly = sys.argv[3] == "fuse"
+    print(f"fuse_assembly = {sys.argv[3] == 'fuse'}")
+once(2)
 once(2)
 pr = cProfile.Profile()
 pr.enable()
