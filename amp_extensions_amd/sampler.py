@@ -227,10 +227,11 @@ class _HostNoise:
     def __init__(self, lib, L: int, K: int, A: int):
         self.lib, self.L, self.K, self.A = lib, L, K, A
         self.states = np.zeros((L, N.AMX_MT_STATE_BYTES), np.uint8)
-        # two pinned buffers: the next chunk's noise is drawn into one while the other's upload
-        # and the current chunk's steps run on the GPU
+        # pinned buffers: the next chunk's noise is drawn into one while another's upload and the
+        # current chunk's steps run on the GPU (the pipelined collector rotates three: chunk
+        # c + 1's draw starts before chunk c - 1 has been read back)
         pin = torch.cuda.is_available()
-        self.bufs = [torch.zeros(K, L, A, dtype=torch.float64, pin_memory=pin) for _ in range(2)]
+        self.bufs = [torch.zeros(K, L, A, dtype=torch.float64, pin_memory=pin) for _ in range(3)]
         self.cur = 0
         self.ahead = -1  # buffer already holding the continuing lanes' next draws (draw_async)
         self._thread, self._err = None, None
@@ -736,8 +737,9 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
             rows_dev.copy_(rows_h, non_blocking=True)
         eng.reset_lanes(mask_dev, rows_dev if rng == "reference" else None)
         if hn is not None:
-            buf = hn.bufs[si]
-            if hn.ahead == si:  # the lanes of the previous chunk were drawn in the background
+            nb = chunks % 3
+            buf = hn.bufs[nb]
+            if hn.ahead == nb:  # the lanes of the previous chunk were drawn in the background
                 hn.join()
                 hn.ahead = -1
                 if new:
@@ -761,15 +763,16 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         done_h.copy_(eng.done[:K], non_blocking=True)
         if ev is not None:
             ev.record()
+        if hn is not None:
+            # the next chunk's draws of this chunk's lanes, on a host thread while chunk c - 1 is
+            # read back (buffer (c + 1) % 3 last served chunk c - 2, whose upload completed before
+            # process() returned for it); a lane that ends or is dropped is re-seeded and re-drawn
+            # if admitted again, so its surplus draws are never used
+            hn.draw_async(active, (chunks + 1) % 3)
         launched = [(int(b), lane_tr[b]) for b in active.tolist()]
         if pending is not None:
             process(pending)
         pending = (si, launched)
-        if hn is not None:
-            # the next chunk's draws of this chunk's lanes (buffer si ^ 1: chunk i - 1's upload
-            # is complete, process() waited for it); a lane that ends or is dropped is re-seeded
-            # and re-drawn if admitted again, so its surplus draws are never used
-            hn.draw_async(active, si ^ 1)
     if hn is not None:
         hn.join()
     trajs = [tr for w in range(W) for tr in adm[w]]
