@@ -15,6 +15,30 @@ from .costs import GAILCost, RBFLinearCost, cost_input, device_discrepancy
 from .dist import feature_mean
 
 
+def _device_rows(paths, key: str, dev):
+    """The paths' `key` rows as the device tensor sample_points already holds (sampler._last_rows)
+    when the paths' arrays are consecutive views of its read-only host copy; else None."""
+    from .sampler import _last_rows
+    ent = _last_rows.get(key)
+    if ent is None or ent[1].device != dev:
+        return None
+    base, rows = ent
+    if base.flags.writeable:
+        return None
+    arrs = [p[key] for p in paths]
+    if not arrs or any(a.base is not base for a in arrs):
+        return None
+    row = base.strides[0]
+    start = arrs[0].__array_interface__["data"][0]
+    off = start
+    for a in arrs:
+        if a.__array_interface__["data"][0] != off or a.shape[1:] != base.shape[1:] or a.flags.writeable:
+            return None
+        off += a.shape[0] * row
+    r0 = (start - base.__array_interface__["data"][0]) // row
+    return rows[r0:r0 + (off - start) // row]
+
+
 def _rows(paths, key: str) -> np.ndarray:
     """np.concatenate([p[key] for p in paths]) -- without the copy when the paths' arrays are
     consecutive views of one buffer (sample_points returns them so)."""
@@ -35,6 +59,42 @@ def _rows(paths, key: str) -> np.ndarray:
     return np.concatenate(arrs)
 
 
+_copy_streams: dict = {}
+
+
+def _upload(paths, dev):
+    """The paths' float64 rows on the device as float32 (the reference's .float() of its
+    tensors), copied on a side stream: actions and observations first (the disagreement's
+    inputs), then the next states, which `next_rows()` hands to the current stream when the
+    caller needs them.  The sampler's paths are views of one pinned buffer, so the copies are
+    asynchronous DMA; other arrays are copied synchronously by torch.  Paths that are views of
+    the last sample_points call's read-only host arrays are read from its device rows instead."""
+    main = torch.cuda.current_stream(dev)
+    d = [_device_rows(paths, k, dev) for k in ("observations", "actions", "next_observations")]
+    if all(x is not None for x in d):  # sample_points' own device rows: no upload
+        return d[0].float(), d[1].float(), lambda: d[2].float()
+    cs = _copy_streams.get(dev)
+    if cs is None:
+        cs = _copy_streams[dev] = torch.cuda.Stream(dev)
+    cs.wait_stream(main)
+    with torch.cuda.stream(cs):
+        a64 = torch.from_numpy(_rows(paths, "actions")).to(dev, non_blocking=True)
+        o64 = torch.from_numpy(_rows(paths, "observations")).to(dev, non_blocking=True)
+        e_sa = torch.cuda.Event()
+        e_sa.record(cs)
+        n64 = torch.from_numpy(_rows(paths, "next_observations")).to(dev, non_blocking=True)
+        e_n = torch.cuda.Event()
+        e_n.record(cs)
+    main.wait_event(e_sa)
+    for t in (a64, o64, n64):
+        t.record_stream(main)  # (allocated on the copy stream, consumed on this one)
+
+    def next_rows():
+        main.wait_event(e_n)
+        return n64.float()
+    return o64.float(), a64.float(), next_rows
+
+
 def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", allreduce=None) -> dict:
     """`cost_input_type` builds the fit_cost input ('ss' or 'sa', batch_reinforce.py:107-110);
     the per-sample rewards use reward_func's own input_type (get_bonus_costs).  With
@@ -46,13 +106,14 @@ def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", all
         raise NotImplementedError(f"cost_input_type {cost_input_type!r}: batch_reinforce builds only 'ss' / 'sa'")
     dev = reward_func.ctx.device
     lens = [len(p["observations"]) for p in paths]
-    obs = torch.from_numpy(_rows(paths, "observations")).to(dev).float()
-    nxt = torch.from_numpy(_rows(paths, "next_observations")).to(dev).float()
-    act = torch.from_numpy(_rows(paths, "actions")).to(dev).float()
+    obs, act, next_rows = _upload(paths, dev)
     bonus_v = ipm_v = None
     if isinstance(reward_func, RBFLinearCost):
         if ensemble is None:
             raise ValueError("the MMD relabel needs the ensemble (batch_reinforce.py:147 asserts a GAIL cost)")
+        # the disagreement first: its ensemble forward runs while the next states upload
+        disc = device_discrepancy(ensemble, obs, act)
+        nxt = next_rows()
         x_fit = cost_input(cost_input_type, obs, act, nxt)
         phi_fit, tot = reward_func.map.embed(x_fit)
         mean = feature_mean(tot, float(x_fit.shape[0]), allreduce if allreduce is not None else (lambda t: t))
@@ -61,10 +122,10 @@ def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", all
             phi = phi_fit
         else:
             phi = reward_func.get_rep(cost_input(reward_func.input_type, obs, act, nxt, reward_func.motion))
-        disc = device_discrepancy(ensemble, obs, act)
         reward, ipm, wb = reward_func._values(phi, disc, ensemble.threshold)
         bonus_v, ipm_v = wb.cpu().numpy(), ipm.cpu().numpy()
     elif isinstance(reward_func, GAILCost):
+        nxt = next_rows()
         # the reference scores [s, s'] here (:152-165); an AMP-feature discriminator scores AMP(s, s')
         x_ss = (cost_input("amp", obs, act, nxt, reward_func.motion) if reward_func.input_type == "amp"
                 else torch.cat([obs, nxt], dim=-1))

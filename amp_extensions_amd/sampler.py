@@ -326,10 +326,19 @@ class _ChunkGraph:
         self.eng._graph_ahead = True
 
 
+# The device rows of the last sample_points call, in path order, beside the read-only host
+# arrays they were copied to: relabel_paths (relabel.py:_device_rows) reads them instead of
+# uploading the same bytes back when its paths are views of those host arrays.  One entry (the
+# newest call); the host arrays are read-only, so the two copies cannot diverge.
+_last_rows: dict = {}
+
+
 def _to_host_path_order(perm: torch.Tensor, arrays) -> list:
     """The store's rows gathered into path order on the device, then ONE copy each into pinned
     host memory (2-4x the pageable .cpu() rate; torch's pinned-block cache reuses the blocks of
-    paths the caller has dropped).  The returned numpy arrays keep their pinned tensors alive."""
+    paths the caller has dropped).  The returned numpy arrays keep their pinned tensors alive and
+    are read-only (the reference's own code only reads the paths' arrays); the device rows of
+    (observations, next observations, actions) stay registered in _last_rows."""
     sel = [x.index_select(0, perm) for x in arrays]
     pin = torch.cuda.is_available()
     host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=pin) for t in sel]
@@ -337,7 +346,12 @@ def _to_host_path_order(perm: torch.Tensor, arrays) -> list:
         h.copy_(t, non_blocking=pin)
     if pin:
         torch.cuda.current_stream(sel[0].device).synchronize()
-    return [h.numpy() for h in host]
+    out = [h.numpy() for h in host]
+    for a in out:
+        a.flags.writeable = False
+    _last_rows.clear()
+    _last_rows.update(observations=(out[0], sel[0]), next_observations=(out[1], sel[1]), actions=(out[2], sel[2]))
+    return out
 
 
 def _chunk_graph(eng: RolloutEngine, K: int, noise_dev, eval_mode: bool) -> _ChunkGraph:
