@@ -85,7 +85,9 @@ class RolloutEngine:
         z = lambda *shape, dt=torch.float32: torch.zeros(*shape, dtype=dt, device=dev)
         # trajectory buffers of one rollout (obs[K] carries the lane state into the next rollout)
         self.obs = z(K + 1, B, S, dt=torch.float64)
-        self.next_obs = z(K, B, S, dt=torch.float64)
+        # gym semantics (auto_reset off: the caller resets): the next observation IS the next
+        # step's input, so next_obs[t] is obs[t + 1] itself (no per-step copy)
+        self.next_obs = z(K, B, S, dt=torch.float64) if auto_reset else self.obs[1:]
         self.acts = z(K, B, A, dt=torch.float64)
         self.done = z(K, B, dt=torch.uint8)
         self.disc = z(K, Bp)
@@ -368,7 +370,7 @@ class RolloutEngine:
                                           ob_next.data_ptr(), self.obs[t + 1].data_ptr(), self.num_steps.data_ptr(),
                                           self.model_idx.data_ptr(), self.reset_count.data_ptr(),
                                           self.reset_rows[t].data_ptr(), B, s), "amx_reset_lanes")
-        else:  # gym semantics: the caller resets (SimEnv facade)
+        elif ob_next.data_ptr() != self.obs[t + 1].data_ptr():  # gym semantics: the caller resets
             self.obs[t + 1].copy_(ob_next)
         self.t += 1
         self.step_counter += 1
