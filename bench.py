@@ -598,8 +598,11 @@ def main():
     flops_per_fwd = ens.mlp_flops_per_sample() * B
     if args.mode == "paths":
         # the sampler's forwards run at its own lane counts (chunks of idle-padded lanes): count
-        # the algorithmic FLOPs of the samples it returned over the forwards' measured time
-        flops_per_fwd = ens.mlp_flops_per_sample() * samples / max(n_fwd, 1)
+        # the algorithmic FLOPs of the samples it returned over the forwards' measured time --
+        # one member per sample while sampling (member-blocked lanes: SimEnv.step's one model;
+        # every member without blocking) plus every member in the relabel's disagreement
+        sampling = 1.0 / ctx.M if (args.gemm == "f16x3" and ctx.M >= 2) else 1.0
+        flops_per_fwd = ens.mlp_flops_per_sample() * samples * (sampling + 1.0) / max(n_fwd, 1)
     achieved_tflops = flops_per_fwd * n_fwd / (gemm_ms * 1e-3) / 1e12
     ens.gemm_events = None
 
