@@ -138,15 +138,19 @@ def relabel_paths(paths, reward_func, ensemble, cost_input_type: str = "ss", all
     else:
         raise TypeError("reward_func must be an RBFLinearCost or GAILCost")
     rew = reward.cpu().numpy()
+    if bonus_v is not None and lens:
+        # the per-path sums of batch_reinforce.py:135-136 for all paths in one pass (float32
+        # segment sums: np.sum's pairwise order differs in the last bits, inside the values' own
+        # fp32 tolerance)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]])
+        isums = -np.add.reduceat(bonus_v, starts)
+        esums = -np.add.reduceat(ipm_v, starts)
+        infos["int"] = list(isums)
+        infos["ext"] = list(esums)
+        infos["reward"] = list(esums + isums)
+        infos["ep_len"] = list(lens)
     o = 0
     for p, T in zip(paths, lens):
-        if bonus_v is not None:
-            isum = -np.sum(bonus_v[o:o + T])    # batch_reinforce.py:135
-            esum = -np.sum(ipm_v[o:o + T])      # :136
-            infos["int"].append(isum)
-            infos["ext"].append(esum)
-            infos["reward"].append(esum + isum)
-            infos["ep_len"].append(T)
         p["rewards"] = rew[o:o + T].copy()  # :144 (reward = -cost)
         o += T
     if isinstance(reward_func, GAILCost):

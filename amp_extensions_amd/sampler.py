@@ -556,7 +556,9 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
     pd = torch.from_numpy(perm).to(dev)
     host = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean))
-    log_std = np.float64(eng.policy.log_std_val)
+    log_std = np.asarray(eng.policy.log_std_val, dtype=np.float64)
+    # every step's log_std row (gaussian_mlp.py:102) as read-only broadcast views of one row
+    ls_rows = np.broadcast_to(log_std, (len(perm), log_std.shape[-1]))
     paths, off = [], 0
     for tr in trajs:
         T = tr.length
@@ -564,7 +566,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
         m = host[3][sl]
         paths.append(dict(observations=host[0][sl], next_observations=host[1][sl], actions=host[2][sl],
                           rewards=np.zeros(T, dtype=np.int64),
-                          agent_infos=dict(mean=m, log_std=np.tile(log_std, (T, 1)), evaluation=m),
+                          agent_infos=dict(mean=m, log_std=ls_rows[sl], evaluation=m),
                           env_infos=[{} for _ in range(T)], terminated=True))
         off += T
     return paths, off
@@ -795,7 +797,9 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
     perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
     pd = torch.from_numpy(perm).to(dev)
     host = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean))
-    log_std = np.float64(eng.policy.log_std_val)
+    log_std = np.asarray(eng.policy.log_std_val, dtype=np.float64)
+    # every step's log_std row (gaussian_mlp.py:102) as read-only broadcast views of one row
+    ls_rows = np.broadcast_to(log_std, (len(perm), log_std.shape[-1]))
     paths, off = [], 0
     for tr in trajs:
         T = tr.length
@@ -803,7 +807,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
         m = host[3][sl]
         paths.append(dict(observations=host[0][sl], next_observations=host[1][sl], actions=host[2][sl],
                           rewards=np.zeros(T, dtype=np.int64),
-                          agent_infos=dict(mean=m, log_std=np.tile(log_std, (T, 1)), evaluation=m),
+                          agent_infos=dict(mean=m, log_std=ls_rows[sl], evaluation=m),
                           env_infos=[{} for _ in range(T)], terminated=True))
         off += T
     return paths, off
