@@ -86,3 +86,48 @@ def test_relabel_paths_matches_oracle(setup):
     np.testing.assert_allclose(infos["ext"], ref_infos["ext"], rtol=1e-4, atol=1e-4 * np.abs(ref_infos["ext"]).max())
     assert infos["ep_len"] == ref_infos["ep_len"]
     np.testing.assert_allclose(infos["bonus_mmd"], ref_infos["bonus_mmd"], rtol=1e-4, atol=1e-7)
+
+
+def test_relabel_paths_device_rows_match_uploaded_copies(setup, monkeypatch):
+    """relabel_paths on sample_points' own paths reads the sampler's device rows (the paths'
+    arrays are read-only views of its host copy: no upload); on writable copies of the same
+    paths it uploads them.  Same bits either way; a subset of the paths (a contiguous range of
+    the views) also takes the device rows."""
+    amx, ens, ens_w, norms = setup
+    from amp_extensions_amd import relabel as RL
+    from amp_extensions_amd.synthetic import reset_table
+    s, a, _ = synthetic_offline(2048, 0)
+    ens.compute_threshold(torch.from_numpy(s).float(), torch.from_numpy(a).float())
+    es, _, es2 = synthetic_offline(800, 3)
+    expert = torch.cat([torch.from_numpy(es).float(), torch.from_numpy(es2).float()], dim=1)
+    cost = amx.RBFLinearCost(expert, feature_dim=512, lambda_b=0.0025, seed=100, ctx=ens.ctx)
+    pw, log_std = R.init_policy_weights(S, A, (32, 32), seed=100)
+    pol = amx.DevicePolicy(ens.ctx, pw, log_std)
+    env = amx.BatchedSimEnv(ens, reset_table(256, S, 1), lanes=64, horizon=15, record_means=True)
+    paths = amx.sample_points(env, pol, num_to_collect=300, base_seed=2)
+    assert not paths[0]["observations"].flags.writeable and not paths[0]["agent_infos"]["log_std"].flags.writeable
+    with pytest.raises(ValueError):
+        paths[0]["observations"][0, 0] = 1.0
+    copies = [{k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in p.items()} for p in paths]
+    used = []
+    real = RL._device_rows
+
+    def spy(ps, key, dev):
+        r = real(ps, key, dev)
+        used.append(r is not None)
+        return r
+    monkeypatch.setattr(RL, "_device_rows", spy)
+    RL.relabel_paths(paths, cost, ens)
+    assert used and all(used)
+    used.clear()
+    RL.relabel_paths(copies, cost, ens)
+    assert used and not any(used)
+    np.testing.assert_array_equal(np.concatenate([p["rewards"] for p in paths]),
+                                  np.concatenate([p["rewards"] for p in copies]))
+    used.clear()
+    sub, sub_copies = paths[2:5], copies[2:5]
+    RL.relabel_paths(sub, cost, ens)
+    assert used and all(used)
+    RL.relabel_paths(sub_copies, cost, ens)
+    np.testing.assert_array_equal(np.concatenate([p["rewards"] for p in sub]),
+                                  np.concatenate([p["rewards"] for p in sub_copies]))
