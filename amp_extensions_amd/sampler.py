@@ -723,7 +723,12 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
                     ests[w] += max(0, lhat)
                     progress = True
         active = np.array([b for b in range(L) if lane_tr[b] is not None], np.int64)
-        if active.size == 0:
+        # nothing to admit and every trajectory in flight reaches the horizon inside the queued
+        # chunk (its length through the chunks read back + K >= R): another chunk would only step
+        # idle lanes -- read the queued one back first
+        tail = (pending is not None and not new
+                and all(lane_tr[b].length + K >= R for b in active.tolist()))
+        if active.size == 0 or tail:
             if pending is None:
                 break
             process(pending)  # the last queued chunk may end trajectories or free admissions
