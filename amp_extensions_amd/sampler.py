@@ -333,25 +333,58 @@ class _ChunkGraph:
 _last_rows: dict = {}
 
 
-def _to_host_path_order(perm: torch.Tensor, arrays) -> list:
+def _to_host_path_order(perm: torch.Tensor, arrays, wait: bool = True):
     """The store's rows gathered into path order on the device, then ONE copy each into pinned
     host memory (2-4x the pageable .cpu() rate; torch's pinned-block cache reuses the blocks of
     paths the caller has dropped).  The returned numpy arrays keep their pinned tensors alive and
     are read-only (the reference's own code only reads the paths' arrays); the device rows of
-    (observations, next observations, actions) stay registered in _last_rows."""
+    (observations, next observations, actions) stay registered in _last_rows.  wait=False:
+    returns (arrays, event) with the copies still in flight (the event completes them)."""
     sel = [x.index_select(0, perm) for x in arrays]
     pin = torch.cuda.is_available()
     host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=pin) for t in sel]
     for h, t in zip(host, sel):
         h.copy_(t, non_blocking=pin)
+    ev = None
     if pin:
-        torch.cuda.current_stream(sel[0].device).synchronize()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(sel[0].device))
+        if wait:
+            ev.synchronize()
     out = [h.numpy() for h in host]
     for a in out:
         a.flags.writeable = False
     _last_rows.clear()
     _last_rows.update(observations=(out[0], sel[0]), next_observations=(out[1], sel[1]), actions=(out[2], sel[2]))
-    return out
+    return out if wait else (out, ev)
+
+
+def _build_paths(trajs, store, eng: RolloutEngine, dev):
+    """The trajectories' transitions in path order: one device gather, one asynchronous copy
+    into pinned host memory, the path dicts built as views while it runs."""
+    segs = [seg for tr in trajs for seg in tr.segs]
+    starts = np.fromiter((b for b, _ in segs), np.int64, len(segs))
+    lens = np.fromiter((n for _, n in segs), np.int64, len(segs))
+    total = int(lens.sum())
+    perm = np.repeat(starts - (np.cumsum(lens) - lens), lens) + np.arange(total, dtype=np.int64)
+    pd = torch.from_numpy(perm).to(dev)
+    host, copied = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean), wait=False)
+    log_std = np.asarray(eng.policy.log_std_val, dtype=np.float64)
+    # every step's log_std row (gaussian_mlp.py:102) as read-only broadcast views of one row
+    ls_rows = np.broadcast_to(log_std, (total, log_std.shape[-1]))
+    paths, off = [], 0
+    for tr in trajs:
+        T = tr.length
+        sl = slice(off, off + T)
+        m = host[3][sl]
+        paths.append(dict(observations=host[0][sl], next_observations=host[1][sl], actions=host[2][sl],
+                          rewards=np.zeros(T, dtype=np.int64),
+                          agent_infos=dict(mean=m, log_std=ls_rows[sl], evaluation=m),
+                          env_infos=[{} for _ in range(T)], terminated=True))
+        off += T
+    if copied is not None:
+        copied.synchronize()
+    return paths, off
 
 
 def _chunk_graph(eng: RolloutEngine, K: int, noise_dev, eval_mode: bool) -> _ChunkGraph:
@@ -553,23 +586,7 @@ def _collect(eng: RolloutEngine, W: int, quota: int, mode: str, base_seed: int, 
     trajs = [tr for w in range(W) for tr in adm[w]]
     if not trajs:
         return [], 0
-    perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
-    pd = torch.from_numpy(perm).to(dev)
-    host = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean))
-    log_std = np.asarray(eng.policy.log_std_val, dtype=np.float64)
-    # every step's log_std row (gaussian_mlp.py:102) as read-only broadcast views of one row
-    ls_rows = np.broadcast_to(log_std, (len(perm), log_std.shape[-1]))
-    paths, off = [], 0
-    for tr in trajs:
-        T = tr.length
-        sl = slice(off, off + T)
-        m = host[3][sl]
-        paths.append(dict(observations=host[0][sl], next_observations=host[1][sl], actions=host[2][sl],
-                          rewards=np.zeros(T, dtype=np.int64),
-                          agent_infos=dict(mean=m, log_std=ls_rows[sl], evaluation=m),
-                          env_infos=[{} for _ in range(T)], terminated=True))
-        off += T
-    return paths, off
+    return _build_paths(trajs, store, eng, dev)
 
 
 
@@ -799,23 +816,7 @@ def _collect_pipelined(eng: RolloutEngine, W: int, quota: int, mode: str, base_s
     trajs = [tr for w in range(W) for tr in adm[w]]
     if not trajs:
         return [], 0
-    perm = np.concatenate([np.arange(b, b + n) for tr in trajs for (b, n) in tr.segs])
-    pd = torch.from_numpy(perm).to(dev)
-    host = _to_host_path_order(pd, (store.obs, store.nxt, store.act, store.mean))
-    log_std = np.asarray(eng.policy.log_std_val, dtype=np.float64)
-    # every step's log_std row (gaussian_mlp.py:102) as read-only broadcast views of one row
-    ls_rows = np.broadcast_to(log_std, (len(perm), log_std.shape[-1]))
-    paths, off = [], 0
-    for tr in trajs:
-        T = tr.length
-        sl = slice(off, off + T)
-        m = host[3][sl]
-        paths.append(dict(observations=host[0][sl], next_observations=host[1][sl], actions=host[2][sl],
-                          rewards=np.zeros(T, dtype=np.int64),
-                          agent_infos=dict(mean=m, log_std=ls_rows[sl], evaluation=m),
-                          env_infos=[{} for _ in range(T)], terminated=True))
-        off += T
-    return paths, off
+    return _build_paths(trajs, store, eng, dev)
 
 def sample_points(env, policy, num_to_collect: int, base_seed: int = 0, num_workers: int = 4, mode: str = "samples",
                   eval_mode: bool = False, verbose: bool = False, deepmimic: bool = False, rng: str = "reference",
