@@ -50,6 +50,8 @@ class AmxContext:
         k0, ldk, nout, kr = (N.C.c_int(), N.C.c_int(), N.C.c_int(), N.C.c_int())
         N.check(self.lib.amx_layout(h, N.C.byref(k0), N.C.byref(ldk), N.C.byref(nout), N.C.byref(kr)), "amx_layout")
         self.k0_pad, self.ldk, self.n_out_pad, self.k_rff_pad = k0.value, ldk.value, nout.value, kr.value
+        # compute units (the C side's tile choices use the same device property)
+        self.n_cus = torch.cuda.get_device_properties(self.device).multi_processor_count
 
     def __del__(self):
         try:
@@ -237,8 +239,11 @@ class DeviceEnsemble:
         return self.ctx.M
 
     def workspace(self, B: int):
-        """Activation + prediction buffers for B lanes (cached per B_pad)."""
+        """Activation + prediction buffers for B lanes (cached per B_pad).  B_pad = round_up(B, 128),
+        or to 256 for large odd counts (the relabel's 40 530 samples: the 256 x 256 tiles need it)."""
         Bp = round_up(max(B, 1), 128)
+        if Bp >= 16384 and Bp % 256:
+            Bp += 128
         ws = self._ws.get(Bp)
         if ws is None:
             c = self.ctx
@@ -531,6 +536,11 @@ class RffMap:
         c = self.ctx
         n = x.shape[0]
         rows = round_up(max(n, 1), 128)
+        # the 160 x 256 one-round tiles (amx_rff_features_h3) need rows = k * 160 * CUs / (F / 256):
+        # worth ~1 % of padding rows (40 530 -> 40 960: 121 -> 76 us on 128 x 128 tiles)
+        r160 = 160 * c.n_cus // max(self.F // 256, 1) if self.F % 256 == 0 else 0
+        if self.W2 is not None and r160 and n >= r160 and round_up(n, r160) <= 1.05 * n:
+            rows = round_up(n, r160)
         xp = torch.zeros(rows, self.Kp, dtype=torch.float32, device=c.device)
         xp[:n, :self.D] = x.to(c.device, torch.float32)
         phi = torch.empty(rows, self.F, dtype=torch.float32, device=c.device)
