@@ -608,6 +608,24 @@ __device__ __forceinline__ void policy_core(const PolicyArgs& p, float* psm, int
   const int t = threadIdx.x;
   const bool on = t < 256;               // wave-uniform
   const int nc1 = (S + 3) >> 2, nc2 = (H1 + 3) >> 2, nc3 = (H2 + 3) >> 2;
+  // the injected noise and the noise scale of this thread's (lane, action pair) items, loaded
+  // before the layers so the round trip hides under them (the action loop below: at most
+  // POL_PRE items per thread)
+  const int npairs = (A + 1) >> 1;
+  constexpr int POL_PRE = 2;
+  double pre_n[POL_PRE][2], pre_s[POL_PRE][2];
+#pragma unroll
+  for (int q = 0; q < POL_PRE; ++q) {
+    const int e = t + 256 * q;
+    const int l = e / npairs, pr = e - l * npairs, b = b0 + l;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = 2 * pr + h;
+      const bool ok = on && e < POL_LANES * npairs && b < p.B && u < A;
+      pre_n[q][h] = (ok && p.noise && !p.eval_mode) ? p.noise[(long long)b * A + u] : 0.0;
+      pre_s[q][h] = (ok && !p.eval_mode) ? p.nscale[u] : 0.0;
+    }
+  }
   if (on) pol_mfma_layer(so, s1, nc1, w1, s1, H1, part);
   __syncthreads();
   if (on) pol_combine(part, H1, nc1, bb1, true, h1, s2);
@@ -622,17 +640,18 @@ __device__ __forceinline__ void policy_core(const PolicyArgs& p, float* psm, int
   __syncthreads();
   // actions: one thread per (lane, pair u = 2pr, 2pr + 1): Box-Muller on one Philox block gives
   // both normals of the pair (gaussian_mlp.py:102-103: float32 mean + float64 noise)
-  const int npairs = (A + 1) >> 1;
   uint32_t ctr_lo = p.ctr_lo, ctr_hi = p.ctr_hi;
   if (p.ctr_dev) {  // device counter + the by-value offset
     const uint64_t cv = *p.ctr_dev + ((uint64_t)p.ctr_hi << 32 | p.ctr_lo);
     ctr_lo = (uint32_t)cv;
     ctr_hi = (uint32_t)(cv >> 32);
   }
-  for (int e = t; on && e < POL_LANES * npairs; e += 256) {
+  // item e = (lane l, pair pr); items t and t + 256 use the prefetched noise, any further ones
+  // (A > 2 * 256 / POL_LANES) load it here
+  auto act_item = [&](int e, const double* pn, const double* ps) {
     const int l = e / npairs, pr = e - l * npairs;
     const int b = b0 + l;
-    if (b >= p.B) continue;
+    if (b >= p.B) return;
     double n[2] = {0.0, 0.0};
     if (!p.eval_mode && !p.noise) {
       const amx::u32x4 r = amx::philox4x32_10(
@@ -654,12 +673,18 @@ __device__ __forceinline__ void policy_core(const PolicyArgs& p, float* psm, int
       if (p.eval_mode) {
         a_out = (double)m;
       } else {
-        const double nz = p.noise ? p.noise[(long long)b * A + u] : n[h];
-        a_out = (double)m + p.nscale[u] * nz;
+        const double nz = p.noise ? (pn ? pn[h] : p.noise[(long long)b * A + u]) : n[h];
+        a_out = (double)m + (ps ? ps[h] : p.nscale[u]) * nz;
       }
       p.act[(long long)b * A + u] = a_out;
       if (p.x0) xa_s[l * A + u] = (float)a_out;
     }
+  };
+  if (on) {
+#pragma unroll
+    for (int q = 0; q < POL_PRE; ++q)
+      if (t + 256 * q < POL_LANES * npairs) act_item(t + 256 * q, pre_n[q], pre_s[q]);
+    for (int e = t + 256 * POL_PRE; e < POL_LANES * npairs; e += 256) act_item(e, nullptr, nullptr);
   }
   if (!p.x0) return;
   __syncthreads();
