@@ -88,6 +88,10 @@ SIGNATURES = {
     "amx_npg_curvature": (c_int, [vp, vp, c_int, c_int, vp, vp]),
     "amx_npg_cg_tail_work": (c_ll, [c_int]),
     "amx_npg_cg_tail": (c_int, [vp, vp, c_int, c_int, c_int, vp, c_dbl, c_dbl, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "amx_npg_cg_reduce": (c_int, [vp, vp, c_int, c_int, c_int, vp, c_dbl, vp, vp, vp, vp, vp]),
+    "amx_npg_cg_xrp": (c_int, [vp, c_int, c_dbl, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "amx_npg_pass_cg": (c_int, [vp, c_int, vp, c_int, c_ll, vp, c_int, vp, vp, c_dbl, vp, vp, vp, vp, vp, vp, vp, vp,
+                                vp, vp]),
     "amx_npg_apply_step": (c_int, [vp, c_int, c_int, vp, vp, vp, c_int, c_dbl, c_dbl, c_flt, vp, vp, vp]),
     "amx_npg_pass_ex": (c_int, [vp, c_int, c_int, vp, c_int, c_ll, vp, c_int, c_ll, vp, vp, vp, c_int, vp, vp, vp, vp]),
     "amx_npg_cg_init": (c_int, [vp, c_int, vp, vp, vp, vp, vp, vp, vp]),

@@ -77,6 +77,24 @@ constexpr int G3SLOTS = (3 * (MAXA / 16) + NW - 1) / NW;         // gW3 tiles pe
 
 enum { NPG_VPG = 0, NPG_FVP = 1, NPG_EVAL = 2 };
 
+// ---- conjugate gradient constants (cg_solve.py:3-23) ----
+constexpr int CGT = 1024;
+constexpr int CGE = 16;              // elements per thread: P <= CGT * CGE
+constexpr int RCT = 1024, RCC = 64;  // k_npg_cg_reduce: threads, columns per block (16 run lanes per column)
+constexpr int XRT = 1024;            // k_npg_cg_xrp threads (and elements owned) per block
+
+// the sum of n fixed-order parts, computed the same way by every wave that calls it (lane-strided
+// partial sums, then an xor butterfly: every lane ends with the same bits)
+__device__ inline double parts_sum(const double* __restrict__ parts, int n) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  for (int i = lane; i < n; i += 64) s += parts[i];
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o);
+  return s;
+}
+
+
 typedef float pf4 __attribute__((ext_vector_type(4)));
 
 struct NpgArgs {
@@ -91,6 +109,12 @@ struct NpgArgs {
   int P;
   const double* gate;        // optional CG state {rdotr, live}: live == 0 -> the pass is a no-op
   float* hcache;             // optional theta forward [N][64] = H1 | H2: VPG writes it, FVP (HC) reads it
+  // FVP with the previous CG iteration's vector step folded in (amx_npg_pass_cg; cg_state_in
+  // null: the tangent is vec): the k_npg_cg_xrp operands, p' (not vec) is the tangent
+  const double* cg_state_in; double* cg_state_out; double cg_tol;
+  double* cg_x; const double* cg_r_in; double* cg_r_out;
+  const double* cg_p_in; double* cg_p_out; float* cg_p32_out;
+  const double* cg_work;     // k_npg_cg_reduce's output: z [P] | p.z parts
 };
 constexpr int HCW = 2 * 32;  // floats per cached row (H1 | H2)
 
@@ -184,6 +208,90 @@ __device__ inline int small_dst(int e, const Geo& g) {  // offsets as carve_smal
 // chunk's global loads stay in flight across it (__syncthreads' fence waits for them too).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// The CG fold (amx_npg_pass_cg): the previous iteration's vector step -- k_npg_cg_xrp's
+// arithmetic in its orders, so the same bits -- at the head of the next Fisher-vector pass,
+// which drops that launch from every iteration but the last.  Every block forms v = r.r / p.z
+// from the p.z parts, r' = r - v z for all P elements and r'.r' in xrp's order (thread t
+// stands in for xrp's threads t and t + 512: elements t + 512 k, k even / odd, two wave
+// butterflies, the 16 wave sums in order), mu = r'.r' / r.r, and stages p' = r' + mu p as
+// float32 in LDS (pb: P floats, then 16 doubles) for the tangent's parameter images; it writes
+// its own slice of x += v p, r', p', float32(p') and block 0 the state {r'.r', live}.  Returns
+// false when the solve has stopped (earlier, or now: r'.r' < tol): no product, as the gate.
+__device__ __forceinline__ bool cg_fold(const NpgArgs& a, float* pb, int t) {
+  const int P = a.P;
+  const int cs = (P + gridDim.x - 1) / gridDim.x;
+  const int lo = blockIdx.x * cs, hi = min(P, lo + cs);
+  if (a.cg_state_in[1] == 0.0) {  // stopped: carry r and p over to the out buffers
+    for (int e = lo + t; e < hi; e += NT) {
+      const double pv = a.cg_p_in[e];
+      a.cg_r_out[e] = a.cg_r_in[e];
+      a.cg_p_out[e] = pv;
+      a.cg_p32_out[e] = (float)pv;
+    }
+    if (blockIdx.x == 0 && t == 0) {
+      a.cg_state_out[0] = a.cg_state_in[0];
+      a.cg_state_out[1] = 0.0;
+    }
+    return false;
+  }
+  constexpr int K = 2 * CGE;  // P <= NT * K
+  const double* zbuf = a.cg_work;
+  double rl[K], zl[K], pl[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int e = t + NT * k;
+    const bool ok = e < P;
+    rl[k] = ok ? a.cg_r_in[e] : 0.0;
+    zl[k] = ok ? zbuf[e] : 0.0;
+    pl[k] = ok ? a.cg_p_in[e] : 0.0;
+  }
+  const double rdotr = a.cg_state_in[0];
+  const double v = rdotr / parts_sum(zbuf + P, (P + RCC - 1) / RCC);
+  double rr0 = 0.0, rr1 = 0.0;
+#pragma unroll
+  for (int u = 0; u < CGE; ++u) {
+    rl[2 * u] = rl[2 * u] - v * zl[2 * u];
+    rr0 += rl[2 * u] * rl[2 * u];
+    rl[2 * u + 1] = rl[2 * u + 1] - v * zl[2 * u + 1];
+    rr1 += rl[2 * u + 1] * rl[2 * u + 1];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    rr0 += __shfl_xor(rr0, o);
+    rr1 += __shfl_xor(rr1, o);
+  }
+  double* red = reinterpret_cast<double*>(pb + r4(P));
+  if ((t & 63) == 0) {
+    red[t >> 6] = rr0;
+    red[NW + (t >> 6)] = rr1;
+  }
+  lds_barrier();
+  double rr = 0.0;
+  for (int w = 0; w < 2 * NW; ++w) rr += red[w];
+  const double mu = rr / rdotr;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int e = t + NT * k;
+    if (e < P) {
+      const double pn = rl[k] + mu * pl[k];
+      pb[e] = (float)pn;
+      if (e >= lo && e < hi) {
+        a.cg_x[e] += v * pl[k];
+        a.cg_r_out[e] = rl[k];
+        a.cg_p_out[e] = pn;
+        a.cg_p32_out[e] = (float)pn;
+      }
+    }
+  }
+  const bool live = !(rr < a.cg_tol);
+  if (blockIdx.x == 0 && t == 0) {
+    a.cg_state_out[0] = rr;
+    a.cg_state_out[1] = live ? 1.0 : 0.0;
+  }
+  lds_barrier();  // p' staged
+  return live;
+}
+
 __device__ __forceinline__ pf4 mma(float a, float b, pf4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -227,6 +335,15 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   float* TAB = carve(p, 2 * g.A16);   // per action: FVP 2 / (2 sigma^2 + 1e-8); VPG sigma; EVAL sigma_old | sigma_new
 
   NPG_STAMP(0);
+  // FVP with the CG fold: the tangent p' is staged in LDS from the X tile on (read below, before
+  // the W1 fragments reuse that space)
+  bool fold = false;
+  if constexpr (MODE == NPG_FVP) {
+    if (a.cg_state_in) {
+      if (!cg_fold(a, X, t)) return;
+      fold = true;
+    }
+  }
   // Setup issues every global load before the first store (one memory round trip, not one per
   // array): W1 (and the tangent's / new W1) as coalesced float4s, the small parameter images,
   // the log_std table and the first chunk's inputs.  W1 then goes through LDS (the X tile's
@@ -244,7 +361,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
     w1a[u] = w1b[u] = pf4{0.f, 0.f, 0.f, 0.f};
     if (e < nw4) {
       if (!HCF) w1a[u] = reinterpret_cast<const pf4*>(a.theta)[e];
-      if (two) w1b[u] = reinterpret_cast<const pf4*>(a.vec)[e];
+      if (two) w1b[u] = fold ? reinterpret_cast<const pf4*>(X)[e] : reinterpret_cast<const pf4*>(a.vec)[e];
     }
   }
   NPG_STAMP(50);
@@ -258,7 +375,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
       const int src = small_src(e, L, g);
       if (src >= 0) {
         sv0[u] = a.theta[src];
-        if (two) sv1[u] = a.vec[src];
+        if (two) sv1[u] = fold ? X[src] : a.vec[src];
       }
     }
   }
@@ -316,6 +433,7 @@ __global__ __launch_bounds__(NT, 1) void k_npg(NpgArgs a) {
   NPG_STAMP(52);
   if (r0 < r1) prefetch(r0, min(RC, r1 - r0));
   NPG_STAMP(53);
+  if (fold) lds_barrier();  // every wave has read p' before the fragments overwrite X
 
   // W1 fragments via LDS: set 0, then (FVP / EVAL) set 1, through the X tile's space
   pf4 wf[JJM];
@@ -847,9 +965,6 @@ __global__ void k_npg_reduce2(const double* __restrict__ mid, int nr, int P, dou
 }
 
 // ---- conjugate gradient (cg_solve.py:3-23) ---------------------------------------------
-constexpr int CGT = 1024;
-constexpr int CGE = 16;  // elements per thread: P <= CGT * CGE
-
 // sum over the workgroup in a fixed order (per-thread sums, wave butterflies, waves in order)
 __device__ double cg_block_sum(double v, double* red) {
 #pragma unroll
@@ -1023,19 +1138,7 @@ __global__ __launch_bounds__(CGT) void k_npg_apply(int P, int A, const double* _
 //    reads all of r while the others write theirs; a stopped solve (state_in live == 0) only
 //    carries r and the state over, so every later iteration stays stopped.
 // work = [zbuf: P | pz parts: ceil(P / 64)].
-constexpr int RCT = 1024, RCC = 64;  // threads, columns per block (16 run lanes per column)
-constexpr int XRT = 1024;            // k_npg_cg_xrp threads (and elements owned) per block
-
-// the sum of n fixed-order parts, computed the same way by every wave that calls it (lane-strided
-// partial sums, then an xor butterfly: every lane ends with the same bits)
-__device__ inline double parts_sum(const double* __restrict__ parts, int n) {
-  const int lane = threadIdx.x & 63;
-  double s = 0.0;
-  for (int i = lane; i < n; i += 64) s += parts[i];
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) s += __shfl_xor(s, o);
-  return s;
-}
+// (RCT, RCC, XRT: with the CG constants at the top of the file)
 
 __global__ __launch_bounds__(RCT) void k_npg_cg_reduce(const double* __restrict__ part, int nb, int P, int A,
                                                        const double* __restrict__ curv, double damping,
@@ -1170,24 +1273,15 @@ extern "C" int amx_npg_pass_gated(amx_ctx* ctx, int mode, int N, const void* obs
                          partials, gate, nullptr, stream);
 }
 
-extern "C" int amx_npg_pass_ex(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
-                               const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
-                               const float* vec, int rows_per_block, double* partials, const double* gate,
-                               float* hcache, void* stream) {
-  AMX_CHECK_ARG(ctx, "amx_npg_pass: null ctx");
+namespace {
+// the pass launch behind amx_npg_pass_ex / amx_npg_pass_cg (cg: the fold's operands, or null)
+int npg_launch(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo, const void* act,
+               int act_dtype, long long lda, const double* adv, const float* theta, const float* vec,
+               int rows_per_block, double* partials, const double* gate, float* hcache, const NpgArgs* cg,
+               void* stream) {
   const int S = ctx->S, A = ctx->A;
-  AMX_CHECK_ARG(mode >= NPG_VPG && mode <= NPG_EVAL, "amx_npg_pass: mode=%d", mode);
-  AMX_CHECK_ARG(S > 0 && S <= MAXS && A > 0 && A <= MAXA, "amx_npg_pass: S=%d (<= %d), A=%d (<= %d)", S, MAXS, A,
-                MAXA);
-  AMX_CHECK_ARG(N > 0 && rows_per_block > 0 && rows_per_block % RC0 == 0,
-                "amx_npg_pass: N=%d rows_per_block=%d (multiple of %d)", N, rows_per_block, RC0);
-  AMX_CHECK_ARG(obs && act && theta && partials, "amx_npg_pass: null buffer");
-  AMX_CHECK_ARG((mode == NPG_FVP || adv) && (mode == NPG_VPG || vec), "amx_npg_pass: adv/vec missing for mode %d",
-                mode);
-  AMX_CHECK_ARG(ldo >= S && lda >= A, "amx_npg_pass: ldo=%lld lda=%lld", ldo, lda);
-  AMX_CHECK_ARG(((uintptr_t)theta & 15) == 0 && ((uintptr_t)vec & 15) == 0,
-                "amx_npg_pass: theta / vec must be 16-byte aligned (W1 is read as float4s)");
   NpgArgs a = {};
+  if (cg) a = *cg;
   a.mode = mode; a.N = N; a.S = S; a.A = A; a.rows_per_block = rows_per_block;
   a.obs = obs; a.ldo = ldo;
   a.act = act; a.lda = lda;
@@ -1225,6 +1319,59 @@ extern "C" int amx_npg_pass_ex(amx_ctx* ctx, int mode, int N, const void* obs, i
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(NT), lds, (hipStream_t)stream, a);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
+}
+}  // namespace
+
+extern "C" int amx_npg_pass_ex(amx_ctx* ctx, int mode, int N, const void* obs, int obs_dtype, long long ldo,
+                               const void* act, int act_dtype, long long lda, const double* adv, const float* theta,
+                               const float* vec, int rows_per_block, double* partials, const double* gate,
+                               float* hcache, void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_npg_pass: null ctx");
+  const int S = ctx->S, A = ctx->A;
+  AMX_CHECK_ARG(mode >= NPG_VPG && mode <= NPG_EVAL, "amx_npg_pass: mode=%d", mode);
+  AMX_CHECK_ARG(S > 0 && S <= MAXS && A > 0 && A <= MAXA, "amx_npg_pass: S=%d (<= %d), A=%d (<= %d)", S, MAXS, A,
+                MAXA);
+  AMX_CHECK_ARG(N > 0 && rows_per_block > 0 && rows_per_block % RC0 == 0,
+                "amx_npg_pass: N=%d rows_per_block=%d (multiple of %d)", N, rows_per_block, RC0);
+  AMX_CHECK_ARG(obs && act && theta && partials, "amx_npg_pass: null buffer");
+  AMX_CHECK_ARG((mode == NPG_FVP || adv) && (mode == NPG_VPG || vec), "amx_npg_pass: adv/vec missing for mode %d",
+                mode);
+  AMX_CHECK_ARG(ldo >= S && lda >= A, "amx_npg_pass: ldo=%lld lda=%lld", ldo, lda);
+  AMX_CHECK_ARG(((uintptr_t)theta & 15) == 0 && ((uintptr_t)vec & 15) == 0,
+                "amx_npg_pass: theta / vec must be 16-byte aligned (W1 is read as float4s)");
+  return npg_launch(ctx, mode, N, obs, obs_dtype, ldo, act, act_dtype, lda, adv, theta, vec, rows_per_block, partials,
+                    gate, hcache, nullptr, stream);
+}
+
+extern "C" int amx_npg_pass_cg(amx_ctx* ctx, int N, const void* obs, int obs_dtype, long long ldo,
+                               const float* theta, int rows_per_block, double* partials, float* hcache, double tol,
+                               double* x, const double* r_in, double* r_out, const double* p_in, double* p_out,
+                               float* p32_out, const double* state_in, double* state_out, const double* work,
+                               void* stream) {
+  AMX_CHECK_ARG(ctx, "amx_npg_pass_cg: null ctx");
+  const int S = ctx->S, A = ctx->A;
+  AMX_CHECK_ARG(S > 0 && S <= MAXS && A > 0 && A <= MAXA, "amx_npg_pass_cg: S=%d (<= %d), A=%d (<= %d)", S, MAXS,
+                A, MAXA);
+  AMX_CHECK_ARG(N > 0 && rows_per_block > 0 && rows_per_block % RC0 == 0,
+                "amx_npg_pass_cg: N=%d rows_per_block=%d (multiple of %d)", N, rows_per_block, RC0);
+  AMX_CHECK_ARG(obs && theta && partials && x && r_in && r_out && p_in && p_out && p32_out && state_in && state_out &&
+                    work,
+                "amx_npg_pass_cg: null buffer");
+  AMX_CHECK_ARG(r_in != r_out && p_in != p_out && state_in != state_out,
+                "amx_npg_pass_cg: r, p and the state must alternate buffers (every block reads all of them)");
+  AMX_CHECK_ARG(ldo >= S && ((uintptr_t)theta & 15) == 0, "amx_npg_pass_cg: ldo=%lld, theta 16-byte aligned", ldo);
+  const int P = (int)amx_npg_param_count(S, A);
+  const Geo g(S, A);
+  // p' (P floats) and the 16 wave sums are staged from the X tile to the end of the LDS image
+  const size_t region = npg_lds_bytes(S, A, NPG_FVP, RC0) - sizeof(float) * 2 * small_floats(g);
+  AMX_CHECK_ARG(P <= NT * 2 * CGE && sizeof(float) * (r4(P) + 4 * NW) <= region,
+                "amx_npg_pass_cg: P=%d does not fit the fold (<= %d, %zu B of staging)", P, NT * 2 * CGE, region);
+  NpgArgs cg = {};
+  cg.cg_state_in = state_in; cg.cg_state_out = state_out; cg.cg_tol = tol;
+  cg.cg_x = x; cg.cg_r_in = r_in; cg.cg_r_out = r_out;
+  cg.cg_p_in = p_in; cg.cg_p_out = p_out; cg.cg_p32_out = p32_out; cg.cg_work = work;
+  return npg_launch(ctx, NPG_FVP, N, obs, obs_dtype, ldo, obs, AMX_IN_F32, A, nullptr, theta, nullptr,
+                    rows_per_block, partials, nullptr, hcache, &cg, stream);
 }
 
 extern "C" int amx_npg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, double* out, void* stream) {
@@ -1278,6 +1425,31 @@ extern "C" int amx_npg_cg_tail(amx_ctx* ctx, const double* partials, int blocks,
   AMX_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_npg_cg_xrp, dim3((P + XRT - 1) / XRT), dim3(XRT), 0, s, P, tol, state_in, state_out, x, r_in,
                      r_out, p, p32, work);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_npg_cg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
+                                 double damping, const double* p, const float* p32, const double* state, double* work,
+                                 void* stream) {
+  AMX_CHECK_ARG(ctx && partials && curv && p && p32 && state && work, "amx_npg_cg_reduce: null argument");
+  AMX_CHECK_ARG(blocks > 0 && blocks <= RB * RCT / RCC && P > A && A > 0 && P <= XRT * CGE,
+                "amx_npg_cg_reduce: blocks=%d (<= %d) P=%d A=%d (P <= %d)", blocks, RB * RCT / RCC, P, A, XRT * CGE);
+  hipLaunchKernelGGL(k_npg_cg_reduce, dim3((P + RCC - 1) / RCC), dim3(RCT), 0, (hipStream_t)stream, partials, blocks,
+                     P, A, curv, damping, p, p32, state, work);
+  AMX_CHECK_LAUNCH();
+  return AMX_OK;
+}
+
+extern "C" int amx_npg_cg_xrp(amx_ctx* ctx, int P, double tol, double* x, const double* r_in, double* r_out,
+                              double* p, float* p32, const double* state_in, double* state_out, const double* work,
+                              void* stream) {
+  AMX_CHECK_ARG(ctx && x && r_in && r_out && p && p32 && state_in && state_out && work,
+                "amx_npg_cg_xrp: null argument");
+  AMX_CHECK_ARG(r_in != r_out && state_in != state_out, "amx_npg_cg_xrp: r and the state must alternate buffers");
+  AMX_CHECK_ARG(P > 0 && P <= XRT * CGE, "amx_npg_cg_xrp: P=%d (<= %d)", P, XRT * CGE);
+  hipLaunchKernelGGL(k_npg_cg_xrp, dim3((P + XRT - 1) / XRT), dim3(XRT), 0, (hipStream_t)stream, P, tol, state_in,
+                     state_out, x, r_in, r_out, p, p32, work);
   AMX_CHECK_LAUNCH();
   return AMX_OK;
 }

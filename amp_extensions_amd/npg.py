@@ -71,6 +71,7 @@ class DeviceNPG:
             raise ValueError("policy shapes do not match the context's S, A")
         FIM_invert_args = FIM_invert_args or {"iters": 10, "damping": 1e-4}
         self.cg_iters = int(FIM_invert_args["iters"])
+        self.cg_fold = True  # the CG vector step folded into the next Fisher-vector pass
         self.damping = float(FIM_invert_args["damping"])
         self.alpha = const_learn_rate
         self.n_step_size = normalized_step_size if kl_dist is None else 2.0 * kl_dist
@@ -197,21 +198,22 @@ class DeviceNPG:
 
     def cg_solve(self, obs, act, b: torch.Tensor, hcache=None) -> torch.Tensor:
         """mjrl/mjrl/utils/cg_solve.py:3-23 (starts from zeros; stops at rdotr < tol) with
-        NPG.HVP as the operator.  Each iteration is one Fisher-vector pass + reduce and one
-        vector step, the pass's reduction folded into the step (amx_npg_cg_tail: column sums and z
-        per block, then x, r and p over the whole chip from fixed-order block parts); the early stop
-        is the step's device-side
-        `live` flag (a finished solve leaves x unchanged), so no host sync between iterations.
-        The FVP pass and its reduction read the same flag (amx_npg_pass_gated): after the stop
-        the remaining iterations are empty launches, not Fisher-vector products.  `hcache`: the
+        NPG.HVP as the operator.  Each iteration is one Fisher-vector pass and one column-sum
+        launch (amx_npg_cg_reduce: z and the p.z parts per block); the vector step (x, r, p from
+        fixed-order block parts) runs at the head of the NEXT iteration's pass (amx_npg_pass_cg,
+        the same bits as the step's own launch) and once more, alone, after the last
+        (amx_npg_cg_xrp).  `cg_fold = False` runs the round-5 form instead: the pass on p32, then
+        amx_npg_cg_tail (the reduction and the step in two launches).  The early stop is the
+        device-side `live` flag (a finished solve leaves x unchanged), so no host sync between
+        iterations; after the stop the passes and reductions are empty launches.  `hcache`: the
         theta forward written by this update's VPG pass (train_from_arrays), so every product
         skips layers 1-2 at theta (bit-identical products)."""
         c = self.ctx
         P = self.P
         dev = c.device
         b = b.to(torch.float64).contiguous()
-        x, r, p, r2 = (torch.empty(P, dtype=torch.float64, device=dev) for _ in range(4))
-        p32 = torch.empty(P, dtype=torch.float32, device=dev)
+        x, r, p, r2, p2 = (torch.empty(P, dtype=torch.float64, device=dev) for _ in range(5))
+        p32, p32b = (torch.empty(P, dtype=torch.float32, device=dev) for _ in range(2))
         state, state2 = (torch.empty(2, dtype=torch.float64, device=dev) for _ in range(2))
         curv = torch.empty(self.A, dtype=torch.float64, device=dev)  # the log_std curvature, same launch
         N.check(c.lib.amx_npg_cg_init_ls(c.h, P, self.A, self.theta.data_ptr(), curv.data_ptr(), b.data_ptr(),
@@ -221,17 +223,41 @@ class DeviceNPG:
         if work is None:
             work = self._bufs["cg_work"] = torch.empty(int(c.lib.amx_npg_cg_tail_work(P)), dtype=torch.float64,
                                                        device=dev)
-        for _ in range(self.cg_iters):
-            part = self._pass(NPG_FVP, obs, act, None, p32, gate=state,
-                              hcache=hcache if obs.dtype == torch.float32 else None, reduce=False)
-            # the partials' column sums and the vector step (amx_npg_cg_tail: two launches); r and
-            # the state alternate buffers from one iteration to the next
-            N.check(c.lib.amx_npg_cg_tail(c.h, part.data_ptr(), part.shape[0], P, self.A, curv.data_ptr(),
-                                          self.damping, self.residual_tol, x.data_ptr(), r.data_ptr(), r2.data_ptr(),
-                                          p.data_ptr(), p32.data_ptr(), state.data_ptr(), state2.data_ptr(),
-                                          work.data_ptr(), c.stream), "amx_npg_cg_tail")
-            r, r2 = r2, r
-            state, state2 = state2, state
+        hc = hcache if obs.dtype == torch.float32 else None
+        if not self.cg_fold:
+            for _ in range(self.cg_iters):
+                part = self._pass(NPG_FVP, obs, act, None, p32, gate=state, hcache=hc, reduce=False)
+                # the partials' column sums and the vector step (amx_npg_cg_tail: two launches); r
+                # and the state alternate buffers from one iteration to the next
+                N.check(c.lib.amx_npg_cg_tail(c.h, part.data_ptr(), part.shape[0], P, self.A, curv.data_ptr(),
+                                              self.damping, self.residual_tol, x.data_ptr(), r.data_ptr(),
+                                              r2.data_ptr(), p.data_ptr(), p32.data_ptr(), state.data_ptr(),
+                                              state2.data_ptr(), work.data_ptr(), c.stream), "amx_npg_cg_tail")
+                r, r2 = r2, r
+                state, state2 = state2, state
+            return x
+        n = obs.shape[0]
+        rpb = self._rows_per_block(n)
+        od = N.AMX_IN_F64 if obs.dtype == torch.float64 else N.AMX_IN_F32
+        for it in range(self.cg_iters):
+            if it == 0:
+                part = self._pass(NPG_FVP, obs, act, None, p32, gate=state, hcache=hc, reduce=False)
+            else:
+                # the previous iteration's vector step, then the product with its p'; r, p, p32
+                # and the state alternate buffers (every block reads all of them)
+                N.check(c.lib.amx_npg_pass_cg(c.h, n, obs.data_ptr(), od, obs.stride(0), self.theta.data_ptr(), rpb,
+                                              part.data_ptr(), None if hc is None else hc.data_ptr(),
+                                              self.residual_tol, x.data_ptr(), r.data_ptr(), r2.data_ptr(),
+                                              p.data_ptr(), p2.data_ptr(), p32b.data_ptr(), state.data_ptr(),
+                                              state2.data_ptr(), work.data_ptr(), c.stream), "amx_npg_pass_cg")
+                r, r2, p, p2, p32, p32b, state, state2 = r2, r, p2, p, p32b, p32, state2, state
+            N.check(c.lib.amx_npg_cg_reduce(c.h, part.data_ptr(), part.shape[0], P, self.A, curv.data_ptr(),
+                                            self.damping, p.data_ptr(), p32.data_ptr(), state.data_ptr(),
+                                            work.data_ptr(), c.stream), "amx_npg_cg_reduce")
+        if self.cg_iters > 0:
+            N.check(c.lib.amx_npg_cg_xrp(c.h, P, self.residual_tol, x.data_ptr(), r.data_ptr(), r2.data_ptr(),
+                                         p.data_ptr(), p32.data_ptr(), state.data_ptr(), state2.data_ptr(),
+                                         work.data_ptr(), c.stream), "amx_npg_cg_xrp")
         return x
 
     def surrogate_kl(self, obs, act, adv_w, new_theta) -> tuple[float, float]:

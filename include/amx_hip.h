@@ -339,6 +339,28 @@ long long amx_npg_cg_tail_work(int P);
 int amx_npg_cg_tail(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
                     double damping, double tol, double* x, const double* r_in, double* r_out, double* p, float* p32,
                     const double* state_in, double* state_out, double* work, void* stream);
+/* amx_npg_cg_tail's two launches, separately: amx_npg_cg_reduce (column sums, z and the p.z
+ * parts into work; skipped when state[1] == 0) and amx_npg_cg_xrp (the vector step from work:
+ * x, r_in -> r_out, p, p32 in place, state_in -> state_out). */
+int amx_npg_cg_reduce(amx_ctx* ctx, const double* partials, int blocks, int P, int A, const double* curv,
+                      double damping, const double* p, const float* p32, const double* state, double* work,
+                      void* stream);
+int amx_npg_cg_xrp(amx_ctx* ctx, int P, double tol, double* x, const double* r_in, double* r_out, double* p,
+                   float* p32, const double* state_in, double* state_out, const double* work, void* stream);
+/* The Fisher-vector pass (mode 1, amx_npg_pass_ex with hcache) with the PREVIOUS CG iteration's
+ * vector step folded into its setup: every block forms amx_npg_cg_xrp's v, r' = r_in - v z,
+ * r'.r' (xrp's summation orders: the same bits) and p' = r' + (r'.r' / r.r) p_in from work (the
+ * previous amx_npg_cg_reduce) and multiplies by float32(p') instead of a vec argument; the blocks
+ * write x += v p_in, r_out, p_out, p32_out (their slices) and state_out {r'.r', live}.  A solve
+ * stopped before (state_in[1] == 0) or by this step (r'.r' < tol) writes no partials (the gate)
+ * and carries r, p and the state over.  r, p and the state alternate buffers (every block reads
+ * all of them).  One CG iteration = amx_npg_pass_cg (or, first, amx_npg_pass_gated on p32) +
+ * amx_npg_cg_reduce; the solve ends with one amx_npg_cg_xrp: the step's own launch is gone from
+ * every iteration but the last.  Actions are not read. */
+int amx_npg_pass_cg(amx_ctx* ctx, int N, const void* obs, int obs_dtype, long long ldo, const float* theta,
+                    int rows_per_block, double* partials, float* hcache, double tol, double* x, const double* r_in,
+                    double* r_out, const double* p_in, double* p_out, float* p32_out, const double* state_in,
+                    double* state_out, const double* work, void* stream);
 int amx_npg_cg_init(amx_ctx* ctx, int P, const double* b, double* x, double* r, double* p, float* p32,
                     double* state, void* stream);
 /* amx_npg_cg_init + amx_npg_curvature (theta's log_std block -> curv [A]) in one launch. */

@@ -59,6 +59,14 @@ def test_round4_entry_points_validate_without_gpu(lib):
                                None, None) == -1
     assert lib.amx_npg_pass_ex(None, 1, 64, None, 1, 197, None, 1, 36, None, None, None, 32, None, None, None,
                                None) == -1
+    # round 6: the CG tail's two launches separately, and the Fisher-vector pass with the step folded in
+    assert lib.amx_npg_cg_reduce(None, None, 1, 10, 4, None, 0.0, None, None, None, None, None) == -1
+    assert b"amx_npg_cg_reduce" in lib.amx_last_error()
+    assert lib.amx_npg_cg_xrp(None, 10, 0.0, None, None, None, None, None, None, None, None, None) == -1
+    assert b"amx_npg_cg_xrp" in lib.amx_last_error()
+    assert lib.amx_npg_pass_cg(None, 64, None, 1, 197, None, 32, None, None, 0.0, None, None, None, None, None, None,
+                               None, None, None, None) == -1
+    assert b"amx_npg_pass_cg" in lib.amx_last_error()
 
 
 def test_dense_layer_shapes_match_basicmlp():

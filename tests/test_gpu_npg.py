@@ -279,6 +279,60 @@ def test_npg_cg_tail_matches_separate():
         assert np.array_equal(u, v)
 
 
+@pytest.mark.parametrize("iters,stop_at,cache", [(1, None, True), (2, None, False), (10, None, True),
+                                                 (10, 3, True), (4, 1, False)])
+def test_npg_cg_fold_bit_identical(iters, stop_at, cache):
+    """amx_npg_pass_cg (the CG vector step folded into the next Fisher-vector pass, one launch per
+    iteration fewer) against the round-5 form (pass on p32 + amx_npg_cg_tail): the same x bit for
+    bit -- the fold forms v, r'.r' and p' in k_npg_cg_xrp's summation orders -- over 1, 2 and 10
+    iterations, with the theta cache and without it (fp64 observations: the uncached pass), and
+    with the solve stopping at iteration 1 or 3 (residual_tol between two r.r values: the stop
+    found by the fold itself, then carried through the later passes and the final step)."""
+    from amp_extensions_amd.policy import init_mlp_policy_params
+    from amp_extensions_amd.npg import pack_policy, NPG_VPG
+    S, A, N = 197, 36, 3000
+    layers, ls = init_mlp_policy_params(S, A, (32, 32), seed=100, init_log_std=-0.25)
+    npg = make(S, A, pack_policy(layers, ls))
+    npg.cg_iters = iters
+    rs = np.random.RandomState(13)
+    o, a, adv = npg._inputs((0.5 * rs.randn(N, S)).astype(np.float32), rs.randn(N, A).astype(np.float32),
+                            rs.randn(N))
+    hc = None
+    if cache:
+        hc = npg._hcache(N)
+        b = npg._pass(NPG_VPG, o, a, adv, None, hcache=hc).clone()
+    else:
+        o = o.double()
+        b = npg._pass(NPG_VPG, o, a, adv, None).clone()
+
+    def solve(fold, tol):
+        npg.cg_fold, npg.residual_tol = fold, tol
+        x = npg.cg_solve(o, a, b, hcache=hc).clone()
+        torch.cuda.synchronize()
+        return x.cpu().numpy()
+
+    tol = 0.0
+    if stop_at is not None:  # r.r after each step from a numpy CG with the device HVP as f_Ax
+        bn = b.cpu().numpy()
+        x_, r_, p_ = np.zeros_like(bn), bn.copy(), bn.copy()
+        hist = [float(bn @ bn)]
+        for _ in range(stop_at):
+            z = npg.HVP(o, a, p_).cpu().numpy()
+            v = hist[-1] / (p_ @ z)
+            r_ = r_ - v * z
+            nr = float(r_ @ r_)
+            p_ = r_ + nr / hist[-1] * p_
+            hist.append(nr)
+        tol = float(np.sqrt(hist[-1] * hist[-2]))  # reached at step `stop_at`, not before
+    x0 = solve(False, tol)
+    x1 = solve(True, tol)
+    assert np.array_equal(x0, x1), np.abs(x0 - x1).max()
+    assert np.array_equal(x1, solve(True, tol))
+    if stop_at is not None:
+        npg.cg_iters = stop_at
+        assert np.array_equal(x1, solve(False, 0.0))  # the stop took effect after `stop_at` steps
+
+
 def test_npg_pass_input_dtypes_bit_identical():
     """amx_npg_pass on fp64 and fp32 inputs (the fp64 C-ABI path: 16 layer-1 K-steps compiled; the
     fp32 path DeviceNPG takes: ceil(S / 16) rounded to 4 / 8 / 13 / 16) gives the same bits in all
