@@ -508,6 +508,10 @@ def main():
             paths_info.update(paths=len(paths), samples=n)
             return n
 
+    # the in-kernel GEMM timer is registered before the warm-up: graphs captured there (the
+    # sampler's chunk graphs in paths mode) carry its buffer in their GEMM arguments, so their
+    # replays in the timed region are timed too (it is zeroed before the timed region)
+    timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
     for _ in range(args.warmup):
         one_rollout()
     torch.cuda.synchronize()
@@ -528,7 +532,6 @@ def main():
     use_graph = args.mode == "engine" and args.graph == "on"
     if use_graph and args.gemm != "f16x3":
         raise SystemExit("--graph needs the f16x3 GEMM (its in-kernel timer)")
-    timer = ctx.gemm_timer() if args.gemm == "f16x3" else None
     # --overlap on (N > 1, MMD): each rollout's all-reduce overlaps the next rollout's first
     # forward and its relabel runs after that forward; the last relabel is flushed inside the
     # timed region (the first timed rollout also recomputes the warm-up's relabel: one extra
